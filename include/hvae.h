@@ -1,0 +1,276 @@
+/*
+ * hvae.h -- C ABI of libhvae.so, the MI355X (gfx950) HybridVAE train/eval path.
+ *
+ * Conventions (every entry point):
+ *   - all pointers are DEVICE pointers owned by the caller (PyTorch tensors in
+ *     the Python host code), except the small config structs, which live on
+ *     the host and are read during the call;
+ *   - sizes are int64_t; matrices are row-major with an explicit leading
+ *     dimension where it matters;
+ *   - `stream` is a hipStream_t passed as void*; work is enqueued on it and
+ *     the call returns without synchronising;
+ *   - nothing allocates, frees or synchronises, so any sequence of calls can
+ *     be captured into a hipGraph;
+ *   - the return value is HVAE_OK (0) or a negative HVAE_ERR_*; the text of
+ *     the last error of the calling thread is available via hvae_last_error.
+ *
+ * Each entry point names the reference interface it replaces
+ * (/root/reference = Aymane-Nouhail/Recommendation-System).
+ */
+#ifndef HVAE_H_
+#define HVAE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HVAE_ABI_VERSION 1
+
+enum {
+  HVAE_OK = 0,
+  HVAE_ERR_ARG = -1,         /* bad shape / null pointer / inconsistent sizes */
+  HVAE_ERR_HIP = -2,         /* HIP runtime error (launch or API)              */
+  HVAE_ERR_UNSUPPORTED = -3, /* shape or dtype this build has no kernel for    */
+  HVAE_ERR_WORKSPACE = -4    /* workspace smaller than the *_workspace() query */
+};
+
+enum { HVAE_F32 = 0, HVAE_BF16 = 1 };
+
+/* ----------------------------------------------------------------- misc -- */
+int hvae_version(void);
+/* Copies the calling thread's last error text (NUL-terminated) into buf. */
+int hvae_last_error(char* buf, size_t len);
+
+/* ------------------------------------------------------------ data view -- */
+/* A batch of user rows of a CSR interaction matrix (users x items).
+ * Replaces the dense row materialisation of UserInteractionDataset.__getitem__
+ * + DataLoader collate (src/ml/train.py:35-47, 248-259): rows are read
+ * in place from the device-resident CSR, never densified. Values are floats
+ * because _build_matrix sums duplicate (user, item) pairs
+ * (src/ml/train.py:175-182), so an entry can be 2.0 or more. */
+typedef struct hvae_csr_batch {
+  const int64_t* row_ptr; /* [n_rows + 1]                                     */
+  const int32_t* col_idx; /* [nnz] item ids                                   */
+  const float* vals;      /* [nnz] interaction values                         */
+  const int32_t* rows;    /* matrix rows of this batch; NULL => 0..nb-1       */
+  const int64_t* rows_offset; /* device index of the batch's first entry in  */
+                          /* `rows` (NULL => 0): a hipGraph replayed once   */
+                          /* per batch advances it with hvae_counter_add    */
+  int64_t nb;             /* users in the batch                               */
+  int64_t n_items;        /* N                                                */
+} hvae_csr_batch;
+
+/* Dense [B, N] input (the reference's collated batch, also what its unit tests
+ * feed: tests/test_unit.py:167, including negative values) -> CSR of its
+ * nonzeros, row order preserved. row_ptr[B] receives the nnz; entries beyond
+ * `cap` are not written (caller sizes cap >= B*N or checks row_ptr[B]). */
+int hvae_dense_to_csr(const float* x, int64_t B, int64_t N, int64_t* row_ptr, int32_t* col_idx,
+                      float* vals, int64_t cap, void* ws, size_t ws_bytes, void* stream);
+size_t hvae_dense_to_csr_workspace(int64_t B, int64_t N);
+
+/* ------------------------------------------------------------- encoder -- */
+/* First encoder layer over sparse rows, fused with its epilogue:
+ *   a = x W1^T + b1 ; h = Dropout(GELU(LayerNorm(a)))
+ * Replaces nn.Linear(N,H) -> LayerNorm(H) -> GELU() -> Dropout(p) of
+ * HybridVAE._build_encoder / encode (src/ml/model.py:111-119, 149).
+ * w1t is the item-major [N, H] image of encoder.0.weight ([H, N]).
+ * drop_mult: optional [nb, H] explicit dropout multipliers (parity mode);
+ * otherwise Philox(seed, *step_dev, layer) masks. train=0 => no dropout.
+ * xhat_out [nb,H] and rstd_out [nb] are saved for the backward (nullable). */
+int hvae_encoder_fwd(const hvae_csr_batch* x, const float* w1t, const float* b1, const float* ln_w,
+                     const float* ln_b, int64_t H, float p_drop, const float* drop_mult,
+                     uint64_t seed, const int64_t* step_dev, int train, float* h_out,
+                     float* xhat_out, float* rstd_out, void* stream);
+
+/* Same epilogue on a dense pre-activation a [nb, H] (hidden layers >= 2,
+ * src/ml/model.py:111-119). `layer` selects the dropout stream. */
+int hvae_ln_gelu_drop_fwd(const float* a, const float* ln_w, const float* ln_b, int64_t nb,
+                          int64_t H, float p_drop, const float* drop_mult, uint64_t seed,
+                          const int64_t* step_dev, uint32_t layer, int train, float* h_out,
+                          float* xhat_out, float* rstd_out, void* stream);
+
+/* Backward of Dropout(GELU(LayerNorm(a))): dh -> da, and d(ln_w), d(ln_b)
+ * (written, not accumulated). Deterministic column sums through ws. */
+int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const float* rstd,
+                          const float* ln_w, const float* ln_b, int64_t nb, int64_t H,
+                          float p_drop, const float* drop_mult, uint64_t seed,
+                          const int64_t* step_dev, uint32_t layer, int train, float* da,
+                          float* d_ln_w, float* d_ln_b, void* ws, size_t ws_bytes, void* stream);
+size_t hvae_ln_gelu_drop_bwd_workspace(int64_t nb, int64_t H);
+
+/* Row-sparse gradient of the item-major first-layer weight W1t [N, H]:
+ *   dW1t[j, :] = sum_{b : j in row b} x_bj * da[b, :]
+ * (autograd of nn.Linear(N,H) at src/ml/model.py:114 under loss.backward(),
+ * src/ml/train.py:90). Only the items present in the batch get a row; rows
+ * are summed in ascending batch-row order, so the result is bitwise
+ * reproducible. Slots are assigned in ascending item order. */
+typedef struct hvae_rowgrad {
+  int32_t* cnt;         /* [N]   scratch; must be zero on entry, left zero      */
+  int32_t* slot_of;     /* [N]   item -> slot, valid iff slot < *n_unique and   */
+                        /*       item_of[slot] == item                          */
+  int32_t* item_of;     /* [cap] slot -> item (ascending)                       */
+  int32_t* seg_off;     /* [cap + 1]                                            */
+  int32_t* fill;        /* [cap] scratch; must be zero on entry, left zero      */
+  int32_t* contrib_row; /* [cap]                                                */
+  float* contrib_val;   /* [cap]                                                */
+  float* rows;          /* [cap, H] gradient rows                               */
+  int32_t* n_unique;    /* [1] device                                           */
+  int64_t cap;          /* >= nnz of any batch                                  */
+  int64_t n_items;      /* N                                                    */
+} hvae_rowgrad;
+int hvae_w1_rowgrad(const hvae_csr_batch* x, const float* da, int64_t H, const hvae_rowgrad* rg,
+                    void* ws, size_t ws_bytes, void* stream);
+size_t hvae_w1_rowgrad_workspace(int64_t n_items);
+/* Scatter the row-sparse gradient into a dense, caller-zeroed buffer laid out
+ * [N, ld] (item-major; ld >= H). */
+int hvae_rowgrad_to_dense(const hvae_rowgrad* rg, int64_t H, float* dense, int64_t ld, void* stream);
+
+/* ---------------------------------------------------------- dense GEMM -- */
+/* C[M,N] = alpha * op(A)[M,K] * op(B)[K,N] + beta * C, then the epilogue.
+ * op(A) = A ([M,K], lda) or A^T (A stored [K,M]); op(B) = B ([K,N]) or B^T
+ * (B stored [N,K], i.e. an nn.Linear weight). fp32 in, fp32 out, on the
+ * exact-f32 MFMA (v_mfma_f32_16x16x4_f32). Replaces the addmm / mm of every
+ * small nn.Linear on the path and its autograd: fc_mu/fc_logvar
+ * (src/ml/model.py:126-127,152-153), the projection MLP (:90-95,195), the
+ * deeper encoder layers (:114), and the materialised scores u E^T (:198). */
+enum {
+  HVAE_EPI_NONE = 0,
+  HVAE_EPI_BIAS = 1,           /* + bias[n]                                        */
+  HVAE_EPI_BIAS_GELU_DROP = 2, /* pre = acc + bias -> pre_out; C = Drop(GELU(pre)) */
+  HVAE_EPI_GELU_DROP_BWD = 3,  /* C = acc * dropmult * GELU'(pre_in)               */
+  HVAE_EPI_DROP_BWD = 4        /* C = acc * dropmult                               */
+};
+typedef struct hvae_epilogue {
+  int kind;
+  const float* bias;      /* [N]                                                   */
+  float* pre_out;         /* [M, ldc] (BIAS_GELU_DROP)                             */
+  const float* pre_in;    /* [M, ldc] (GELU_DROP_BWD)                              */
+  float p_drop;           /* dropout probability                                   */
+  const float* drop_mult; /* [M, N] explicit multipliers (parity mode) or NULL     */
+  uint64_t seed;
+  const int64_t* step_dev;
+  uint32_t tag;           /* Philox stream tag (see hvae_common.h)                 */
+  int train;              /* 0 => dropout is identity                              */
+} hvae_epilogue;
+int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
+                  const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
+                  int64_t ldc, const hvae_epilogue* epi, void* ws, size_t ws_bytes, void* stream);
+size_t hvae_gemm_f32_workspace(int64_t M, int64_t N, int64_t K);
+
+/* out[n] = beta * out[n] + sum_m X[m, n]  (bias gradients; deterministic) */
+int hvae_colsum(const float* X, int64_t M, int64_t N, int64_t ldx, float beta, float* out,
+                void* ws, size_t ws_bytes, void* stream);
+size_t hvae_colsum_workspace(int64_t M, int64_t N);
+
+/* ------------------------------------------------------ latent (K5, K9) -- */
+/* z = mu + eps * exp(0.5 logvar) (train) or z = mu (eval), and the per-row KL
+ * term kl_rows[b] = -0.5 * sum_l (1 + lv - mu^2 - exp(lv)).
+ * Replaces HybridVAE.reparameterize (src/ml/model.py:157-179) and the KL line
+ * of vae_loss_function (src/ml/model.py:287). eps_in: explicit noise [nb,L]
+ * (parity mode) or NULL for Philox normals; eps_out saves it (nullable). */
+int hvae_reparam_kl_fwd(const float* mu, const float* logvar, int64_t ld, int64_t nb, int64_t L,
+                        int train, const float* eps_in, uint64_t seed, const int64_t* step_dev,
+                        float* z, float* eps_out, float* kl_rows, void* stream);
+/* dmu = dz + kl_scale * mu ; dlv = dz * eps * 0.5 exp(0.5 lv) + kl_scale * 0.5 (exp(lv) - 1)
+ * with kl_scale = beta / nb (dz may be NULL: KL-only gradient). */
+int hvae_reparam_kl_bwd(const float* dz, const float* mu, const float* logvar, int64_t ld,
+                        const float* eps, int64_t nb, int64_t L, float kl_scale, int train,
+                        float* dmu, float* dlogvar, int64_t ld_out, void* stream);
+
+/* -------------------------------------------------- decoder (K7, K8, K10) -- */
+/* Streaming decoder over all N items, scores never stored:
+ *   lse[b] = log sum_i exp(u_b . E_i)         (multinomial normaliser)
+ *   O[b,:] = sum_i softmax(u_b E^T)_i E_i     (what d(u) needs; O may be NULL)
+ * i.e. one flash-attention style pass with Q = U, K = V = E (E frozen, so no dE).
+ * Replaces torch.matmul(u, E.t()) (src/ml/model.py:198), F.log_softmax
+ * (src/ml/model.py:281) and their autograd. dtype HVAE_BF16: E is a bf16 copy,
+ * U is rounded to bf16, MFMA 32x32x16 bf16 with f32 accumulation, and
+ * e_maxnorm (device scalar, hvae_row_norm_max) bounds the scores; HVAE_F32:
+ * exact-f32 MFMA (e_maxnorm unused). ws >= hvae_decoder_workspace() bytes. */
+int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
+                     int64_t nb, int64_t N, int64_t D, float* lse, float* O, void* ws,
+                     size_t ws_bytes, void* stream);
+size_t hvae_decoder_workspace(int dtype, int64_t nb, int64_t N, int64_t D);
+/* 1 if this build has a streaming decoder kernel for (dtype, D). */
+int hvae_decoder_supported(int dtype, int64_t D);
+/* *out = max_i ||E_i||_2 of an fp32 / bf16 [N, D] matrix (computed once: E is frozen). */
+int hvae_row_norm_max(int dtype, const void* E, int64_t N, int64_t D, float* out, void* stream);
+/* Sparse half of the loss and of d(u), in fp32 against the fp32 E:
+ *   recon_rows[b] = n_b * lse[b] - sum_{j in row b} x_bj (u_b . E_j),  n_b = sum_j x_bj
+ *   dU[b,:]       = grad_scale * (n_b * O[b,:] - sum_{j in row b} x_bj E_j)
+ * (dU / O may be NULL for a loss-only pass, e.g. VAETrainer.validate). */
+int hvae_decoder_bwd(const hvae_csr_batch* x, const float* U, int64_t ldu, const float* E32,
+                     int64_t D, const float* lse, const float* O, float grad_scale,
+                     float* recon_rows, float* dU, void* stream);
+
+/* Materialised-score form of the multinomial loss (the module API path where
+ * forward() returns the [nb, N] scores, src/ml/model.py:202-221, 281):
+ *   lse[b] = logsumexp(S[b,:]); recon_rows[b] = sum_i X[b,i] * (lse[b] - S[b,i])
+ *   dS[b,i] = scale * (n_b * softmax(S[b,:])_i - X[b,i]),  n_b = sum_i X[b,i]  */
+int hvae_nll_rows_fwd(const float* S, int64_t lds, const float* X, int64_t ldx, int64_t nb,
+                      int64_t N, float* lse, float* recon_rows, void* stream);
+int hvae_nll_rows_bwd(const float* S, int64_t lds, const float* X, int64_t ldx, const float* lse,
+                      int64_t nb, int64_t N, float scale, float* dS, int64_t ldd, void* stream);
+
+/* total = mean(recon_rows) + beta * mean(kl_rows) -> out3 = {total, recon, kl};
+ * accum3 (nullable, fp64) += out3: the epoch sums of VAETrainer.train_epoch
+ * (src/ml/train.py:94-96) without a host sync per batch. */
+int hvae_loss_finalize(const float* recon_rows, const float* kl_rows, int64_t nb, float beta,
+                       float* out3, double* accum3, void* stream);
+
+/* ------------------------------------------------- optimiser (K13, K14) -- */
+/* Global L2 norm over a dense flat gradient and an optional row-sparse one,
+ * then coef = min(1, max_norm / (norm + 1e-6)):
+ * torch.nn.utils.clip_grad_norm_(params, 5.0) at src/ml/train.py:91. The
+ * multiplier is applied inside the Adam launches (no extra pass). */
+int hvae_clip_grad_norm(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg, int64_t H,
+                        float max_norm, float* norm_out, float* coef_out, void* ws,
+                        size_t ws_bytes, void* stream);
+size_t hvae_clip_grad_norm_workspace(int64_t n_dense, int64_t cap, int64_t H);
+
+/* torch.optim.Adam (src/ml/train.py:63, 92; single-tensor semantics):
+ *   g = coef * grad (+ wd * p); m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2
+ *   p -= lr / (1 - b1^t) * m / (sqrt(v) / sqrt(1 - b2^t) + eps)
+ * with t = *step_dev + 1 (the caller advances step_dev afterwards). */
+typedef struct hvae_adam {
+  double lr, beta1, beta2, eps, weight_decay; /* Python-float values, as torch */
+  const int64_t* step_dev; /* completed optimizer steps                        */
+  const float* coef_dev;   /* clip multiplier or NULL (=> 1)                    */
+} hvae_adam;
+int hvae_adam_dense(const hvae_adam* cfg, float* p, float* m, float* v, const float* g, int64_t n,
+                    void* stream);
+/* Dense Adam over the item-major W1t [N, H] whose gradient is row-sparse:
+ * untouched rows get g = 0 (their moments still decay, as in torch). */
+int hvae_adam_rows(const hvae_adam* cfg, float* p, float* m, float* v, const hvae_rowgrad* rg,
+                   int64_t N, int64_t H, void* stream);
+/* *counter += delta (device-side step/batch counters for graph replay). */
+int hvae_counter_add(int64_t* counter, int64_t delta, void* stream);
+
+/* ------------------------------------------------------------ eval (K16) -- */
+/* scores[r, c] = U[user_row[r], :] . E32[cand[r, c], :]   (fp32)
+ * The 99-negative protocol of RecommendationEvaluator.evaluate_user_with_negatives
+ * (src/ml/evaluate.py:149-185), batched over test rows. */
+int hvae_score_candidates(const float* U, int64_t ldu, const int32_t* user_row, const float* E32,
+                          int64_t D, const int32_t* cand, int64_t R, int64_t C, float* scores,
+                          void* stream);
+/* rank[r] = #{c : scores[r,c] > scores[r,0]} + #{c > 0 : scores[r,c] == scores[r,0]}
+ * i.e. the position of candidate 0 in a stable descending-then-reversed order
+ * (candidates[np.argsort(s)[::-1]] with argsort stable). */
+int hvae_rank_first(const float* scores, int64_t R, int64_t C, int32_t* rank, void* stream);
+/* Exact top-K per row of a score matrix [R, N] (ld), seen items of row r
+ * (exclude, nullable) masked to -inf first, in place in `scores` (get_user_recommendations,
+ * src/ml/evaluate.py:137-147; HybridVAE.recommend, src/ml/model.py:236-256).
+ * Order: score descending, ties by larger item index first. K <= 64. */
+int hvae_topk(const float* scores, int64_t R, int64_t N, int64_t ld, const hvae_csr_batch* exclude,
+              int64_t K, int32_t* idx, float* val, void* stream);
+
+/* fp32 -> bf16 (round to nearest even) copy of the frozen embeddings. */
+int hvae_cast_bf16(const float* x, void* y, int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HVAE_H_ */

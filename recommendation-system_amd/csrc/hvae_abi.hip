@@ -1,0 +1,66 @@
+// hvae_abi.hip -- version / error plumbing of the C ABI and small utility launchers.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "hvae_common.h"
+
+namespace hvae {
+
+static thread_local char g_last_error[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+}
+
+__global__ void k_counter_add(int64_t* c, int64_t d) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *c += d;
+}
+
+__global__ void k_cast_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
+    if (i + 3 < n) {
+      const float4 v = *reinterpret_cast<const float4*>(x + i);
+      ushort4 o;
+      o.x = f2bf(v.x); o.y = f2bf(v.y); o.z = f2bf(v.z); o.w = f2bf(v.w);
+      *reinterpret_cast<ushort4*>(y + i) = o;
+    } else {
+      for (int64_t j = i; j < n; ++j) y[j] = f2bf(x[j]);
+    }
+  }
+}
+
+}  // namespace hvae
+
+using namespace hvae;
+
+extern "C" int hvae_version(void) { return HVAE_ABI_VERSION; }
+
+extern "C" int hvae_last_error(char* buf, size_t len) {
+  if (!buf || len == 0) return HVAE_ERR_ARG;
+  strncpy(buf, g_last_error, len - 1);
+  buf[len - 1] = '\0';
+  return HVAE_OK;
+}
+
+extern "C" int hvae_counter_add(int64_t* counter, int64_t delta, void* stream) {
+  HVAE_REQUIRE(counter, "hvae_counter_add: null counter");
+  k_counter_add<<<1, 64, 0, as_stream(stream)>>>(counter, delta);
+  HVAE_LAUNCH_CHECK("k_counter_add");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_cast_bf16(const float* x, void* y, int64_t n, void* stream) {
+  HVAE_REQUIRE(n >= 0 && (n == 0 || (x && y)), "hvae_cast_bf16: bad args");
+  HVAE_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)y % 8) == 0,
+               "hvae_cast_bf16: x must be 16-B and y 8-B aligned");
+  if (n == 0) return HVAE_OK;
+  const int64_t blocks = std::min<int64_t>(cdiv(n, 256 * 4), 4096);
+  k_cast_bf16<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(x, (bf16_t*)y, n);
+  HVAE_LAUNCH_CHECK("k_cast_bf16");
+  return HVAE_OK;
+}

@@ -1,0 +1,176 @@
+// hvae_common.h -- shared device/host helpers for libhvae (gfx950 / CDNA4 only).
+//
+// Everything here is written for 64-lane wavefronts (wave = 64 on gfx950) and
+// for the launch conventions of the C-ABI in include/hvae.h: raw device
+// pointers owned by the caller, a hipStream_t passed as void*, no allocation
+// and no host synchronisation inside any launcher (so every launcher can be
+// captured into a hipGraph).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+#include <math.h>
+
+#include "../../include/hvae.h"
+
+namespace hvae {
+
+// ---------------------------------------------------------------- errors ---
+// Thread-local last-error text, returned by hvae_last_error().
+void set_error(const char* fmt, ...);
+
+#define HVAE_FAIL(code, ...)                                                   \
+  do {                                                                         \
+    ::hvae::set_error(__VA_ARGS__);                                            \
+    return (code);                                                             \
+  } while (0)
+
+#define HVAE_REQUIRE(cond, ...)                                                \
+  do {                                                                         \
+    if (!(cond)) HVAE_FAIL(HVAE_ERR_ARG, __VA_ARGS__);                         \
+  } while (0)
+
+#define HVAE_HIP(call)                                                         \
+  do {                                                                         \
+    hipError_t e_ = (call);                                                    \
+    if (e_ != hipSuccess)                                                      \
+      HVAE_FAIL(HVAE_ERR_HIP, "%s failed: %s (%s:%d)", #call,                  \
+                hipGetErrorString(e_), __FILE__, __LINE__);                    \
+  } while (0)
+
+// After a <<<>>> launch: surface launch-configuration errors immediately.
+#define HVAE_LAUNCH_CHECK(name)                                                \
+  do {                                                                         \
+    hipError_t e_ = hipGetLastError();                                         \
+    if (e_ != hipSuccess)                                                      \
+      HVAE_FAIL(HVAE_ERR_HIP, "launch of %s failed: %s", name,                 \
+                hipGetErrorString(e_));                                        \
+  } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// --------------------------------------------------------------- device ----
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` must hold NT/64
+// floats. Result valid in every thread.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  return t;
+}
+
+// Exact (erf) GELU, as torch.nn.GELU() default (approximate='none').
+__device__ __forceinline__ float gelu_f(float x) {
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+// d/dx GELU(x) = Phi(x) + x * phi(x)
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+  const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+// ------------------------------------------------------ Philox4x32-10 ------
+// Counter-based RNG: every random value is a pure function of
+// (seed, step, stream tag, element index), so dropout masks and reparameter-
+// isation noise can be regenerated in the backward pass instead of stored, and
+// a hipGraph replay advances them through the device-side step counter.
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Stream tags (the 4th counter word) so that independent draws never collide.
+enum : uint32_t {
+  kTagEncDrop = 0x100u,   // + hidden layer index
+  kTagProjDrop = 0x200u,
+  kTagEps = 0x300u,
+};
+
+__device__ __forceinline__ uint32_t rng_u32(uint64_t seed, int64_t step, uint32_t tag, uint64_t idx) {
+  const u32x4 c{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)step, tag};
+  return philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32)).x;
+}
+// uniform in [0, 1) with 24 random bits
+__device__ __forceinline__ float u01(uint32_t r) { return (float)(r >> 8) * (1.0f / 16777216.0f); }
+
+// Dropout multiplier: 0 or 1/(1-p) (torch semantics: keep with prob 1-p and
+// scale the survivors). External masks (parity mode) override the RNG.
+__device__ __forceinline__ float dropout_mult(float p, float scale, const float* ext, uint64_t i,
+                                           uint64_t seed, int64_t step, uint32_t tag) {
+  if (ext) return ext[i];
+  if (p <= 0.f) return 1.f;
+  if (p >= 1.f) return 0.f;
+  return (u01(rng_u32(seed, step, tag, i)) >= p) ? scale : 0.f;
+}
+
+// Standard normal via Box-Muller from one Philox call.
+__device__ __forceinline__ float normal_f(uint64_t seed, int64_t step, uint32_t tag, uint64_t idx) {
+  const u32x4 c{(uint32_t)idx, (uint32_t)(idx >> 32), (uint32_t)step, tag};
+  const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float a = ((float)(r.x >> 8) + 1.0f) * (1.0f / 16777216.0f);  // (0, 1]
+  const float b = (float)(r.y >> 8) * (1.0f / 16777216.0f);
+  return sqrtf(-2.0f * logf(a)) * cospif(2.0f * b);
+}
+
+// Matrix row of batch entry b (hvae_csr_batch.rows / rows_offset).
+__device__ __forceinline__ int64_t batch_row(const int32_t* rows, const int64_t* rows_offset, int64_t b) {
+  return rows ? (int64_t)rows[(rows_offset ? *rows_offset : 0) + b] : b;
+}
+
+__device__ __forceinline__ int64_t load_step(const int64_t* step_dev) {
+  return step_dev ? *step_dev : 0;
+}
+
+// ------------------------------------------------------------ bf16 ---------
+typedef unsigned short bf16_t;
+// round-to-nearest-even (inputs here are finite activations/embeddings)
+__device__ __host__ __forceinline__ bf16_t f2bf(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+__device__ __host__ __forceinline__ float bf2f(bf16_t h) {
+  uint32_t u = ((uint32_t)h) << 16;
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}
+
+}  // namespace hvae

@@ -1,0 +1,774 @@
+// hvae_decoder.hip -- the frozen-embedding decoder fused with the multinomial
+// loss and its backward (K7, K8, K10 of SURVEY §2.1).
+//
+// Reference: HybridVAE.decode (src/ml/model.py:181-200) computes the full
+// [B, N] scores u E^T; vae_loss_function (src/ml/model.py:281) takes
+// log_softmax over items; autograd then forms d(u) = dS E. Because E is a
+// frozen buffer (model.py:72-73) only d(u) is needed, and
+//   d(u_b) = (1/B) (n_b * sum_i softmax(s_b)_i E_i - sum_{i in row b} x_bi E_i)
+// so the dense part is exactly the output of an attention forward with
+// Q = U, K = V = E. One streaming pass over E produces lse_b and
+// O_b = softmax(s_b) E: 4 * B * N * D FLOPs, scores never leave registers.
+//
+// Layout / schedule (bf16 kernel, D <= 384):
+//   * 4 waves x 32 users per workgroup; U fragments of the wave's 32 users
+//     stay in VGPRs for the whole sweep; the O accumulator (D x 32 fp32)
+//     too (192 VGPRs at D = 384) -> one wave per SIMD;
+//   * items stream through LDS in tiles of 32 rows, double buffered,
+//     register-staged; the LDS image is cut into 128-column segments of
+//     [32 rows][256 B] with the chunk XOR swizzle (row&3)<<2 | (row>>2)&3,
+//     which makes both the row reads of GEMM1 (ds_read_b128) and the
+//     transposed reads of GEMM2 (ds_read_b64_tr_b16) bank-conflict free;
+//   * "swapped" GEMM1 S^T = E_tile U^T puts one user per lane column, so the
+//     per-user max/sum are in-lane + one lane^32 exchange, and the S^T
+//     accumulator is directly the B operand of GEMM2 O^T += E_tile^T P^T
+//     (k order permuted to the accumulator's row order);
+//   * online softmax with a deferred rescale (only when a user's max grows
+//     by more than kThr);
+//   * the item axis is split over workgroups (flash-decoding); splits are a
+//     multiple of 8 so all user blocks of one split share an XCD (blocks b
+//     and b+8 share one), keeping the split's E slice L2-resident; a merge
+//     kernel combines the (m, l, O) partials.
+#include <algorithm>
+
+#include "hvae_common.h"
+
+namespace hvae {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+// Deferred-rescale threshold (natural-log units): O and l are rescaled only
+// when a user's running max grows by more than kThr, so P = exp(s - m) stays
+// <= e^kThr (bf16/fp32 range is ample; N * e^kThr << FLT_MAX for N <= 2^31).
+constexpr float kThr = 20.0f;
+// bf16 kernel: fixed offset within kOffsetSpan of the score bound; a user whose
+// real max is more than kUnderflowSpan below its offset is recomputed exactly.
+constexpr float kOffsetSpan = 60.0f;
+constexpr float kUnderflowSpan = 70.0f;
+
+struct DecOut {
+  int* flag;    // [nb] set when a user's result must be recomputed exactly (bf16 path)
+  float* m;     // [splits][nb] running max      (partial mode)
+  float* l;     // [splits][nb] sum exp(s - m)   (partial mode)
+  float* O;     // [splits][nb][D] partial O, or final O [nb][D] (direct mode)
+  float* lse;   // [nb] (direct mode)
+  int direct;
+};
+
+// ------------------------------------------------------------------ bf16 ---
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// two fp32 -> one packed bf16 pair (v_cvt_pk_bf16_f32, round to nearest even)
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+constexpr int kBfTI = 32;          // items per tile
+constexpr int kBfUsersPerWave = 32;
+constexpr int kBfUsersPerBlock = 128;
+
+__device__ __forceinline__ int bf_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// byte offset of 16-B chunk `chunk` (0 .. D/8-1) of tile row `row` (0..31)
+__device__ __forceinline__ int bf_off(int row, int chunk) {
+  return ((chunk >> 4) << 13) + (row << 8) + (((chunk & 15) ^ bf_swz(row)) << 4);
+}
+
+template <int D>
+constexpr int bf_tile_bytes() { return ((D + 127) / 128) * 8192; }
+
+template <int D, bool WITH_O>
+__global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, int64_t ldu,
+                                                  const bf16_t* __restrict__ E,
+                                                  const float* __restrict__ e_maxnorm, int64_t nb,
+                                                  int64_t N, int splits, int64_t tiles_per_split,
+                                                  DecOut out) {
+  static_assert(D % 32 == 0, "D must be a multiple of 32");
+  constexpr int KS = D / 16;              // GEMM1 k-steps (even)
+  constexpr int DB = D / 32;              // GEMM2 d-blocks
+  constexpr int CH = D / 8;               // 16-B chunks per row
+  constexpr int NSEG = (D + 127) / 128;
+  constexpr int TB = bf_tile_bytes<D>();  // NSEG * 8 KiB
+  constexpr int PIECES_PER_WAVE = NSEG * 2;  // 1-KiB LDS-DMA pieces per wave per tile
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int split = blockIdx.x % splits;
+  const int64_t ub = blockIdx.x / splits;
+  const int64_t u0 = ub * kBfUsersPerBlock + w * kBfUsersPerWave;
+  const int64_t user = u0 + col;
+  const bool wave_active = u0 < nb;
+  const int64_t ntiles = (N + kBfTI - 1) / kBfTI;
+  const int64_t t_beg = (int64_t)split * tiles_per_split;
+  const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
+
+  // U fragments (B operand of GEMM1): lane holds U[user][16 ks + 8 h + j],
+  // packed bf16 pairs (4 VGPRs per k-step).
+  uint4 uf[KS];
+  float usq = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (user < nb) {
+      a = *reinterpret_cast<const float4*>(U + user * ldu + 16 * ks + 8 * h);
+      b = *reinterpret_cast<const float4*>(U + user * ldu + 16 * ks + 8 * h + 4);
+    }
+    usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+    uf[ks] = make_uint4(pack_bf16x2(a.x, a.y), pack_bf16x2(a.z, a.w), pack_bf16x2(b.x, b.y),
+                        pack_bf16x2(b.z, b.w));
+  }
+  usq += __shfl_xor(usq, 32, 64);
+  // Upper bound of every score of this user (bf16 rounding margin included).
+  const float bound = sqrtf(usq) * (*e_maxnorm) * 1.02f;
+
+  f32x16 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m = -INFINITY, lsum = 0.f, mtrue = -INFINITY;
+
+  // E tile -> LDS by LDS-DMA (global_load_lds_dwordx4). The destination of a
+  // wave-instruction is 1 KiB contiguous (base + 16 lane), so the XOR swizzle
+  // is applied to the per-lane SOURCE: LDS slot -> (row, chunk) -> E address.
+  // Tail rows (item >= N) re-read row N-1; their scores are masked to -inf.
+  auto issue_tile = [&](int64_t t, unsigned char* buf) {
+#pragma unroll
+    for (int i = 0; i < PIECES_PER_WAVE; ++i) {
+      const int piece = w * PIECES_PER_WAVE + i;
+      const int o_b = piece * 1024 + lane * 16;  // byte offset in the tile image
+      const int seg = o_b >> 13, row = (o_b >> 8) & 31, slot = (o_b >> 4) & 15;
+      const int gc = seg * 16 + (slot ^ bf_swz(row));
+      int64_t item = t * kBfTI + row;
+      item = item < N ? item : N - 1;
+      const bf16_t* src = E + item * D + (gc < CH ? gc : 0) * 8;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(buf + piece * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  if (t_beg < t_end) {
+    issue_tile(t_beg, lds);
+    __syncthreads();  // vmcnt(0) + barrier: tile t_beg has landed
+  }
+  int cur = 0;
+  for (int64_t t = t_beg; t < t_end; ++t) {
+    if (t + 1 < t_end) issue_tile(t + 1, lds + (cur ^ 1) * TB);
+    const unsigned char* buf = lds + cur * TB;
+    if (wave_active) {
+      // ---- GEMM1: S^T[32 items][32 users] = E_tile U^T, A reads one group ahead
+      f32x16 s;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[r] = 0.f;
+      auto rdA = [&](int ks) {
+        return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(buf + bf_off(col, 2 * ks + h)));
+      };
+      bf16x8 an0 = rdA(0), an1 = rdA(1);
+#pragma unroll
+      for (int g = 0; g < KS / 2; ++g) {
+        const bf16x8 ac0 = an0, ac1 = an1;
+        if (g + 1 < KS / 2) { an0 = rdA(2 * g + 2); an1 = rdA(2 * g + 3); }
+        __builtin_amdgcn_sched_barrier(0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ac0, __builtin_bit_cast(bf16x8, uf[2 * g]), s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ac1, __builtin_bit_cast(bf16x8, uf[2 * g + 1]), s, 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- mask the tail, online softmax with deferred rescale
+      const int64_t ib = t * kBfTI + 4 * h;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t item = ib + (r & 3) + 8 * (r >> 2);
+        if (item >= N) s[r] = -INFINITY;
+        mx = fmaxf(mx, s[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      // Fixed per-user offset, set once: m >= bound - kOffsetSpan means every
+      // later p = exp(s - m) <= e^kOffsetSpan (no overflow, so no rescale of
+      // the AGPR-resident O accumulator is ever needed); m >= first-tile max
+      // keeps the large terms normal. mtrue tracks the real max for the
+      // underflow check done at the end (fixed up by k_dec_fixup).
+      if (t == t_beg) m = fmaxf(mx, bound - kOffsetSpan);
+      mtrue = fmaxf(mtrue, mx);
+      float pv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        pv[r] = __expf(s[r] - m);
+        lsum += pv[r];
+      }
+      bf16x8 pf[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        pf[s2] = __builtin_bit_cast(bf16x8, make_uint4(pack_bf16x2(pv[8 * s2 + 0], pv[8 * s2 + 1]),
+                                                       pack_bf16x2(pv[8 * s2 + 2], pv[8 * s2 + 3]),
+                                                       pack_bf16x2(pv[8 * s2 + 4], pv[8 * s2 + 5]),
+                                                       pack_bf16x2(pv[8 * s2 + 6], pv[8 * s2 + 7])));
+      if (WITH_O) {
+        // ---- GEMM2: O^T[D][32 users] += E_tile^T P^T, transposed LDS reads
+        const int g = (lane >> 4) & 1, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+        auto rdT = [&](int d, int row) {
+          const int chunk = 4 * d + 2 * g + (pp >> 1);
+          auto* p = (__attribute__((address_space(3))) s16x4*)(void*)(buf + bf_off(row, chunk) + 8 * (pp & 1));
+          return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+        };
+        s16x4 n00 = rdT(0, 4 * h + q), n01 = rdT(0, 8 + 4 * h + q);
+        s16x4 n10 = rdT(0, 16 + 4 * h + q), n11 = rdT(0, 24 + 4 * h + q);
+#pragma unroll
+        for (int d = 0; d < (WITH_O ? DB : 1); ++d) {
+          const s16x4 c00 = n00, c01 = n01, c10 = n10, c11 = n11;
+          if (d + 1 < DB) {
+            n00 = rdT(d + 1, 4 * h + q); n01 = rdT(d + 1, 8 + 4 * h + q);
+            n10 = rdT(d + 1, 16 + 4 * h + q); n11 = rdT(d + 1, 24 + 4 * h + q);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          const s16x8 a0 = {c00[0], c00[1], c00[2], c00[3], c01[0], c01[1], c01[2], c01[3]};
+          const s16x8 a1 = {c10[0], c10[1], c10[2], c10[3], c11[0], c11[1], c11[2], c11[3]};
+          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a0), pf[0], o[d], 0, 0, 0);
+          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a1), pf[1], o[d], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    __syncthreads();  // next tile landed (vmcnt(0)), this tile's reads done
+    cur ^= 1;
+  }
+
+  if (!wave_active) return;
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  if (user >= nb) return;
+  // the max term itself may have lost precision: exact recompute by k_dec_fixup
+  if (h == 0 && t_beg < t_end && !(mtrue >= m - kUnderflowSpan && ltot > 0.f)) out.flag[user] = 1;
+  if (out.direct) {
+    const float inv = 1.0f / ltot;
+    if (h == 0) out.lse[user] = m + logf(ltot);
+    if (WITH_O) {
+#pragma unroll
+      for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int dd = 32 * d + 8 * g4 + 4 * h;
+          *reinterpret_cast<float4*>(out.O + user * D + dd) =
+              make_float4(o[d][4 * g4] * inv, o[d][4 * g4 + 1] * inv, o[d][4 * g4 + 2] * inv, o[d][4 * g4 + 3] * inv);
+        }
+    }
+  } else {
+    const int64_t pi = (int64_t)split * nb + user;
+    if (h == 0) { out.m[pi] = m; out.l[pi] = ltot; }
+    if (WITH_O) {
+#pragma unroll
+      for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int dd = 32 * d + 8 * g4 + 4 * h;
+          *reinterpret_cast<float4*>(out.O + pi * D + dd) =
+              make_float4(o[d][4 * g4], o[d][4 * g4 + 1], o[d][4 * g4 + 2], o[d][4 * g4 + 3]);
+        }
+    }
+  }
+}
+
+// ------------------------------------------------------------------- f32 ---
+// Same algorithm on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 sums):
+// 4 waves x 16 users, 16-item tiles, LDS rows padded to D+2 floats
+// (conflict-free GEMM1 reads, 2-way on half of the GEMM2 reads).
+constexpr int kF32TI = 16;
+constexpr int kF32UsersPerWave = 16;
+constexpr int kF32UsersPerBlock = 64;
+
+template <int D>
+constexpr int f32_tile_bytes() { return kF32TI * (D + 2) * 4; }
+
+template <int D, bool WITH_O>
+__global__ void __launch_bounds__(256) k_dec_f32(const float* __restrict__ U, int64_t ldu,
+                                                 const float* __restrict__ E, int64_t nb, int64_t N,
+                                                 int splits, int64_t tiles_per_split, DecOut out) {
+  static_assert(D % 16 == 0, "D must be a multiple of 16");
+  constexpr int KS = D / 4;
+  constexpr int DB = D / 16;
+  constexpr int LD = D + 2;
+  constexpr int TF = kF32TI * LD;           // floats per tile buffer
+  constexpr int Q4 = D / 4;                 // float4 per row
+  constexpr int LPT = (kF32TI * Q4 + 255) / 256;
+  extern __shared__ __attribute__((aligned(16))) float ldsf[];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, q = lane >> 4, c16 = lane & 15;
+  const int split = blockIdx.x % splits;
+  const int64_t ub = blockIdx.x / splits;
+  const int64_t u0 = ub * kF32UsersPerBlock + w * kF32UsersPerWave;
+  const int64_t user = u0 + c16;
+  const bool wave_active = u0 < nb;
+  const int64_t ntiles = (N + kF32TI - 1) / kF32TI;
+  const int64_t t_beg = (int64_t)split * tiles_per_split;
+  const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
+
+  float uf[KS];  // B operand of GEMM1: U[user][4 ks + q]
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) uf[ks] = (user < nb) ? U[user * ldu + 4 * ks + q] : 0.f;
+
+  f32x4 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, lsum = 0.f;
+
+  float4 stage[LPT];
+  auto gload = [&](int64_t t) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c / Q4, c4 = c % Q4;
+      const int64_t item = t * kF32TI + row;
+      stage[i] = (c < kF32TI * Q4 && item < N) ? *reinterpret_cast<const float4*>(E + item * D + 4 * c4)
+                                               : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto lstore = [&](float* buf) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i;
+      if (c < kF32TI * Q4) {
+        const int row = c / Q4, c4 = c % Q4;
+        float* dst = buf + row * LD + 4 * c4;  // LD is even: 8-B aligned pairs
+        dst[0] = stage[i].x; dst[1] = stage[i].y; dst[2] = stage[i].z; dst[3] = stage[i].w;
+      }
+    }
+  };
+
+  if (t_beg < t_end) {
+    gload(t_beg);
+    lstore(ldsf);
+    __syncthreads();
+  }
+  int cur = 0;
+  for (int64_t t = t_beg; t < t_end; ++t) {
+    const bool more = t + 1 < t_end;
+    if (more) gload(t + 1);
+    const float* buf = ldsf + cur * TF;
+    if (wave_active) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        s = __builtin_amdgcn_mfma_f32_16x16x4f32(buf[c16 * LD + 4 * ks + q], uf[ks], s, 0, 0, 0);
+      // S^T: row = item 4q + r, col = user c16
+      const int64_t ib = t * kF32TI + 4 * q;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (ib + r >= N) s[r] = -INFINITY;
+        mx = fmaxf(mx, s[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (__any(mx > m + kThr)) {
+        const float mn = fmaxf(m, mx);
+        const float alpha = __expf(m - mn);
+        lsum *= alpha;
+        if (WITH_O) {
+#pragma unroll
+          for (int d = 0; d < (WITH_O ? DB : 1); ++d) o[d] *= alpha;
+        }
+        m = mn;
+      }
+      float p[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        p[r] = __expf(s[r] - m);
+        lsum += p[r];
+      }
+      if (WITH_O) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+            o[d] = __builtin_amdgcn_mfma_f32_16x16x4f32(buf[(4 * q + r) * LD + 16 * d + c16], p[r], o[d], 0, 0, 0);
+      }
+    }
+    if (more) lstore(ldsf + (cur ^ 1) * TF);
+    __syncthreads();
+    cur ^= 1;
+  }
+
+  if (!wave_active) return;
+  float ltot = lsum + __shfl_xor(lsum, 16, 64);
+  ltot += __shfl_xor(ltot, 32, 64);
+  if (user >= nb) return;
+  // O^T block d: lane holds d-rows 16 d + 4 q + r for user c16
+  if (out.direct) {
+    const float inv = 1.0f / ltot;
+    if (q == 0) out.lse[user] = m + logf(ltot);
+    if (WITH_O) {
+#pragma unroll
+      for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+        *reinterpret_cast<float4*>(out.O + user * D + 16 * d + 4 * q) =
+            make_float4(o[d][0] * inv, o[d][1] * inv, o[d][2] * inv, o[d][3] * inv);
+    }
+  } else {
+    const int64_t pi = (int64_t)split * nb + user;
+    if (q == 0) { out.m[pi] = m; out.l[pi] = ltot; }
+    if (WITH_O) {
+#pragma unroll
+      for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+        *reinterpret_cast<float4*>(out.O + pi * D + 16 * d + 4 * q) = make_float4(o[d][0], o[d][1], o[d][2], o[d][3]);
+    }
+  }
+}
+
+// Combine the per-split (m, l, O) partials: one wave per user.
+__global__ void __launch_bounds__(256) k_dec_merge(const float* __restrict__ pm, const float* __restrict__ pl,
+                                                   const float* __restrict__ pO, int splits, int64_t nb,
+                                                   int64_t D, float* __restrict__ lse, float* __restrict__ O) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  float M = -INFINITY;
+  for (int s = lane; s < splits; s += 64) M = fmaxf(M, pm[(int64_t)s * nb + b]);
+  M = wave_max(M);
+  float L = 0.f;
+  for (int s = lane; s < splits; s += 64) {
+    const float ms = pm[(int64_t)s * nb + b];
+    L += (ms == -INFINITY) ? 0.f : pl[(int64_t)s * nb + b] * __expf(ms - M);
+  }
+  L = wave_sum(L);
+  if (lane == 0) lse[b] = M + logf(L);
+  if (!O) return;
+  const float inv = 1.0f / L;
+  for (int64_t d = lane; d < D; d += 64) {
+    float acc = 0.f;
+    for (int s = 0; s < splits; ++s) {
+      const float ms = pm[(int64_t)s * nb + b];
+      if (ms == -INFINITY) continue;
+      acc += __expf(ms - M) * pO[((int64_t)s * nb + b) * D + d];
+    }
+    O[b * D + d] = acc * inv;
+  }
+}
+
+// Exact recompute of the users flagged by k_dec_bf16 (their max score sits
+// more than kUnderflowSpan below the fixed offset: only possible for |u| in
+// the hundreds). Two passes in fp32 over the bf16 E, one block per flagged
+// user; blocks of unflagged users exit at once.
+__global__ void __launch_bounds__(256) k_dec_fixup(const int* __restrict__ flag, const float* __restrict__ U,
+                                                   int64_t ldu, const bf16_t* __restrict__ E, int64_t N,
+                                                   int64_t D, float* __restrict__ lse, float* __restrict__ O) {
+  __shared__ float red[4];
+  __shared__ float pbuf[256];
+  const int64_t b = blockIdx.x;
+  if (!flag[b]) return;
+  const float* u = U + b * ldu;
+  auto score = [&](int64_t i) {
+    float s = 0.f;
+    for (int64_t d = 0; d < D; ++d) s += u[d] * bf2f(E[i * D + d]);
+    return s;
+  };
+  float mx = -INFINITY;
+  for (int64_t i = threadIdx.x; i < N; i += 256) mx = fmaxf(mx, score(i));
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float l = 0.f;
+  float oacc[4] = {0.f, 0.f, 0.f, 0.f};  // thread owns d = threadIdx.x + 256 k (D <= 1024)
+  for (int64_t i0 = 0; i0 < N; i0 += 256) {
+    const int64_t i = i0 + threadIdx.x;
+    const float pv = (i < N) ? expf(score(i) - mx) : 0.f;
+    pbuf[threadIdx.x] = pv;
+    l += pv;
+    __syncthreads();
+    const int64_t cnt = min((int64_t)256, N - i0);
+    for (int64_t j = 0; j < cnt; ++j)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t d = threadIdx.x + 256 * k;
+        if (d < D) oacc[k] += pbuf[j] * bf2f(E[(i0 + j) * D + d]);
+      }
+    __syncthreads();
+  }
+  l = block_sum<256>(l, red);
+  if (threadIdx.x == 0) lse[b] = mx + logf(l);
+  if (O) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t d = threadIdx.x + 256 * k;
+      if (d < D) O[b * D + d] = oacc[k] / l;
+    }
+  }
+}
+
+// max_i ||E_i||_2 over an fp32 or bf16 [N, D] matrix (score bound of the bf16 path).
+__global__ void __launch_bounds__(256) k_row_norm_max(int dtype, const void* __restrict__ E, int64_t N, int64_t D,
+                                                      unsigned* __restrict__ out_bits) {
+  const int lane = threadIdx.x & 63;
+  float best = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); i < N; i += (int64_t)gridDim.x * 4) {
+    float s = 0.f;
+    for (int64_t d = lane; d < D; d += 64) {
+      const float v = dtype == HVAE_BF16 ? bf2f(((const bf16_t*)E)[i * D + d]) : ((const float*)E)[i * D + d];
+      s += v * v;
+    }
+    best = fmaxf(best, sqrtf(wave_sum(s)));
+  }
+  if (lane == 0) atomicMax(out_bits, __float_as_uint(best));  // non-negative floats order as uints
+}
+
+// Sparse half of the loss / gradient against the fp32 E (one wave per row):
+//   recon_rows[b] = n_b lse_b - sum_j x_bj (u_b . E_j)
+//   dU[b]         = scale (n_b O_b - sum_j x_bj E_j)
+template <int NV>
+__global__ void __launch_bounds__(256) k_dec_sparse(const int64_t* __restrict__ row_ptr,
+                                                    const int32_t* __restrict__ col_idx,
+                                                    const float* __restrict__ vals,
+                                                    const int32_t* __restrict__ rows,
+    const int64_t* __restrict__ rows_offset, int64_t nb,
+                                                    const float* __restrict__ U, int64_t ldu,
+                                                    const float* __restrict__ E, int64_t D,
+                                                    const float* __restrict__ lse,
+                                                    const float* __restrict__ O, float scale,
+                                                    float* __restrict__ recon_rows,
+                                                    float* __restrict__ dU) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  const int64_t r = batch_row(rows, rows_offset, b);
+  const int64_t beg = row_ptr[r], end = row_ptr[r + 1];
+  float4 u[NV], acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t e = 4 * (int64_t)(lane + 64 * k);
+    u[k] = (e < D) ? *reinterpret_cast<const float4*>(U + b * ldu + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  float n = 0.f;
+  for (int64_t base = beg; base < end; base += 64) {
+    const int64_t cnt = min((int64_t)64, end - base);
+    const int my_j = (lane < cnt) ? col_idx[base + lane] : 0;
+    const float my_x = (lane < cnt) ? vals[base + lane] : 0.f;
+    n += my_x;
+    for (int t = 0; t < cnt; ++t) {
+      const int j = __builtin_amdgcn_readlane(my_j, t);
+      const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), t));
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int64_t e = 4 * (int64_t)(lane + 64 * k);
+        if (e >= D) continue;
+        const float4 ev = *reinterpret_cast<const float4*>(E + (int64_t)j * D + e);
+        acc[k].x += x * ev.x; acc[k].y += x * ev.y; acc[k].z += x * ev.z; acc[k].w += x * ev.w;
+      }
+    }
+  }
+  n = wave_sum(n);
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    dot += (u[k].x * acc[k].x + u[k].y * acc[k].y) + (u[k].z * acc[k].z + u[k].w * acc[k].w);
+  dot = wave_sum(dot);
+  if (lane == 0) recon_rows[b] = n * lse[b] - dot;
+  if (!dU) return;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t e = 4 * (int64_t)(lane + 64 * k);
+    if (e >= D) continue;
+    const float4 ov = *reinterpret_cast<const float4*>(O + b * D + e);
+    *reinterpret_cast<float4*>(dU + b * D + e) =
+        make_float4(scale * (n * ov.x - acc[k].x), scale * (n * ov.y - acc[k].y),
+                    scale * (n * ov.z - acc[k].z), scale * (n * ov.w - acc[k].w));
+  }
+}
+
+// ------------------------------------------------------------- planning ---
+struct DecPlan {
+  int splits;
+  int64_t tiles_per_split;
+  int64_t blocks;
+  size_t lds;
+};
+
+static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
+  const int64_t upb = dtype == HVAE_BF16 ? kBfUsersPerBlock : kF32UsersPerBlock;
+  const int64_t ti = dtype == HVAE_BF16 ? kBfTI : kF32TI;
+  const int64_t target = dtype == HVAE_BF16 ? 256 : 512;
+  const int64_t nub = cdiv(nb, upb), tiles = cdiv(N, ti);
+  int64_t s = cdiv(target, nub);
+  s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 2));
+  s = std::min<int64_t>(s, std::max<int64_t>(1, N / std::max<int64_t>(1, 2 * nb)));
+  if (s >= 8) s = s / 8 * 8;
+  s = std::max<int64_t>(1, std::min<int64_t>(s, 4096));
+  DecPlan p;
+  p.tiles_per_split = cdiv(tiles, s);
+  p.splits = (int)cdiv(tiles, p.tiles_per_split);
+  if (p.splits >= 8 && p.splits % 8) {  // keep "split shares an XCD" when possible
+    const int64_t s8 = (int64_t)p.splits / 8 * 8;
+    p.tiles_per_split = cdiv(tiles, s8);
+    p.splits = (int)cdiv(tiles, p.tiles_per_split);
+  }
+  p.blocks = nub * p.splits;
+  p.lds = 0;
+  return p;
+}
+
+static size_t dec_ws_bytes(int splits, int64_t nb, int64_t D) {
+  const size_t flags = (size_t)cdiv(nb * sizeof(int), 256) * 256;
+  return flags + (splits > 1 ? (size_t)splits * nb * (D + 2) * sizeof(float) : 0);
+}
+
+template <int D, bool WO>
+static int launch_bf16(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                       const DecPlan& p, DecOut o, hipStream_t st) {
+  constexpr int lds = 2 * bf_tile_bytes<D>();
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec_bf16<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr_set = true;
+  }
+  k_dec_bf16<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N, p.splits,
+                                                         p.tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec_bf16");
+  return HVAE_OK;
+}
+
+template <int D, bool WO>
+static int launch_f32(const float* U, int64_t ldu, const void* E, int64_t nb, int64_t N, const DecPlan& p,
+                      DecOut o, hipStream_t st) {
+  constexpr int lds = 2 * f32_tile_bytes<D>();
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec_f32<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr_set = true;
+  }
+  k_dec_f32<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, (const float*)E, nb, N, p.splits,
+                                                        p.tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec_f32");
+  return HVAE_OK;
+}
+
+template <bool WO>
+static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb,
+                    int64_t N, int64_t D, const DecPlan& p, DecOut o, hipStream_t st) {
+  if (dtype == HVAE_BF16) {
+    switch (D) {
+      case 64: return launch_bf16<64, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      case 128: return launch_bf16<128, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      case 256: return launch_bf16<256, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      case 384: return launch_bf16<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      default: break;
+    }
+  } else {
+    switch (D) {
+      case 32: return launch_f32<32, WO>(U, ldu, E, nb, N, p, o, st);
+      case 64: return launch_f32<64, WO>(U, ldu, E, nb, N, p, o, st);
+      case 128: return launch_f32<128, WO>(U, ldu, E, nb, N, p, o, st);
+      case 256: return launch_f32<256, WO>(U, ldu, E, nb, N, p, o, st);
+      case 384: return launch_f32<384, WO>(U, ldu, E, nb, N, p, o, st);
+      default: break;
+    }
+  }
+  HVAE_FAIL(HVAE_ERR_UNSUPPORTED, "hvae_decoder_fwd: no %s kernel for D=%lld",
+            dtype == HVAE_BF16 ? "bf16" : "f32", (long long)D);
+}
+
+}  // namespace hvae
+
+using namespace hvae;
+
+extern "C" int hvae_decoder_supported(int dtype, int64_t D) {
+  if (dtype == HVAE_BF16) return D == 64 || D == 128 || D == 256 || D == 384;
+  if (dtype == HVAE_F32) return D == 32 || D == 64 || D == 128 || D == 256 || D == 384;
+  return 0;
+}
+
+extern "C" int hvae_row_norm_max(int dtype, const void* E, int64_t N, int64_t D, float* out, void* stream) {
+  HVAE_REQUIRE(E && out && N > 0 && D > 0 && (dtype == HVAE_F32 || dtype == HVAE_BF16),
+               "hvae_row_norm_max: bad args");
+  hipStream_t st = as_stream(stream);
+  HVAE_HIP(hipMemsetAsync(out, 0, sizeof(float), st));
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, 4), 1024);
+  k_row_norm_max<<<grid, 256, 0, st>>>(dtype, E, N, D, (unsigned*)out);
+  HVAE_LAUNCH_CHECK("k_row_norm_max");
+  return HVAE_OK;
+}
+
+extern "C" size_t hvae_decoder_workspace(int dtype, int64_t nb, int64_t N, int64_t D) {
+  const DecPlan p = dec_plan(dtype, nb, N, D);
+  return dec_ws_bytes(p.splits, nb, D);
+}
+
+extern "C" int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
+                                int64_t nb, int64_t N, int64_t D, float* lse, float* O, void* ws,
+                                size_t ws_bytes, void* stream) {
+  HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32, "hvae_decoder_fwd: bad dtype");
+  HVAE_REQUIRE(U && E && lse && N > 0 && D > 0 && ldu >= D, "hvae_decoder_fwd: bad args");
+  HVAE_REQUIRE(dtype != HVAE_BF16 || e_maxnorm, "hvae_decoder_fwd: bf16 needs e_maxnorm");
+  HVAE_REQUIRE(ldu % 4 == 0 && ((uintptr_t)U % 16) == 0 && ((uintptr_t)E % 16) == 0 &&
+                   (!O || ((uintptr_t)O % 16) == 0),
+               "hvae_decoder_fwd: U/E/O must be 16-B aligned with ldu %% 4 == 0");
+  HVAE_REQUIRE(N < (1ll << 31), "hvae_decoder_fwd: N too large");
+  if (nb == 0) return HVAE_OK;
+  hipStream_t st = as_stream(stream);
+  const size_t flag_bytes = (size_t)cdiv(nb * sizeof(int), 256) * 256;
+  if (!ws || ws_bytes < flag_bytes)
+    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_decoder_fwd: workspace %zu < %zu", ws_bytes, flag_bytes);
+  DecPlan p = dec_plan(dtype, nb, N, D);
+  if (p.splits > 1 && ws_bytes < dec_ws_bytes(p.splits, nb, D)) {
+    // fall back to fewer splits that fit the given workspace
+    int64_t fit = (int64_t)((ws_bytes - flag_bytes) / ((size_t)nb * (D + 2) * sizeof(float)));
+    const int64_t tiles = cdiv(N, dtype == HVAE_BF16 ? kBfTI : kF32TI);
+    if (fit < 2) fit = 1;
+    p.tiles_per_split = cdiv(tiles, fit);
+    p.splits = (int)cdiv(tiles, p.tiles_per_split);
+    p.blocks = cdiv(nb, dtype == HVAE_BF16 ? kBfUsersPerBlock : kF32UsersPerBlock) * p.splits;
+  }
+  DecOut o{};
+  o.flag = (int*)ws;
+  HVAE_HIP(hipMemsetAsync(o.flag, 0, nb * sizeof(int), st));
+  if (p.splits == 1) {
+    o.direct = 1;
+    o.lse = lse;
+    o.O = O;
+  } else {
+    float* base = (float*)((char*)ws + flag_bytes);
+    o.direct = 0;
+    o.m = base;
+    o.l = base + (size_t)p.splits * nb;
+    o.O = base + (size_t)2 * p.splits * nb;
+  }
+  int rc = O ? dispatch<true>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st)
+             : dispatch<false>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st);
+  if (rc) return rc;
+  if (p.splits > 1) {
+    k_dec_merge<<<(unsigned)cdiv(nb, 4), 256, 0, st>>>(o.m, o.l, o.O, p.splits, nb, D, lse, O);
+    HVAE_LAUNCH_CHECK("k_dec_merge");
+  }
+  if (dtype == HVAE_BF16) {
+    HVAE_REQUIRE(D <= 1024, "hvae_decoder_fwd: D too large for the fixup");
+    k_dec_fixup<<<(unsigned)nb, 256, 0, st>>>(o.flag, U, ldu, (const bf16_t*)E, N, D, lse, O);
+    HVAE_LAUNCH_CHECK("k_dec_fixup");
+  }
+  return HVAE_OK;
+}
+
+extern "C" int hvae_decoder_bwd(const hvae_csr_batch* x, const float* U, int64_t ldu, const float* E32,
+                                int64_t D, const float* lse, const float* O, float grad_scale,
+                                float* recon_rows, float* dU, void* stream) {
+  HVAE_REQUIRE(x && x->row_ptr && U && E32 && lse && recon_rows && D > 0 && ldu >= D,
+               "hvae_decoder_bwd: bad args");
+  HVAE_REQUIRE(!dU || O, "hvae_decoder_bwd: dU needs O");
+  HVAE_REQUIRE(D % 4 == 0 && ldu % 4 == 0, "hvae_decoder_bwd: D and ldu must be multiples of 4");
+  if (x->nb == 0) return HVAE_OK;
+  const unsigned grid = (unsigned)cdiv(x->nb, 4);
+  hipStream_t st = as_stream(stream);
+  const int64_t nv = cdiv(D, 256);
+#define HVAE_DS(NV_)                                                                               \
+  k_dec_sparse<NV_><<<grid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->vals, x->rows, x->rows_offset, x->nb, U, ldu, \
+                                          E32, D, lse, O, grad_scale, recon_rows, dU)
+  if (nv <= 1) HVAE_DS(1);
+  else if (nv <= 2) HVAE_DS(2);
+  else if (nv <= 3) HVAE_DS(3);
+  else if (nv <= 4) HVAE_DS(4);
+  else HVAE_FAIL(HVAE_ERR_UNSUPPORTED, "hvae_decoder_bwd: D=%lld > 1024", (long long)D);
+#undef HVAE_DS
+  HVAE_LAUNCH_CHECK("k_dec_sparse");
+  return HVAE_OK;
+}

@@ -1,0 +1,692 @@
+// hvae_encoder.hip -- encoder kernels (K1-K3, K11 partial, K12 of SURVEY §2.1).
+//
+//   * sparse first layer: a = x W1^T + b1 gathered row-by-row from the
+//     item-major W1t [N, H] (one wave per user row, 2 KB item rows at H=512
+//     read as float4 per lane), fused with LayerNorm -> GELU -> Dropout;
+//   * the same epilogue for dense hidden layers, and its backward;
+//   * the row-sparse first-layer weight gradient, built by a deterministic
+//     counting sort over the batch nonzeros (no float atomics);
+//   * dense [B, N] -> CSR for the module-API path.
+//
+// Reference: src/ml/model.py:103-127 (_build_encoder), 138-155 (encode).
+#include <algorithm>
+
+#include "hvae_common.h"
+
+namespace hvae {
+
+constexpr float kLnEps = 1e-5f;  // nn.LayerNorm default (src/ml/model.py:115)
+
+// --------------------------------------------------------------------------
+// LayerNorm -> GELU -> Dropout epilogue on one row held as NV float4 chunks
+// per lane (chunk c = lane + 64 k covers elements 4c .. 4c+3, valid if 4c < H).
+template <int NV>
+__device__ __forceinline__ void ln_gelu_drop_row(float4 (&acc)[NV], int lane, int64_t H, int64_t row,
+                                                 const float* __restrict__ ln_w,
+                                                 const float* __restrict__ ln_b, float p_drop,
+                                                 float scale, const float* __restrict__ drop_mult,
+                                                 uint64_t seed, int64_t step, uint32_t tag,
+                                                 int train, float* __restrict__ h_out,
+                                                 float* __restrict__ xhat_out,
+                                                 float* __restrict__ rstd_out) {
+  const float invH = 1.0f / (float)H;
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t e = 4 * (int64_t)(lane + 64 * k);
+    if (e < H) s += (acc[k].x + acc[k].y) + (acc[k].z + acc[k].w);
+  }
+  const float mean = wave_sum(s) * invH;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t e = 4 * (int64_t)(lane + 64 * k);
+    if (e < H) {
+      acc[k].x -= mean; acc[k].y -= mean; acc[k].z -= mean; acc[k].w -= mean;
+      q += (acc[k].x * acc[k].x + acc[k].y * acc[k].y) + (acc[k].z * acc[k].z + acc[k].w * acc[k].w);
+    }
+  }
+  const float var = wave_sum(q) * invH;  // biased variance, as nn.LayerNorm
+  const float rstd = 1.0f / sqrtf(var + kLnEps);
+  if (rstd_out && lane == 0) rstd_out[row] = rstd;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t e = 4 * (int64_t)(lane + 64 * k);
+    if (e >= H) continue;
+    float4 xh = make_float4(acc[k].x * rstd, acc[k].y * rstd, acc[k].z * rstd, acc[k].w * rstd);
+    if (xhat_out) *reinterpret_cast<float4*>(xhat_out + row * H + e) = xh;
+    const float4 w = *reinterpret_cast<const float4*>(ln_w + e);
+    const float4 b = *reinterpret_cast<const float4*>(ln_b + e);
+    float y[4] = {xh.x * w.x + b.x, xh.y * w.y + b.y, xh.z * w.z + b.z, xh.w * w.w + b.w};
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float g = gelu_f(y[i]);
+      const uint64_t idx = (uint64_t)(row * H + e + i);
+      o[i] = train ? g * dropout_mult(p_drop, scale, drop_mult, idx, seed, step, tag) : g;
+    }
+    *reinterpret_cast<float4*>(h_out + row * H + e) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// Sparse first layer + epilogue. One wave per batch row, 4 waves per block.
+template <int NV>
+__global__ void __launch_bounds__(256) k_encoder_sparse_fwd(
+    const int64_t* __restrict__ row_ptr, const int32_t* __restrict__ col_idx,
+    const float* __restrict__ vals, const int32_t* __restrict__ rows,
+    const int64_t* __restrict__ rows_offset, int64_t nb,
+    const float* __restrict__ w1t, const float* __restrict__ b1, const float* __restrict__ ln_w,
+    const float* __restrict__ ln_b, int64_t H, float p_drop, float scale,
+    const float* __restrict__ drop_mult, uint64_t seed, const int64_t* __restrict__ step_dev,
+    int train, float* __restrict__ h_out, float* __restrict__ xhat_out,
+    float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  const int64_t step = load_step(step_dev);
+  const int64_t r = batch_row(rows, rows_offset, b);
+  const int64_t beg = row_ptr[r], end = row_ptr[r + 1];
+
+  float4 acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t e = 4 * (int64_t)(lane + 64 * k);
+    acc[k] = (e < H) ? *reinterpret_cast<const float4*>(b1 + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  // Row entries are fetched 64 at a time (one per lane) and broadcast with
+  // v_readlane; four item rows are in flight per step for memory parallelism.
+  for (int64_t base = beg; base < end; base += 64) {
+    const int64_t n = min((int64_t)64, end - base);
+    const int my_j = (lane < n) ? col_idx[base + lane] : 0;
+    const float my_x = (lane < n) ? vals[base + lane] : 0.f;
+    int t = 0;
+    for (; t + 4 <= n; t += 4) {
+      int j[4];
+      float x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        j[u] = __builtin_amdgcn_readlane(my_j, t + u);
+        x[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), t + u));
+      }
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int64_t e = 4 * (int64_t)(lane + 64 * k);
+        if (e >= H) continue;
+        float4 w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const float4*>(w1t + (int64_t)j[u] * H + e);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          acc[k].x += x[u] * w[u].x; acc[k].y += x[u] * w[u].y;
+          acc[k].z += x[u] * w[u].z; acc[k].w += x[u] * w[u].w;
+        }
+      }
+    }
+    for (; t < n; ++t) {
+      const int j = __builtin_amdgcn_readlane(my_j, t);
+      const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), t));
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int64_t e = 4 * (int64_t)(lane + 64 * k);
+        if (e >= H) continue;
+        const float4 w = *reinterpret_cast<const float4*>(w1t + (int64_t)j * H + e);
+        acc[k].x += x * w.x; acc[k].y += x * w.y; acc[k].z += x * w.z; acc[k].w += x * w.w;
+      }
+    }
+  }
+  ln_gelu_drop_row<NV>(acc, lane, H, b, ln_w, ln_b, p_drop, scale, drop_mult, seed, step,
+                       kTagEncDrop + 0u, train, h_out, xhat_out, rstd_out);
+}
+
+template <int NV>
+__global__ void __launch_bounds__(256) k_ln_gelu_drop_fwd(
+    const float* __restrict__ a, const float* __restrict__ ln_w, const float* __restrict__ ln_b,
+    int64_t nb, int64_t H, float p_drop, float scale, const float* __restrict__ drop_mult,
+    uint64_t seed, const int64_t* __restrict__ step_dev, uint32_t tag, int train,
+    float* __restrict__ h_out, float* __restrict__ xhat_out, float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  const int64_t step = load_step(step_dev);
+  float4 acc[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t e = 4 * (int64_t)(lane + 64 * k);
+    acc[k] = (e < H) ? *reinterpret_cast<const float4*>(a + b * H + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  ln_gelu_drop_row<NV>(acc, lane, H, b, ln_w, ln_b, p_drop, scale, drop_mult, seed, step, tag,
+                       train, h_out, xhat_out, rstd_out);
+}
+
+// Backward of Dropout(GELU(LN(a))). 16 rows per block (4 waves x 4 rows);
+// per-block column partials of d(ln_w) = sum dy * xhat and d(ln_b) = sum dy.
+constexpr int kLnBwdRows = 16;
+
+template <int NV>
+__global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
+    const float* __restrict__ dh, const float* __restrict__ xhat, const float* __restrict__ rstd,
+    const float* __restrict__ ln_w, const float* __restrict__ ln_b, int64_t nb, int64_t H,
+    float p_drop, float scale, const float* __restrict__ drop_mult, uint64_t seed,
+    const int64_t* __restrict__ step_dev, uint32_t tag, int train, float* __restrict__ da,
+    float* __restrict__ part /* [nblocks][2][H] */) {
+  extern __shared__ __attribute__((aligned(16))) float lds_part[];  // [4 waves][2][H]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t step = load_step(step_dev);
+  const float invH = 1.0f / (float)H;
+  float4 pg[NV], pb[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) { pg[k] = make_float4(0.f, 0.f, 0.f, 0.f); pb[k] = pg[k]; }
+
+  for (int rr = 0; rr < kLnBwdRows / 4; ++rr) {
+    const int64_t b = (int64_t)blockIdx.x * kLnBwdRows + rr * 4 + w;
+    if (b >= nb) break;
+    const float rs = rstd[b];
+    float4 dxh[NV], xh[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t e = 4 * (int64_t)(lane + 64 * k);
+      if (e >= H) { dxh[k] = make_float4(0.f, 0.f, 0.f, 0.f); xh[k] = dxh[k]; continue; }
+      const float4 g = *reinterpret_cast<const float4*>(dh + b * H + e);
+      xh[k] = *reinterpret_cast<const float4*>(xhat + b * H + e);
+      const float4 lw = *reinterpret_cast<const float4*>(ln_w + e);
+      const float4 lb = *reinterpret_cast<const float4*>(ln_b + e);
+      const float gv[4] = {g.x, g.y, g.z, g.w};
+      const float xv[4] = {xh[k].x, xh[k].y, xh[k].z, xh[k].w};
+      const float wv[4] = {lw.x, lw.y, lw.z, lw.w};
+      const float bv[4] = {lb.x, lb.y, lb.z, lb.w};
+      float dy[4], dx[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint64_t idx = (uint64_t)(b * H + e + i);
+        const float dm = train ? dropout_mult(p_drop, scale, drop_mult, idx, seed, step, tag) : 1.f;
+        dy[i] = gv[i] * dm * gelu_grad_f(xv[i] * wv[i] + bv[i]);
+        dx[i] = dy[i] * wv[i];
+        s1 += dx[i];
+        s2 += dx[i] * xv[i];
+      }
+      pg[k].x += dy[0] * xv[0]; pg[k].y += dy[1] * xv[1]; pg[k].z += dy[2] * xv[2]; pg[k].w += dy[3] * xv[3];
+      pb[k].x += dy[0]; pb[k].y += dy[1]; pb[k].z += dy[2]; pb[k].w += dy[3];
+      dxh[k] = make_float4(dx[0], dx[1], dx[2], dx[3]);
+    }
+    const float m1 = wave_sum(s1) * invH, m2 = wave_sum(s2) * invH;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t e = 4 * (int64_t)(lane + 64 * k);
+      if (e >= H) continue;
+      float4 o;
+      o.x = rs * (dxh[k].x - m1 - xh[k].x * m2);
+      o.y = rs * (dxh[k].y - m1 - xh[k].y * m2);
+      o.z = rs * (dxh[k].z - m1 - xh[k].z * m2);
+      o.w = rs * (dxh[k].w - m1 - xh[k].w * m2);
+      *reinterpret_cast<float4*>(da + b * H + e) = o;
+    }
+  }
+  // combine the 4 waves' column partials in a fixed order
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int64_t e = 4 * (int64_t)(lane + 64 * k);
+    if (e >= H) continue;
+    *reinterpret_cast<float4*>(lds_part + (w * 2 + 0) * H + e) = pg[k];
+    *reinterpret_cast<float4*>(lds_part + (w * 2 + 1) * H + e) = pb[k];
+  }
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < 2 * H; i += blockDim.x) {
+    const float v = ((lds_part[i] + lds_part[2 * H + i]) + lds_part[4 * H + i]) + lds_part[6 * H + i];
+    part[(int64_t)blockIdx.x * 2 * H + i] = v;
+  }
+}
+
+// Sum the per-block partials [nparts][2][H] -> (d_ln_w, d_ln_b), fixed order.
+__global__ void k_ln_part_reduce(const float* __restrict__ part, int64_t nparts, int64_t H,
+                                 float* __restrict__ d_ln_w, float* __restrict__ d_ln_b) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * H) return;
+  float s = 0.f;
+  for (int64_t p = 0; p < nparts; ++p) s += part[p * 2 * H + i];
+  if (i < H) d_ln_w[i] = s; else d_ln_b[i - H] = s;
+}
+
+// --------------------------------------------------------------------------
+// dense [B, N] -> CSR (row order preserved)
+__global__ void __launch_bounds__(256) k_dense_row_count(const float* __restrict__ x, int64_t N,
+                                                         int64_t* __restrict__ cnt) {
+  __shared__ float red[4];
+  const int64_t b = blockIdx.x;
+  float c = 0.f;
+  for (int64_t i = threadIdx.x; i < N; i += 256) c += (x[b * N + i] != 0.f) ? 1.f : 0.f;
+  c = block_sum<256>(c, red);
+  if (threadIdx.x == 0) cnt[b] = (int64_t)c;
+}
+
+// Single-block exclusive scan of n int64 counts in place -> row_ptr[0..n].
+__global__ void __launch_bounds__(1024) k_scan_i64(int64_t* __restrict__ v, int64_t n) {
+  __shared__ int64_t sh[1024];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t val = (i < n) ? v[i] : 0;
+    sh[threadIdx.x] = val;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int64_t t = (threadIdx.x >= o) ? sh[threadIdx.x - o] : 0;
+      __syncthreads();
+      sh[threadIdx.x] += t;
+      __syncthreads();
+    }
+    if (i < n) v[i] = carry + sh[threadIdx.x] - val;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry += sh[1023];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) v[n] = carry;
+}
+
+__global__ void __launch_bounds__(256) k_dense_compact(const float* __restrict__ x, int64_t N,
+                                                       const int64_t* __restrict__ row_ptr,
+                                                       int32_t* __restrict__ col, float* __restrict__ val,
+                                                       int64_t cap) {
+  __shared__ int wcnt[4];
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t pos = row_ptr[b];
+  for (int64_t base = 0; base < N; base += 256) {
+    const int64_t i = base + threadIdx.x;
+    const float v = (i < N) ? x[b * N + i] : 0.f;
+    const bool nz = v != 0.f;
+    const uint64_t m = __ballot(nz);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wcnt[w] = __popcll(m);
+    __syncthreads();
+    int off = 0;
+    for (int k = 0; k < w; ++k) off += wcnt[k];
+    const int tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+    if (nz) {
+      const int64_t p = pos + off + before;
+      if (p < cap) { col[p] = (int32_t)i; val[p] = v; }
+    }
+    pos += tot;
+    __syncthreads();
+  }
+}
+
+// --------------------------------------------------------------------------
+// Row-sparse W1 gradient (K12): counting sort of the batch nonzeros by item.
+constexpr int kScanItemsPerBlock = 4096;  // 256 threads x 16 items
+
+__global__ void __launch_bounds__(256) k_rg_count(const int64_t* __restrict__ row_ptr,
+                                                  const int32_t* __restrict__ col_idx,
+                                                  const int32_t* __restrict__ rows,
+    const int64_t* __restrict__ rows_offset, int64_t nb,
+                                                  int32_t* __restrict__ cnt) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  const int64_t r = batch_row(rows, rows_offset, b);
+  for (int64_t e = row_ptr[r] + lane; e < row_ptr[r + 1]; e += 64) atomicAdd(&cnt[col_idx[e]], 1);
+}
+
+// per 4096-item block: (#items with cnt > 0, sum of cnt)
+__global__ void __launch_bounds__(256) k_rg_scan1(const int32_t* __restrict__ cnt, int64_t N,
+                                                  int64_t* __restrict__ blocktot /* [nblk][2] */) {
+  __shared__ float red[4];
+  int nf = 0, nc = 0;
+  const int64_t base = (int64_t)blockIdx.x * kScanItemsPerBlock + threadIdx.x * 16;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t j = base + i;
+    const int c = (j < N) ? cnt[j] : 0;
+    nf += c > 0;
+    nc += c;
+  }
+  // counts are small integers: exact in fp32 up to 2^24 per block
+  const float tf = block_sum<256>((float)nf, red);
+  const float tc = block_sum<256>((float)nc, red);
+  if (threadIdx.x == 0) {
+    blocktot[2 * blockIdx.x + 0] = (int64_t)tf;
+    blocktot[2 * blockIdx.x + 1] = (int64_t)tc;
+  }
+}
+
+// single block: exclusive scan of the block totals; n_unique, seg_off[n_unique]
+__global__ void __launch_bounds__(1024) k_rg_scan2(int64_t* __restrict__ blocktot, int64_t nblk,
+                                                   int32_t* __restrict__ n_unique,
+                                                   int32_t* __restrict__ seg_off, int64_t cap) {
+  __shared__ int64_t sf[1024], sc[1024];
+  __shared__ int64_t cf, cc;
+  if (threadIdx.x == 0) { cf = 0; cc = 0; }
+  __syncthreads();
+  for (int64_t base = 0; base < nblk; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t vf = (i < nblk) ? blocktot[2 * i] : 0, vc = (i < nblk) ? blocktot[2 * i + 1] : 0;
+    sf[threadIdx.x] = vf;
+    sc[threadIdx.x] = vc;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int64_t tf = (threadIdx.x >= o) ? sf[threadIdx.x - o] : 0;
+      const int64_t tc = (threadIdx.x >= o) ? sc[threadIdx.x - o] : 0;
+      __syncthreads();
+      sf[threadIdx.x] += tf;
+      sc[threadIdx.x] += tc;
+      __syncthreads();
+    }
+    if (i < nblk) {
+      blocktot[2 * i] = cf + sf[threadIdx.x] - vf;
+      blocktot[2 * i + 1] = cc + sc[threadIdx.x] - vc;
+    }
+    __syncthreads();
+    if (threadIdx.x == 1023) { cf += sf[1023]; cc += sc[1023]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *n_unique = (int32_t)cf;
+    if (cf <= cap) seg_off[cf] = (int32_t)cc;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rg_scan3(int32_t* __restrict__ cnt, int64_t N,
+                                                  const int64_t* __restrict__ blockoff,
+                                                  int32_t* __restrict__ slot_of,
+                                                  int32_t* __restrict__ item_of,
+                                                  int32_t* __restrict__ seg_off, int64_t cap) {
+  __shared__ int sf[256], sc[256];
+  const int64_t base = (int64_t)blockIdx.x * kScanItemsPerBlock + threadIdx.x * 16;
+  int c[16];
+  int nf = 0, nc = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t j = base + i;
+    c[i] = (j < N) ? cnt[j] : 0;
+    nf += c[i] > 0;
+    nc += c[i];
+  }
+  sf[threadIdx.x] = nf;
+  sc[threadIdx.x] = nc;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {
+    const int tf = (threadIdx.x >= o) ? sf[threadIdx.x - o] : 0;
+    const int tc = (threadIdx.x >= o) ? sc[threadIdx.x - o] : 0;
+    __syncthreads();
+    sf[threadIdx.x] += tf;
+    sc[threadIdx.x] += tc;
+    __syncthreads();
+  }
+  int64_t slot = blockoff[2 * blockIdx.x] + sf[threadIdx.x] - nf;
+  int64_t off = blockoff[2 * blockIdx.x + 1] + sc[threadIdx.x] - nc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    if (c[i] > 0) {
+      const int64_t j = base + i;
+      if (slot < cap) {
+        slot_of[j] = (int32_t)slot;
+        item_of[slot] = (int32_t)j;
+        seg_off[slot] = (int32_t)off;
+      }
+      cnt[j] = 0;  // leave the histogram zeroed for the next batch
+      ++slot;
+      off += c[i];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rg_scatter(const int64_t* __restrict__ row_ptr,
+                                                    const int32_t* __restrict__ col_idx,
+                                                    const float* __restrict__ vals,
+                                                    const int32_t* __restrict__ rows,
+    const int64_t* __restrict__ rows_offset, int64_t nb,
+                                                    const int32_t* __restrict__ slot_of,
+                                                    const int32_t* __restrict__ seg_off,
+                                                    int32_t* __restrict__ fill,
+                                                    int32_t* __restrict__ contrib_row,
+                                                    float* __restrict__ contrib_val, int64_t cap) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= nb) return;
+  const int64_t r = batch_row(rows, rows_offset, b);
+  for (int64_t e = row_ptr[r] + lane; e < row_ptr[r + 1]; e += 64) {
+    const int s = slot_of[col_idx[e]];
+    const int64_t pos = (int64_t)seg_off[s] + atomicAdd(&fill[s], 1);
+    if (pos < cap) {
+      contrib_row[pos] = (int32_t)b;
+      contrib_val[pos] = vals[e];
+    }
+  }
+}
+
+// One block per item segment (grid-stride): sort the segment's contributions
+// by batch row (bitonic in LDS), then sum x * da[b, :] in that order.
+constexpr int kSegSortCap = 4096;
+
+__global__ void __launch_bounds__(256) k_rg_rows(const int32_t* __restrict__ n_unique,
+                                                 const int32_t* __restrict__ seg_off,
+                                                 int32_t* __restrict__ fill,
+                                                 const int32_t* __restrict__ contrib_row,
+                                                 const float* __restrict__ contrib_val,
+                                                 const float* __restrict__ da, int64_t H,
+                                                 float* __restrict__ out_rows) {
+  __shared__ int key[kSegSortCap];
+  __shared__ float kval[kSegSortCap];
+  const int nu = *n_unique;
+  for (int s = blockIdx.x; s < nu; s += gridDim.x) {
+    const int beg = seg_off[s], len = seg_off[s + 1] - beg;
+    const bool sorted_path = len <= kSegSortCap;
+    if (sorted_path && len > 1) {
+      int p2 = 1;
+      while (p2 < len) p2 <<= 1;
+      for (int i = threadIdx.x; i < p2; i += 256) {
+        key[i] = (i < len) ? contrib_row[beg + i] : 0x7fffffff;
+        kval[i] = (i < len) ? contrib_val[beg + i] : 0.f;
+      }
+      __syncthreads();
+      for (int k = 2; k <= p2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = threadIdx.x; i < p2; i += 256) {
+            const int ixj = i ^ j;
+            if (ixj > i) {
+              const bool up = (i & k) == 0;
+              const int a = key[i], c = key[ixj];
+              if ((a > c) == up) {
+                key[i] = c; key[ixj] = a;
+                const float t = kval[i]; kval[i] = kval[ixj]; kval[ixj] = t;
+              }
+            }
+          }
+          __syncthreads();
+        }
+      }
+    } else if (len == 1) {
+      if (threadIdx.x == 0) { key[0] = contrib_row[beg]; kval[0] = contrib_val[beg]; }
+      __syncthreads();
+    }
+    for (int64_t c4 = threadIdx.x; 4 * c4 < H; c4 += 256) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int i = 0; i < len; ++i) {
+        const int b = sorted_path ? key[i] : contrib_row[beg + i];
+        const float x = sorted_path ? kval[i] : contrib_val[beg + i];
+        const float4 d = *reinterpret_cast<const float4*>(da + (int64_t)b * H + 4 * c4);
+        acc.x += x * d.x; acc.y += x * d.y; acc.z += x * d.z; acc.w += x * d.w;
+      }
+      *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + 4 * c4) = acc;
+    }
+    if (threadIdx.x == 0) fill[s] = 0;
+    __syncthreads();
+  }
+}
+
+__global__ void k_rg_to_dense(const int32_t* __restrict__ n_unique, const int32_t* __restrict__ item_of,
+                              const float* __restrict__ rows, int64_t H, float* __restrict__ dense,
+                              int64_t ld) {
+  const int nu = *n_unique;
+  for (int s = blockIdx.x; s < nu; s += gridDim.x) {
+    const int64_t j = item_of[s];
+    for (int64_t h = threadIdx.x; h < H; h += blockDim.x) dense[j * ld + h] = rows[(int64_t)s * H + h];
+  }
+}
+
+}  // namespace hvae
+
+using namespace hvae;
+
+// ------------------------------------------------------------- launchers ---
+#define HVAE_NV_DISPATCH(H, KERNEL_CALL)                                        \
+  do {                                                                          \
+    const int64_t nv_ = cdiv((H), 256);                                         \
+    if (nv_ <= 1) { constexpr int NV = 1; KERNEL_CALL; }                        \
+    else if (nv_ <= 2) { constexpr int NV = 2; KERNEL_CALL; }                   \
+    else if (nv_ <= 4) { constexpr int NV = 4; KERNEL_CALL; }                   \
+    else if (nv_ <= 8) { constexpr int NV = 8; KERNEL_CALL; }                   \
+    else HVAE_FAIL(HVAE_ERR_UNSUPPORTED, "hidden width %lld > 2048 unsupported", (long long)(H)); \
+  } while (0)
+
+static int check_hidden(int64_t H) {
+  HVAE_REQUIRE(H > 0 && H % 4 == 0, "hidden width %lld must be a positive multiple of 4",
+               (long long)H);
+  return HVAE_OK;
+}
+
+extern "C" int hvae_encoder_fwd(const hvae_csr_batch* x, const float* w1t, const float* b1,
+                                const float* ln_w, const float* ln_b, int64_t H, float p_drop,
+                                const float* drop_mult, uint64_t seed, const int64_t* step_dev,
+                                int train, float* h_out, float* xhat_out, float* rstd_out,
+                                void* stream) {
+  HVAE_REQUIRE(x && x->row_ptr && w1t && b1 && ln_w && ln_b && h_out, "hvae_encoder_fwd: null arg");
+  if (int rc = check_hidden(H)) return rc;
+  if (x->nb == 0) return HVAE_OK;
+  HVAE_REQUIRE(x->col_idx && x->vals, "hvae_encoder_fwd: null CSR arrays");
+  const float scale = (p_drop < 1.f) ? 1.0f / (1.0f - p_drop) : 0.f;
+  const unsigned grid = (unsigned)cdiv(x->nb, 4);
+  HVAE_NV_DISPATCH(H, (k_encoder_sparse_fwd<NV><<<grid, 256, 0, as_stream(stream)>>>(
+                          x->row_ptr, x->col_idx, x->vals, x->rows, x->rows_offset, x->nb, w1t, b1, ln_w, ln_b, H,
+                          p_drop, scale, drop_mult, seed, step_dev, train, h_out, xhat_out,
+                          rstd_out)));
+  HVAE_LAUNCH_CHECK("k_encoder_sparse_fwd");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_ln_gelu_drop_fwd(const float* a, const float* ln_w, const float* ln_b,
+                                     int64_t nb, int64_t H, float p_drop, const float* drop_mult,
+                                     uint64_t seed, const int64_t* step_dev, uint32_t layer,
+                                     int train, float* h_out, float* xhat_out, float* rstd_out,
+                                     void* stream) {
+  HVAE_REQUIRE(a && ln_w && ln_b && h_out, "hvae_ln_gelu_drop_fwd: null arg");
+  if (int rc = check_hidden(H)) return rc;
+  if (nb == 0) return HVAE_OK;
+  const float scale = (p_drop < 1.f) ? 1.0f / (1.0f - p_drop) : 0.f;
+  const unsigned grid = (unsigned)cdiv(nb, 4);
+  HVAE_NV_DISPATCH(H, (k_ln_gelu_drop_fwd<NV><<<grid, 256, 0, as_stream(stream)>>>(
+                          a, ln_w, ln_b, nb, H, p_drop, scale, drop_mult, seed, step_dev,
+                          kTagEncDrop + layer, train, h_out, xhat_out, rstd_out)));
+  HVAE_LAUNCH_CHECK("k_ln_gelu_drop_fwd");
+  return HVAE_OK;
+}
+
+extern "C" size_t hvae_ln_gelu_drop_bwd_workspace(int64_t nb, int64_t H) {
+  return (size_t)cdiv(nb, kLnBwdRows) * 2 * (size_t)H * sizeof(float);
+}
+
+extern "C" int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const float* rstd,
+                                     const float* ln_w, const float* ln_b, int64_t nb, int64_t H,
+                                     float p_drop, const float* drop_mult, uint64_t seed,
+                                     const int64_t* step_dev, uint32_t layer, int train, float* da,
+                                     float* d_ln_w, float* d_ln_b, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  HVAE_REQUIRE(dh && xhat && rstd && ln_w && ln_b && da && d_ln_w && d_ln_b,
+               "hvae_ln_gelu_drop_bwd: null arg");
+  if (int rc = check_hidden(H)) return rc;
+  if (nb == 0) {
+    HVAE_HIP(hipMemsetAsync(d_ln_w, 0, H * sizeof(float), as_stream(stream)));
+    HVAE_HIP(hipMemsetAsync(d_ln_b, 0, H * sizeof(float), as_stream(stream)));
+    return HVAE_OK;
+  }
+  const size_t need = hvae_ln_gelu_drop_bwd_workspace(nb, H);
+  if (ws_bytes < need || !ws)
+    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_ln_gelu_drop_bwd: workspace %zu < %zu", ws_bytes, need);
+  const float scale = (p_drop < 1.f) ? 1.0f / (1.0f - p_drop) : 0.f;
+  const int64_t nparts = cdiv(nb, kLnBwdRows);
+  const size_t lds = (size_t)8 * H * sizeof(float);
+  HVAE_REQUIRE(lds <= 64 * 1024, "hvae_ln_gelu_drop_bwd: H too large");
+  HVAE_NV_DISPATCH(H, (k_ln_gelu_drop_bwd<NV><<<(unsigned)nparts, 256, lds, as_stream(stream)>>>(
+                          dh, xhat, rstd, ln_w, ln_b, nb, H, p_drop, scale, drop_mult, seed,
+                          step_dev, kTagEncDrop + layer, train, da, (float*)ws)));
+  HVAE_LAUNCH_CHECK("k_ln_gelu_drop_bwd");
+  k_ln_part_reduce<<<(unsigned)cdiv(2 * H, 256), 256, 0, as_stream(stream)>>>((const float*)ws, nparts,
+                                                                               H, d_ln_w, d_ln_b);
+  HVAE_LAUNCH_CHECK("k_ln_part_reduce");
+  return HVAE_OK;
+}
+
+extern "C" size_t hvae_dense_to_csr_workspace(int64_t, int64_t) { return 0; }
+
+extern "C" int hvae_dense_to_csr(const float* x, int64_t B, int64_t N, int64_t* row_ptr,
+                                 int32_t* col_idx, float* vals, int64_t cap, void*, size_t,
+                                 void* stream) {
+  HVAE_REQUIRE(row_ptr && B >= 0 && N >= 0, "hvae_dense_to_csr: bad args");
+  HVAE_REQUIRE(N < (int64_t)INT32_MAX, "hvae_dense_to_csr: N too large");
+  if (B == 0) {
+    HVAE_HIP(hipMemsetAsync(row_ptr, 0, sizeof(int64_t), as_stream(stream)));
+    return HVAE_OK;
+  }
+  HVAE_REQUIRE(x && col_idx && vals, "hvae_dense_to_csr: null arg");
+  k_dense_row_count<<<(unsigned)B, 256, 0, as_stream(stream)>>>(x, N, row_ptr);
+  HVAE_LAUNCH_CHECK("k_dense_row_count");
+  k_scan_i64<<<1, 1024, 0, as_stream(stream)>>>(row_ptr, B);
+  HVAE_LAUNCH_CHECK("k_scan_i64");
+  k_dense_compact<<<(unsigned)B, 256, 0, as_stream(stream)>>>(x, N, row_ptr, col_idx, vals, cap);
+  HVAE_LAUNCH_CHECK("k_dense_compact");
+  return HVAE_OK;
+}
+
+extern "C" size_t hvae_w1_rowgrad_workspace(int64_t n_items) {
+  return (size_t)2 * cdiv(n_items, kScanItemsPerBlock) * sizeof(int64_t);
+}
+
+extern "C" int hvae_w1_rowgrad(const hvae_csr_batch* x, const float* da, int64_t H,
+                               const hvae_rowgrad* rg, void* ws, size_t ws_bytes, void* stream) {
+  HVAE_REQUIRE(x && x->row_ptr && da && rg, "hvae_w1_rowgrad: null arg");
+  HVAE_REQUIRE(rg->cnt && rg->slot_of && rg->item_of && rg->seg_off && rg->fill &&
+                   rg->contrib_row && rg->contrib_val && rg->rows && rg->n_unique,
+               "hvae_w1_rowgrad: null rowgrad buffer");
+  if (int rc = check_hidden(H)) return rc;
+  HVAE_REQUIRE(rg->n_items == x->n_items, "hvae_w1_rowgrad: n_items mismatch");
+  const int64_t N = x->n_items;
+  const size_t need = hvae_w1_rowgrad_workspace(N);
+  if (ws_bytes < need || !ws)
+    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_w1_rowgrad: workspace %zu < %zu", ws_bytes, need);
+  hipStream_t st = as_stream(stream);
+  if (x->nb == 0) {
+    HVAE_HIP(hipMemsetAsync(rg->n_unique, 0, sizeof(int32_t), st));
+    return HVAE_OK;
+  }
+  const unsigned rgrid = (unsigned)cdiv(x->nb, 4);
+  k_rg_count<<<rgrid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->rows, x->rows_offset, x->nb, rg->cnt);
+  HVAE_LAUNCH_CHECK("k_rg_count");
+  const int64_t nblk = cdiv(N, kScanItemsPerBlock);
+  int64_t* blocktot = (int64_t*)ws;
+  k_rg_scan1<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, blocktot);
+  HVAE_LAUNCH_CHECK("k_rg_scan1");
+  k_rg_scan2<<<1, 1024, 0, st>>>(blocktot, nblk, rg->n_unique, rg->seg_off, rg->cap);
+  HVAE_LAUNCH_CHECK("k_rg_scan2");
+  k_rg_scan3<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, blocktot, rg->slot_of, rg->item_of,
+                                             rg->seg_off, rg->cap);
+  HVAE_LAUNCH_CHECK("k_rg_scan3");
+  k_rg_scatter<<<rgrid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->vals, x->rows, x->rows_offset, x->nb, rg->slot_of,
+                                      rg->seg_off, rg->fill, rg->contrib_row, rg->contrib_val,
+                                      rg->cap);
+  HVAE_LAUNCH_CHECK("k_rg_scatter");
+  const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(rg->cap, 2048));
+  k_rg_rows<<<sgrid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->fill, rg->contrib_row,
+                                   rg->contrib_val, da, H, rg->rows);
+  HVAE_LAUNCH_CHECK("k_rg_rows");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_rowgrad_to_dense(const hvae_rowgrad* rg, int64_t H, float* dense, int64_t ld,
+                                     void* stream) {
+  HVAE_REQUIRE(rg && dense && ld >= H, "hvae_rowgrad_to_dense: bad args");
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(rg->cap, 2048));
+  k_rg_to_dense<<<grid, 256, 0, as_stream(stream)>>>(rg->n_unique, rg->item_of, rg->rows, H, dense, ld);
+  HVAE_LAUNCH_CHECK("k_rg_to_dense");
+  return HVAE_OK;
+}

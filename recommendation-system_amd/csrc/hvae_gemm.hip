@@ -1,0 +1,331 @@
+// hvae_gemm.hip -- small dense fp32 GEMMs of the path on the exact-f32 MFMA.
+//
+// v_mfma_f32_16x16x4_f32: one f32 A and one f32 B per lane, 4 accumulators,
+// numerically a k-ordered fmaf chain (no reduced-precision fast path exists
+// on gfx950, and none is wanted: these GEMMs carry the fp32 parity of the
+// reference's nn.Linear layers). Tile 64x64x16 per 4-wave block, 32x32 per
+// wave (2x2 MFMA tiles); operands staged through LDS k-major so both
+// fragments are conflict-free ds_read_b32; split-K through a caller
+// workspace with a deterministic reduction for the tall-skinny weight
+// gradients (K = batch).
+#include <algorithm>
+
+#include "hvae_common.h"
+
+namespace hvae {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int GBM = 64, GBN = 64, GBK = 16;
+constexpr int GLDA = GBM + 16;  // row stride of the k-major LDS images (see header)
+constexpr int GLDB = GBN + 16;
+
+struct EpiArgs {
+  int kind;
+  const float* bias;
+  float* pre_out;
+  const float* pre_in;
+  float p_drop, scale;
+  const float* drop_mult;
+  uint64_t seed;
+  const int64_t* step_dev;
+  uint32_t tag;
+  int train;
+};
+
+__device__ __forceinline__ float epi_apply(const EpiArgs& ep, int64_t step, int64_t row, int64_t col,
+                                           int64_t N, int64_t ldc, float c) {
+  switch (ep.kind) {
+    case HVAE_EPI_BIAS:
+      return c + ep.bias[col];
+    case HVAE_EPI_BIAS_GELU_DROP: {
+      const float pre = c + (ep.bias ? ep.bias[col] : 0.f);
+      ep.pre_out[row * ldc + col] = pre;
+      const float g = gelu_f(pre);
+      return ep.train ? g * dropout_mult(ep.p_drop, ep.scale, ep.drop_mult, (uint64_t)(row * N + col),
+                                      ep.seed, step, ep.tag)
+                      : g;
+    }
+    case HVAE_EPI_GELU_DROP_BWD: {
+      const float dm = ep.train ? dropout_mult(ep.p_drop, ep.scale, ep.drop_mult,
+                                            (uint64_t)(row * N + col), ep.seed, step, ep.tag)
+                                : 1.f;
+      return c * dm * gelu_grad_f(ep.pre_in[row * ldc + col]);
+    }
+    case HVAE_EPI_DROP_BWD: {
+      const float dm = ep.train ? dropout_mult(ep.p_drop, ep.scale, ep.drop_mult,
+                                            (uint64_t)(row * N + col), ep.seed, step, ep.tag)
+                                : 1.f;
+      return c * dm;
+    }
+    default:
+      return c;
+  }
+}
+
+// Load 4 consecutive elements along the contiguous dimension, zero-filled
+// outside [0, lim); vectorised when the caller proved 16-B alignment.
+__device__ __forceinline__ float4 load4(const float* __restrict__ p, int64_t idx, int64_t lim, bool vec) {
+  if (vec && idx + 3 < lim) return *reinterpret_cast<const float4*>(p);
+  float4 r;
+  r.x = (idx + 0 < lim) ? p[0] : 0.f;
+  r.y = (idx + 1 < lim) ? p[1] : 0.f;
+  r.z = (idx + 2 < lim) ? p[2] : 0.f;
+  r.w = (idx + 3 < lim) ? p[3] : 0.f;
+  return r;
+}
+
+template <bool TA, bool TB>
+__global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t K, int64_t k_per_split,
+                                                  float alpha, const float* __restrict__ A, int64_t lda,
+                                                  const float* __restrict__ B, int64_t ldb, float beta,
+                                                  float* __restrict__ C, int64_t ldc,
+                                                  float* __restrict__ slab, EpiArgs ep, bool vec_a,
+                                                  bool vec_b) {
+  __shared__ __attribute__((aligned(16))) float sA[GBK * GLDA];
+  __shared__ __attribute__((aligned(16))) float sB[GBK * GLDB];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
+  const int64_t kb = (int64_t)blockIdx.z * k_per_split;
+  const int64_t ke = min(K, kb + k_per_split);
+  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 ra, rb;
+  auto gload = [&](int64_t k0) {
+    if (!TA) {  // A[m][k] at A[m*lda + k]
+      const int64_t m = m0 + (t >> 2), k = k0 + (t & 3) * 4;
+      ra = (m < M) ? load4(A + m * lda + k, k, ke, vec_a) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {    // A[m][k] at A[k*lda + m]
+      const int64_t k = k0 + (t >> 4), m = m0 + (t & 15) * 4;
+      ra = (k < ke) ? load4(A + k * lda + m, m, M, vec_a) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (!TB) {  // B[k][n] at B[k*ldb + n]
+      const int64_t k = k0 + (t >> 4), n = n0 + (t & 15) * 4;
+      rb = (k < ke) ? load4(B + k * ldb + n, n, N, vec_b) : make_float4(0.f, 0.f, 0.f, 0.f);
+    } else {    // B[k][n] at B[n*ldb + k]
+      const int64_t n = n0 + (t >> 2), k = k0 + (t & 3) * 4;
+      rb = (n < N) ? load4(B + n * ldb + k, k, ke, vec_b) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto lstore = [&]() {
+    if (!TA) {
+      const int m = t >> 2, k = (t & 3) * 4;
+      sA[(k + 0) * GLDA + m] = ra.x; sA[(k + 1) * GLDA + m] = ra.y;
+      sA[(k + 2) * GLDA + m] = ra.z; sA[(k + 3) * GLDA + m] = ra.w;
+    } else {
+      const int k = t >> 4, m = (t & 15) * 4;
+      *reinterpret_cast<float4*>(&sA[k * GLDA + m]) = ra;
+    }
+    if (!TB) {
+      const int k = t >> 4, n = (t & 15) * 4;
+      *reinterpret_cast<float4*>(&sB[k * GLDB + n]) = rb;
+    } else {
+      const int n = t >> 2, k = (t & 3) * 4;
+      sB[(k + 0) * GLDB + n] = rb.x; sB[(k + 1) * GLDB + n] = rb.y;
+      sB[(k + 2) * GLDB + n] = rb.z; sB[(k + 3) * GLDB + n] = rb.w;
+    }
+  };
+
+  if (kb < ke) {
+    gload(kb);
+    lstore();
+    __syncthreads();
+    for (int64_t k0 = kb; k0 < ke; k0 += GBK) {
+      const bool more = k0 + GBK < ke;
+      if (more) gload(k0 + GBK);
+#pragma unroll
+      for (int kk = 0; kk < GBK / 4; ++kk) {
+        const int kr = 4 * kk + (lane >> 4);
+        float af[2], bfr[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = sA[kr * GLDA + wm + i * 16 + (lane & 15)];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bfr[j] = sB[kr * GLDB + wn + j * 16 + (lane & 15)];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+      if (more) {
+        lstore();
+        __syncthreads();
+      }
+    }
+  }
+
+  const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP) ? load_step(ep.step_dev) : 0;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
+        const int64_t col = n0 + wn + j * 16 + (lane & 15);
+        if (row >= M || col >= N) continue;
+        if (slab) {
+          slab[((int64_t)blockIdx.z * M + row) * N + col] = acc[i][j][r];
+        } else {
+          float c = alpha * acc[i][j][r];
+          if (beta != 0.f) c += beta * C[row * ldc + col];
+          C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
+        }
+      }
+}
+
+__global__ void k_gemm_splitk_reduce(int64_t M, int64_t N, int splits, float alpha,
+                                     const float* __restrict__ slab, float beta, float* __restrict__ C,
+                                     int64_t ldc, EpiArgs ep) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * N) return;
+  const int64_t row = i / N, col = i % N;
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * M * N + i];
+  float c = alpha * s;
+  if (beta != 0.f) c += beta * C[row * ldc + col];
+  const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP) ? load_step(ep.step_dev) : 0;
+  C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
+}
+
+// ---------------------------------------------------------------- colsum ---
+__global__ void k_colsum_part(const float* __restrict__ X, int64_t M, int64_t N, int64_t ldx,
+                              int64_t rows_per_part, float beta, float* __restrict__ out,
+                              bool direct) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_part, r1 = min(M, r0 + rows_per_part);
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += X[r * ldx + n];
+  if (direct) {
+    out[n] = (beta != 0.f ? beta * out[n] : 0.f) + s;
+  } else {
+    out[(int64_t)blockIdx.y * N + n] = s;
+  }
+}
+
+__global__ void k_colsum_final(const float* __restrict__ part, int64_t P, int64_t N, float beta,
+                               float* __restrict__ out) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int64_t p = 0; p < P; ++p) s += part[p * N + n];
+  out[n] = (beta != 0.f ? beta * out[n] : 0.f) + s;
+}
+
+static int gemm_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = cdiv(M, GBM) * cdiv(N, GBN);
+  if (tiles >= 128 || K < 256) return 1;
+  int64_t s = std::min<int64_t>(cdiv(256, tiles), K / 128);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 32));
+}
+
+static int colsum_parts(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 64), 64)); }
+
+}  // namespace hvae
+
+using namespace hvae;
+
+extern "C" size_t hvae_gemm_f32_workspace(int64_t M, int64_t N, int64_t K) {
+  const int s = gemm_splits(M, N, K);
+  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+}
+
+extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
+                             const float* A, int64_t lda, const float* B, int64_t ldb, float beta,
+                             float* C, int64_t ldc, const hvae_epilogue* epi, void* ws,
+                             size_t ws_bytes, void* stream) {
+  HVAE_REQUIRE(M >= 0 && N >= 0 && K >= 0 && C, "hvae_gemm_f32: bad shape / null C");
+  HVAE_REQUIRE(ldc >= N, "hvae_gemm_f32: ldc < N");
+  HVAE_REQUIRE(M < (1ll << 31) / GBM * GBM && N < (1ll << 31), "hvae_gemm_f32: too large");
+  if (M == 0 || N == 0) return HVAE_OK;
+  HVAE_REQUIRE(K == 0 || (A && B), "hvae_gemm_f32: null A/B");
+  HVAE_REQUIRE(trans_a ? lda >= M : lda >= K, "hvae_gemm_f32: bad lda");
+  HVAE_REQUIRE(trans_b ? ldb >= K : ldb >= N, "hvae_gemm_f32: bad ldb");
+  EpiArgs ep{};
+  ep.kind = HVAE_EPI_NONE;
+  if (epi) {
+    ep.kind = epi->kind;
+    ep.bias = epi->bias;
+    ep.pre_out = epi->pre_out;
+    ep.pre_in = epi->pre_in;
+    ep.p_drop = epi->p_drop;
+    ep.scale = (epi->p_drop < 1.f) ? 1.0f / (1.0f - epi->p_drop) : 0.f;
+    ep.drop_mult = epi->drop_mult;
+    ep.seed = epi->seed;
+    ep.step_dev = epi->step_dev;
+    ep.tag = epi->tag;
+    ep.train = epi->train;
+    HVAE_REQUIRE(ep.kind >= 0 && ep.kind <= HVAE_EPI_DROP_BWD, "hvae_gemm_f32: bad epilogue");
+    HVAE_REQUIRE(ep.kind != HVAE_EPI_BIAS || ep.bias, "hvae_gemm_f32: BIAS without bias");
+    HVAE_REQUIRE(ep.kind != HVAE_EPI_BIAS_GELU_DROP || ep.pre_out, "hvae_gemm_f32: no pre_out");
+    HVAE_REQUIRE(ep.kind != HVAE_EPI_GELU_DROP_BWD || ep.pre_in, "hvae_gemm_f32: no pre_in");
+  }
+  hipStream_t st = as_stream(stream);
+  int splits = gemm_splits(M, N, K);
+  if (splits > 1) {
+    const int64_t fit = ws ? (int64_t)(ws_bytes / ((size_t)M * N * sizeof(float))) : 0;
+    splits = (int)std::min<int64_t>(splits, fit);
+    if (splits < 2) splits = 1;
+  }
+  int64_t kps = K;
+  if (splits > 1) {
+    kps = cdiv(cdiv(K, splits), GBK) * GBK;
+    splits = (int)cdiv(K, kps);
+  }
+  const bool vec_a = (((uintptr_t)A) % 16 == 0) && (lda % 4 == 0);
+  const bool vec_b = (((uintptr_t)B) % 16 == 0) && (ldb % 4 == 0);
+  dim3 grid((unsigned)cdiv(N, GBN), (unsigned)cdiv(M, GBM), (unsigned)std::max(splits, 1));
+  float* slab = splits > 1 ? (float*)ws : nullptr;
+  if (K == 0) kps = 0;
+#define HVAE_GEMM_CALL(TA_, TB_)                                                                  \
+  k_gemm_f32<TA_, TB_><<<grid, 256, 0, st>>>(M, N, K, kps, alpha, A, lda, B, ldb, beta, C, ldc,   \
+                                             slab, ep, vec_a, vec_b)
+  if (!trans_a && !trans_b) HVAE_GEMM_CALL(false, false);
+  else if (!trans_a && trans_b) HVAE_GEMM_CALL(false, true);
+  else if (trans_a && !trans_b) HVAE_GEMM_CALL(true, false);
+  else HVAE_GEMM_CALL(true, true);
+#undef HVAE_GEMM_CALL
+  HVAE_LAUNCH_CHECK("k_gemm_f32");
+  if (slab) {
+    k_gemm_splitk_reduce<<<(unsigned)cdiv(M * N, 256), 256, 0, st>>>(M, N, splits, alpha, slab, beta,
+                                                                     C, ldc, ep);
+    HVAE_LAUNCH_CHECK("k_gemm_splitk_reduce");
+  }
+  return HVAE_OK;
+}
+
+extern "C" size_t hvae_colsum_workspace(int64_t M, int64_t N) {
+  const int P = colsum_parts(M);
+  return P > 1 ? (size_t)P * N * sizeof(float) : 0;
+}
+
+extern "C" int hvae_colsum(const float* X, int64_t M, int64_t N, int64_t ldx, float beta, float* out,
+                           void* ws, size_t ws_bytes, void* stream) {
+  HVAE_REQUIRE(out && N >= 0 && M >= 0 && ldx >= N, "hvae_colsum: bad args");
+  if (N == 0) return HVAE_OK;
+  hipStream_t st = as_stream(stream);
+  if (M == 0) {
+    if (beta == 0.f) HVAE_HIP(hipMemsetAsync(out, 0, N * sizeof(float), st));
+    return HVAE_OK;
+  }
+  HVAE_REQUIRE(X, "hvae_colsum: null X");
+  int P = colsum_parts(M);
+  if (P > 1 && (!ws || ws_bytes < (size_t)P * N * sizeof(float))) P = 1;
+  const int64_t rpp = cdiv(M, P);
+  dim3 grid((unsigned)cdiv(N, 256), (unsigned)P);
+  k_colsum_part<<<grid, 256, 0, st>>>(X, M, N, ldx, rpp, beta, P > 1 ? (float*)ws : out, P == 1);
+  HVAE_LAUNCH_CHECK("k_colsum_part");
+  if (P > 1) {
+    k_colsum_final<<<(unsigned)cdiv(N, 256), 256, 0, st>>>((const float*)ws, P, N, beta, out);
+    HVAE_LAUNCH_CHECK("k_colsum_final");
+  }
+  return HVAE_OK;
+}

@@ -1,0 +1,192 @@
+// hvae_optim.hip -- gradient clipping and Adam (K13, K14 of SURVEY §2.1).
+//
+// Reference: VAETrainer.train_epoch (src/ml/train.py:88-92):
+//   torch.nn.utils.clip_grad_norm_(params, max_norm=5.0); optimizer.step()
+// with optim.Adam(lr, betas=(0.9, 0.999), eps=1e-8, weight_decay) built at
+// src/ml/train.py:63. Both passes are HBM-bound; the clip multiplier never
+// takes its own pass over the gradients -- it is read by the Adam launches.
+#include <algorithm>
+
+#include "hvae_common.h"
+
+namespace hvae {
+
+constexpr int kNormBlocks = 512;
+
+// Sum of squares over a dense flat gradient + the valid rows of a row-sparse
+// one, fixed grid, per-block partials in fp64 (deterministic).
+__global__ void __launch_bounds__(256) k_sqnorm_part(const float* __restrict__ g, int64_t n,
+                                                     const float* __restrict__ rows,
+                                                     const int32_t* __restrict__ n_unique, int64_t H,
+                                                     double* __restrict__ part) {
+  __shared__ double red[4];
+  const int64_t nr = rows ? (int64_t)(*n_unique) * H : 0;
+  const int64_t tot = n + nr;
+  double s = 0.0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
+    const float v = (i < n) ? g[i] : rows[i - n];
+    s += (double)v * (double)v;
+  }
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ void __launch_bounds__(256) k_sqnorm_final(const double* __restrict__ part, int nparts,
+                                                      float max_norm, float* __restrict__ norm_out,
+                                                      float* __restrict__ coef_out) {
+  __shared__ double red[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float norm = (float)sqrt(((red[0] + red[1]) + red[2]) + red[3]);
+    // torch: clip_coef = max_norm / (total_norm + 1e-6); clamp(max=1.0)
+    const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);
+    if (norm_out) *norm_out = norm;
+    *coef_out = coef;
+  }
+}
+
+struct AdamK {
+  float lr_over_bc1;  // step_size
+  float bc2_sqrt;
+  float omb1, b2, omb2, eps, wd;
+};
+
+// torch.optim.Adam single-tensor arithmetic, element-wise.
+__device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamK& k) {
+  if (k.wd != 0.f) g = g + k.wd * p;
+  m = m + k.omb1 * (g - m);                 // exp_avg.lerp_(grad, 1 - beta1)
+  v = v * k.b2 + k.omb2 * g * g;            // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
+  const float denom = sqrtf(v) / k.bc2_sqrt + k.eps;
+  p = p - k.lr_over_bc1 * (m / denom);      // param.addcdiv_(exp_avg, denom, -step_size)
+}
+
+struct AdamArgs {
+  double lr, b1, b2, eps, wd;
+  const int64_t* step_dev;
+  const float* coef_dev;
+};
+
+__device__ __forceinline__ AdamK adam_consts(const AdamArgs& a) {
+  const int64_t t = load_step(a.step_dev) + 1;
+  const double bc1 = 1.0 - pow(a.b1, (double)t);
+  const double bc2 = 1.0 - pow(a.b2, (double)t);
+  AdamK k;
+  k.lr_over_bc1 = (float)(a.lr / bc1);
+  k.bc2_sqrt = (float)sqrt(bc2);
+  k.omb1 = (float)(1.0 - a.b1);
+  k.b2 = (float)a.b2;
+  k.omb2 = (float)(1.0 - a.b2);
+  k.eps = (float)a.eps;
+  k.wd = (float)a.wd;
+  return k;
+}
+
+__global__ void __launch_bounds__(256) k_adam_dense(AdamArgs a, float* __restrict__ p, float* __restrict__ m,
+                                                    float* __restrict__ v, const float* __restrict__ g,
+                                                    int64_t n) {
+  const AdamK k = adam_consts(a);
+  const float coef = a.coef_dev ? *a.coef_dev : 1.f;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float pp = p[i], mm = m[i], vv = v[i];
+    adam_elem(pp, mm, vv, g[i] * coef, k);
+    p[i] = pp; m[i] = mm; v[i] = vv;
+  }
+}
+
+// Item-major W1t [N, H] with a row-sparse gradient: float4 per thread.
+__global__ void __launch_bounds__(256) k_adam_rows(AdamArgs a, float* __restrict__ p, float* __restrict__ m,
+                                                   float* __restrict__ v, const float* __restrict__ rows,
+                                                   const int32_t* __restrict__ slot_of,
+                                                   const int32_t* __restrict__ item_of,
+                                                   const int32_t* __restrict__ n_unique, int64_t N,
+                                                   int64_t H) {
+  const AdamK k = adam_consts(a);
+  const float coef = a.coef_dev ? *a.coef_dev : 1.f;
+  const int nu = *n_unique;
+  const int64_t H4 = H / 4, n4 = N * H4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const int64_t row = i / H4, c = i - row * H4;
+    const int s = slot_of[row];
+    float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (s >= 0 && s < nu && item_of[s] == (int32_t)row) {
+      gv = *reinterpret_cast<const float4*>(rows + (int64_t)s * H + 4 * c);
+      gv.x *= coef; gv.y *= coef; gv.z *= coef; gv.w *= coef;
+    }
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_elem(pp.x, mm.x, vv.x, gv.x, k);
+    adam_elem(pp.y, mm.y, vv.y, gv.y, k);
+    adam_elem(pp.z, mm.z, vv.z, gv.z, k);
+    adam_elem(pp.w, mm.w, vv.w, gv.w, k);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+}
+
+static AdamArgs to_args(const hvae_adam* c) {
+  AdamArgs a;
+  a.lr = c->lr; a.b1 = c->beta1; a.b2 = c->beta2; a.eps = c->eps; a.wd = c->weight_decay;
+  a.step_dev = c->step_dev;
+  a.coef_dev = c->coef_dev;
+  return a;
+}
+
+}  // namespace hvae
+
+using namespace hvae;
+
+extern "C" size_t hvae_clip_grad_norm_workspace(int64_t, int64_t, int64_t) {
+  return kNormBlocks * sizeof(double);
+}
+
+extern "C" int hvae_clip_grad_norm(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg,
+                                   int64_t H, float max_norm, float* norm_out, float* coef_out,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  HVAE_REQUIRE(coef_out && n_dense >= 0 && (n_dense == 0 || g_dense), "hvae_clip_grad_norm: bad args");
+  HVAE_REQUIRE(!rg || (rg->rows && rg->n_unique && H > 0), "hvae_clip_grad_norm: bad rowgrad");
+  if (!ws || ws_bytes < kNormBlocks * sizeof(double))
+    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_clip_grad_norm: workspace too small");
+  hipStream_t st = as_stream(stream);
+  k_sqnorm_part<<<kNormBlocks, 256, 0, st>>>(g_dense, n_dense, rg ? rg->rows : nullptr,
+                                             rg ? rg->n_unique : nullptr, H, (double*)ws);
+  HVAE_LAUNCH_CHECK("k_sqnorm_part");
+  k_sqnorm_final<<<1, 256, 0, st>>>((const double*)ws, kNormBlocks, max_norm, norm_out, coef_out);
+  HVAE_LAUNCH_CHECK("k_sqnorm_final");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_adam_dense(const hvae_adam* cfg, float* p, float* m, float* v, const float* g,
+                               int64_t n, void* stream) {
+  HVAE_REQUIRE(cfg && (n == 0 || (p && m && v && g)), "hvae_adam_dense: bad args");
+  if (n == 0) return HVAE_OK;
+  const int64_t blocks = std::min<int64_t>(cdiv(n, 256), 4096);
+  k_adam_dense<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(to_args(cfg), p, m, v, g, n);
+  HVAE_LAUNCH_CHECK("k_adam_dense");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_adam_rows(const hvae_adam* cfg, float* p, float* m, float* v, const hvae_rowgrad* rg,
+                              int64_t N, int64_t H, void* stream) {
+  HVAE_REQUIRE(cfg && p && m && v && rg && rg->rows && rg->slot_of && rg->item_of && rg->n_unique,
+               "hvae_adam_rows: bad args");
+  HVAE_REQUIRE(H % 4 == 0 && ((uintptr_t)p % 16) == 0 && ((uintptr_t)m % 16) == 0 &&
+                   ((uintptr_t)v % 16) == 0,
+               "hvae_adam_rows: H %% 4 and 16-B alignment required");
+  if (N == 0) return HVAE_OK;
+  const int64_t blocks = std::min<int64_t>(cdiv(N * H / 4, 256), 8192);
+  k_adam_rows<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(to_args(cfg), p, m, v, rg->rows, rg->slot_of,
+                                                             rg->item_of, rg->n_unique, N, H);
+  HVAE_LAUNCH_CHECK("k_adam_rows");
+  return HVAE_OK;
+}

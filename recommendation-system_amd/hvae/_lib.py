@@ -1,0 +1,156 @@
+"""ctypes binding of libhvae.so (the C ABI declared in include/hvae.h).
+
+The shared library is built in-tree by ``make -C recommendation-system_amd lib``
+(``hipcc --offload-arch=gfx950``). There is deliberately no fallback: if the
+library is missing, or the tensors are not on a HIP device, every op raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import torch
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("HVAE_LIB", _HERE / "libhvae.so"))
+
+HVAE_OK = 0
+HVAE_F32 = 0
+HVAE_BF16 = 1
+
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU_DROP, EPI_GELU_DROP_BWD, EPI_DROP_BWD = range(5)
+
+# Philox stream tags (csrc/hvae_common.h)
+TAG_ENC_DROP = 0x100
+TAG_PROJ_DROP = 0x200
+TAG_EPS = 0x300
+
+vp = C.c_void_p
+i64 = C.c_int64
+u64 = C.c_uint64
+f32 = C.c_float
+f64 = C.c_double
+sz = C.c_size_t
+cint = C.c_int
+u32 = C.c_uint32
+
+
+class CsrBatch(C.Structure):
+    _fields_ = [("row_ptr", vp), ("col_idx", vp), ("vals", vp), ("rows", vp), ("rows_offset", vp), ("nb", i64),
+                ("n_items", i64)]
+
+
+class RowGrad(C.Structure):
+    _fields_ = [
+        ("cnt", vp), ("slot_of", vp), ("item_of", vp), ("seg_off", vp), ("fill", vp),
+        ("contrib_row", vp), ("contrib_val", vp), ("rows", vp), ("n_unique", vp),
+        ("cap", i64), ("n_items", i64),
+    ]
+
+
+class Epilogue(C.Structure):
+    _fields_ = [
+        ("kind", cint), ("bias", vp), ("pre_out", vp), ("pre_in", vp), ("p_drop", f32),
+        ("drop_mult", vp), ("seed", u64), ("step_dev", vp), ("tag", u32), ("train", cint),
+    ]
+
+
+class Adam(C.Structure):
+    _fields_ = [
+        ("lr", f64), ("beta1", f64), ("beta2", f64), ("eps", f64), ("weight_decay", f64),
+        ("step_dev", vp), ("coef_dev", vp),
+    ]
+
+
+P = C.POINTER
+# name -> (restype, argtypes); mirrors include/hvae.h one to one.
+SIGNATURES = {
+    "hvae_version": (cint, []),
+    "hvae_last_error": (cint, [C.c_char_p, sz]),
+    "hvae_dense_to_csr": (cint, [vp, i64, i64, vp, vp, vp, i64, vp, sz, vp]),
+    "hvae_dense_to_csr_workspace": (sz, [i64, i64]),
+    "hvae_encoder_fwd": (cint, [P(CsrBatch), vp, vp, vp, vp, i64, f32, vp, u64, vp, cint, vp, vp, vp, vp]),
+    "hvae_ln_gelu_drop_fwd": (cint, [vp, vp, vp, i64, i64, f32, vp, u64, vp, u32, cint, vp, vp, vp, vp]),
+    "hvae_ln_gelu_drop_bwd": (cint, [vp, vp, vp, vp, vp, i64, i64, f32, vp, u64, vp, u32, cint, vp, vp, vp,
+                                     vp, sz, vp]),
+    "hvae_ln_gelu_drop_bwd_workspace": (sz, [i64, i64]),
+    "hvae_w1_rowgrad": (cint, [P(CsrBatch), vp, i64, P(RowGrad), vp, sz, vp]),
+    "hvae_w1_rowgrad_workspace": (sz, [i64]),
+    "hvae_rowgrad_to_dense": (cint, [P(RowGrad), i64, vp, i64, vp]),
+    "hvae_gemm_f32": (cint, [cint, cint, i64, i64, i64, f32, vp, i64, vp, i64, f32, vp, i64, P(Epilogue), vp,
+                             sz, vp]),
+    "hvae_gemm_f32_workspace": (sz, [i64, i64, i64]),
+    "hvae_colsum": (cint, [vp, i64, i64, i64, f32, vp, vp, sz, vp]),
+    "hvae_colsum_workspace": (sz, [i64, i64]),
+    "hvae_reparam_kl_fwd": (cint, [vp, vp, i64, i64, i64, cint, vp, u64, vp, vp, vp, vp, vp]),
+    "hvae_reparam_kl_bwd": (cint, [vp, vp, vp, i64, vp, i64, i64, f32, cint, vp, vp, i64, vp]),
+    "hvae_decoder_fwd": (cint, [cint, vp, i64, vp, vp, i64, i64, i64, vp, vp, vp, sz, vp]),
+    "hvae_decoder_workspace": (sz, [cint, i64, i64, i64]),
+    "hvae_decoder_supported": (cint, [cint, i64]),
+    "hvae_row_norm_max": (cint, [cint, vp, i64, i64, vp, vp]),
+    "hvae_decoder_bwd": (cint, [P(CsrBatch), vp, i64, vp, i64, vp, vp, f32, vp, vp, vp]),
+    "hvae_nll_rows_fwd": (cint, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),
+    "hvae_nll_rows_bwd": (cint, [vp, i64, vp, i64, vp, i64, i64, f32, vp, i64, vp]),
+    "hvae_loss_finalize": (cint, [vp, vp, i64, f32, vp, vp, vp]),
+    "hvae_clip_grad_norm": (cint, [vp, i64, P(RowGrad), i64, f32, vp, vp, vp, sz, vp]),
+    "hvae_clip_grad_norm_workspace": (sz, [i64, i64, i64]),
+    "hvae_adam_dense": (cint, [P(Adam), vp, vp, vp, vp, i64, vp]),
+    "hvae_adam_rows": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp]),
+    "hvae_counter_add": (cint, [vp, i64, vp]),
+    "hvae_score_candidates": (cint, [vp, i64, vp, vp, i64, vp, i64, i64, vp, vp]),
+    "hvae_rank_first": (cint, [vp, i64, i64, vp, vp]),
+    "hvae_topk": (cint, [vp, i64, i64, i64, P(CsrBatch), i64, vp, vp, vp]),
+    "hvae_cast_bf16": (cint, [vp, vp, i64, vp]),
+}
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libhvae.so once (after torch, so the HIP runtime torch loaded is reused)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(
+                f"libhvae.so not found at {LIB_PATH}; build it with "
+                f"`make -C {LIB_PATH.parent.parent} lib` (hipcc --offload-arch=gfx950). "
+                "There is no CPU fallback for the HybridVAE MI355X path."
+            )
+        L = C.CDLL(str(LIB_PATH), mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.hvae_version() != 1:
+            raise RuntimeError(f"libhvae ABI version {L.hvae_version()} != 1")
+        _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    buf = C.create_string_buffer(1024)
+    lib().hvae_last_error(buf, 1024)
+    return buf.value.decode(errors="replace")
+
+
+def check(rc: int, what: str) -> None:
+    if rc != HVAE_OK:
+        raise RuntimeError(f"{what} failed (rc={rc}): {last_error()}")
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_hip(*ts: torch.Tensor | None) -> None:
+    for t in ts:
+        if t is not None and t.device.type != "cuda":
+            raise RuntimeError(
+                "HybridVAE MI355X path: tensors must live on the HIP device (torch 'cuda' on ROCm); "
+                f"got {t.device}. There is no CPU fallback."
+            )

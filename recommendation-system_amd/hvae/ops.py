@@ -1,0 +1,370 @@
+"""Tensor-level wrappers of the libhvae C ABI.
+
+Every function here takes/returns torch tensors that live on the HIP device,
+checks shapes, allocates outputs, and launches on the current stream. They
+are the building blocks of the module-API autograd path (hvae/autograd.py)
+and of the parity tests. The fused trainer (hvae/executor.py) calls the C ABI
+directly with preallocated buffers instead.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from . import _lib
+from ._lib import (CsrBatch, Epilogue, RowGrad, Adam, check, lib, ptr, require_hip, stream_of)
+
+_WS: dict[torch.device, torch.Tensor] = {}
+
+
+def workspace(device: torch.device, nbytes: int) -> torch.Tensor:
+    """Per-device scratch buffer, grown on demand (never shrunk)."""
+    nbytes = max(int(nbytes), 256)
+    ws = _WS.get(device)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes + (nbytes >> 2), dtype=torch.uint8, device=device)
+        _WS[device] = ws
+    return ws
+
+
+class Csr:
+    """A device CSR batch view (keeps the tensors alive for the C struct)."""
+
+    def __init__(self, row_ptr: torch.Tensor, col_idx: torch.Tensor, vals: torch.Tensor, n_items: int,
+                 rows: torch.Tensor | None = None, nb: int | None = None,
+                 rows_offset: torch.Tensor | None = None):
+        require_hip(row_ptr, col_idx, vals, rows)
+        assert row_ptr.dtype == torch.int64 and col_idx.dtype == torch.int32 and vals.dtype == torch.float32
+        assert rows is None or rows.dtype == torch.int32
+        self.row_ptr, self.col_idx, self.vals, self.rows = row_ptr, col_idx, vals, rows
+        self.rows_offset = rows_offset
+        self.n_items = int(n_items)
+        self.nb = int(nb if nb is not None else (rows.numel() if rows is not None else row_ptr.numel() - 1))
+        self.struct = CsrBatch(ptr(row_ptr), ptr(col_idx), ptr(vals), ptr(rows), ptr(rows_offset), self.nb,
+                               self.n_items)
+
+    @property
+    def ref(self):
+        return C.byref(self.struct)
+
+
+def csr_from_scipy(mat, device) -> Csr:
+    """Upload a scipy.sparse CSR matrix (float values, summed duplicates kept) to the device."""
+    mat = mat.tocsr()
+    mat.sum_duplicates()
+    row_ptr = torch.as_tensor(mat.indptr.astype("int64"), device=device)
+    col = torch.as_tensor(mat.indices.astype("int32"), device=device)
+    vals = torch.as_tensor(mat.data.astype("float32"), device=device)
+    return Csr(row_ptr, col, vals, mat.shape[1])
+
+
+def dense_to_csr(x: torch.Tensor) -> Csr:
+    """Dense [B, N] (any values, zeros skipped) -> device CSR of the nonzeros."""
+    require_hip(x)
+    x = x.contiguous().float()
+    B, N = x.shape
+    cap = max(B * N, 1)
+    row_ptr = torch.empty(B + 1, dtype=torch.int64, device=x.device)
+    col = torch.empty(cap, dtype=torch.int32, device=x.device)
+    vals = torch.empty(cap, dtype=torch.float32, device=x.device)
+    check(lib().hvae_dense_to_csr(ptr(x), B, N, ptr(row_ptr), ptr(col), ptr(vals), cap, None, 0,
+                                  stream_of(x)), "hvae_dense_to_csr")
+    return Csr(row_ptr, col, vals, N)
+
+
+# ------------------------------------------------------------------ encoder --
+def encoder_fwd(x: Csr, w1t, b1, ln_w, ln_b, p_drop: float, train: bool, seed: int, step=None,
+                drop_mult=None, save=True):
+    H = w1t.shape[1]
+    dev = w1t.device
+    require_hip(w1t, b1, ln_w, ln_b, drop_mult)
+    h = torch.empty(x.nb, H, device=dev)
+    xhat = torch.empty(x.nb, H, device=dev) if save else None
+    rstd = torch.empty(x.nb, device=dev) if save else None
+    check(lib().hvae_encoder_fwd(x.ref, ptr(w1t), ptr(b1), ptr(ln_w), ptr(ln_b), H, float(p_drop), ptr(drop_mult),
+                                 seed, ptr(step), int(train), ptr(h), ptr(xhat), ptr(rstd), stream_of(w1t)),
+          "hvae_encoder_fwd")
+    return h, xhat, rstd
+
+
+def ln_gelu_drop_fwd(a, ln_w, ln_b, p_drop, train, seed, layer, step=None, drop_mult=None, save=True):
+    require_hip(a, ln_w, ln_b, drop_mult)
+    a = a.contiguous()
+    nb, H = a.shape
+    h = torch.empty_like(a)
+    xhat = torch.empty_like(a) if save else None
+    rstd = torch.empty(nb, device=a.device) if save else None
+    check(lib().hvae_ln_gelu_drop_fwd(ptr(a), ptr(ln_w), ptr(ln_b), nb, H, float(p_drop), ptr(drop_mult), seed,
+                                      ptr(step), layer, int(train), ptr(h), ptr(xhat), ptr(rstd), stream_of(a)),
+          "hvae_ln_gelu_drop_fwd")
+    return h, xhat, rstd
+
+
+def ln_gelu_drop_bwd(dh, xhat, rstd, ln_w, ln_b, p_drop, train, seed, layer, step=None, drop_mult=None):
+    require_hip(dh, xhat, rstd, ln_w, ln_b)
+    dh = dh.contiguous()
+    nb, H = dh.shape
+    da = torch.empty_like(dh)
+    dw = torch.empty(H, device=dh.device)
+    db = torch.empty(H, device=dh.device)
+    need = lib().hvae_ln_gelu_drop_bwd_workspace(nb, H)
+    ws = workspace(dh.device, need)
+    check(lib().hvae_ln_gelu_drop_bwd(ptr(dh), ptr(xhat), ptr(rstd), ptr(ln_w), ptr(ln_b), nb, H, float(p_drop),
+                                      ptr(drop_mult), seed, ptr(step), layer, int(train), ptr(da), ptr(dw), ptr(db),
+                                      ptr(ws), ws.numel(), stream_of(dh)), "hvae_ln_gelu_drop_bwd")
+    return da, dw, db
+
+
+class RowGradBuffers:
+    """Device buffers of the row-sparse first-layer weight gradient."""
+
+    def __init__(self, n_items: int, H: int, cap: int, device):
+        i32 = dict(dtype=torch.int32, device=device)
+        self.cnt = torch.zeros(n_items, **i32)
+        self.slot_of = torch.full((n_items,), -1, **i32)
+        self.item_of = torch.zeros(cap, **i32)
+        self.seg_off = torch.zeros(cap + 1, **i32)
+        self.fill = torch.zeros(cap, **i32)
+        self.contrib_row = torch.zeros(cap, **i32)
+        self.contrib_val = torch.zeros(cap, dtype=torch.float32, device=device)
+        self.rows = torch.zeros(cap, H, dtype=torch.float32, device=device)
+        self.n_unique = torch.zeros(1, **i32)
+        self.cap, self.n_items, self.H = cap, n_items, H
+        self.struct = RowGrad(ptr(self.cnt), ptr(self.slot_of), ptr(self.item_of), ptr(self.seg_off), ptr(self.fill),
+                              ptr(self.contrib_row), ptr(self.contrib_val), ptr(self.rows), ptr(self.n_unique), cap,
+                              n_items)
+        self.ws = torch.empty(max(int(lib().hvae_w1_rowgrad_workspace(n_items)), 256), dtype=torch.uint8,
+                              device=device)
+
+    @property
+    def ref(self):
+        return C.byref(self.struct)
+
+
+def w1_rowgrad(x: Csr, da: torch.Tensor, rg: RowGradBuffers) -> None:
+    require_hip(da)
+    check(lib().hvae_w1_rowgrad(x.ref, ptr(da), da.shape[1], rg.ref, ptr(rg.ws), rg.ws.numel(), stream_of(da)),
+          "hvae_w1_rowgrad")
+
+
+def rowgrad_to_dense(rg: RowGradBuffers, out: torch.Tensor) -> None:
+    """out: zero-filled [N, ld] item-major buffer."""
+    check(lib().hvae_rowgrad_to_dense(rg.ref, rg.H, ptr(out), out.stride(0), stream_of(out)),
+          "hvae_rowgrad_to_dense")
+
+
+# --------------------------------------------------------------------- GEMM --
+def _as_operand(t: torch.Tensor):
+    """(base tensor, transposed?, ld) such that t == base or t == base.T with base row-major."""
+    if t.dim() != 2:
+        raise ValueError("GEMM operands must be 2-D")
+    if t.stride(1) == 1 and t.stride(0) >= max(t.shape[1], 1):
+        return t, False, t.stride(0)
+    if t.stride(0) == 1 and t.stride(1) >= max(t.shape[0], 1):
+        return t, True, t.stride(1)
+    return t.contiguous(), False, t.shape[1]
+
+
+def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, alpha=1.0, beta=0.0, epi=None):
+    """out[M,N] = alpha * a[M,K] @ b[K,N] + beta * out (fp32 MFMA), then the epilogue.
+
+    a and b may be transposed views (e.g. a Linear weight .t()); no copies are made.
+    """
+    require_hip(a, b)
+    M, K = a.shape
+    K2, N = b.shape
+    assert K == K2, f"gemm shape mismatch {a.shape} @ {b.shape}"
+    A, ta, lda = _as_operand(a)
+    B, tb, ldb = _as_operand(b)
+    if out is None:
+        out = torch.empty(M, N, device=a.device)
+        beta = 0.0
+    assert out.stride(1) == 1
+    need = lib().hvae_gemm_f32_workspace(M, N, K)
+    ws = workspace(a.device, need) if need else None
+    check(lib().hvae_gemm_f32(int(ta), int(tb), M, N, K, float(alpha), ptr(A), lda, ptr(B), ldb, float(beta),
+                              ptr(out), out.stride(0), C.byref(epi) if epi is not None else None, ptr(ws),
+                              ws.numel() if ws is not None else 0, stream_of(a)), "hvae_gemm_f32")
+    return out
+
+
+def epilogue(kind, bias=None, pre_out=None, pre_in=None, p_drop=0.0, drop_mult=None, seed=0, step=None,
+             tag=0, train=False) -> Epilogue:
+    return Epilogue(kind, ptr(bias), ptr(pre_out), ptr(pre_in), float(p_drop), ptr(drop_mult), int(seed), ptr(step),
+                    int(tag), int(train))
+
+
+def colsum(x: torch.Tensor, out: torch.Tensor | None = None, beta=0.0):
+    require_hip(x)
+    assert x.stride(1) == 1
+    M, N = x.shape
+    if out is None:
+        out = torch.empty(N, device=x.device)
+        beta = 0.0
+    need = lib().hvae_colsum_workspace(M, N)
+    ws = workspace(x.device, need)
+    check(lib().hvae_colsum(ptr(x), M, N, x.stride(0), float(beta), ptr(out), ptr(ws), ws.numel(), stream_of(x)),
+          "hvae_colsum")
+    return out
+
+
+# ------------------------------------------------------------------- latent --
+def reparam_kl_fwd(mu, logvar, train: bool, seed: int, step=None, eps_in=None):
+    require_hip(mu, logvar, eps_in)
+    assert mu.stride(1) == 1 and logvar.stride(1) == 1 and mu.stride(0) == logvar.stride(0)
+    nb, L = mu.shape
+    z = torch.empty(nb, L, device=mu.device)
+    eps = torch.empty(nb, L, device=mu.device) if train else None
+    kl_rows = torch.empty(nb, device=mu.device)
+    check(lib().hvae_reparam_kl_fwd(ptr(mu), ptr(logvar), mu.stride(0), nb, L, int(train), ptr(eps_in), seed,
+                                    ptr(step), ptr(z), ptr(eps), ptr(kl_rows), stream_of(mu)), "hvae_reparam_kl_fwd")
+    return z, eps, kl_rows
+
+
+def reparam_kl_bwd(dz, mu, logvar, eps, kl_scale: float, train: bool, dmu=None, dlv=None):
+    nb, L = mu.shape
+    if dmu is None:
+        dmu = torch.empty(nb, L, device=mu.device)
+        dlv = torch.empty(nb, L, device=mu.device)
+    check(lib().hvae_reparam_kl_bwd(ptr(dz), ptr(mu), ptr(logvar), mu.stride(0), ptr(eps), nb, L, float(kl_scale),
+                                    int(train), ptr(dmu), ptr(dlv), dmu.stride(0), stream_of(mu)),
+          "hvae_reparam_kl_bwd")
+    return dmu, dlv
+
+
+# ------------------------------------------------------------------ decoder --
+def row_norm_max(E: torch.Tensor) -> torch.Tensor:
+    require_hip(E)
+    out = torch.empty(1, device=E.device)
+    dtype = _lib.HVAE_BF16 if E.dtype == torch.bfloat16 else _lib.HVAE_F32
+    check(lib().hvae_row_norm_max(dtype, ptr(E), E.shape[0], E.shape[1], ptr(out), stream_of(E)),
+          "hvae_row_norm_max")
+    return out
+
+
+def cast_bf16(x: torch.Tensor) -> torch.Tensor:
+    require_hip(x)
+    x = x.contiguous()
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    check(lib().hvae_cast_bf16(ptr(x), ptr(y), x.numel(), stream_of(x)), "hvae_cast_bf16")
+    return y
+
+
+def decoder_supported(dtype: int, D: int) -> bool:
+    return bool(lib().hvae_decoder_supported(dtype, D))
+
+
+def decoder_fwd(U: torch.Tensor, E: torch.Tensor, enorm: torch.Tensor | None, with_o: bool = True):
+    """(lse [nb], O [nb, D] or None) of the streaming decoder; E fp32 or bf16."""
+    require_hip(U, E)
+    assert U.stride(1) == 1
+    nb, D = U.shape
+    N = E.shape[0]
+    dtype = _lib.HVAE_BF16 if E.dtype == torch.bfloat16 else _lib.HVAE_F32
+    lse = torch.empty(nb, device=U.device)
+    O = torch.empty(nb, D, device=U.device) if with_o else None
+    need = lib().hvae_decoder_workspace(dtype, nb, N, D)
+    ws = workspace(U.device, need)
+    check(lib().hvae_decoder_fwd(dtype, ptr(U), U.stride(0), ptr(E), ptr(enorm), nb, N, D, ptr(lse), ptr(O),
+                                 ptr(ws), ws.numel(), stream_of(U)), "hvae_decoder_fwd")
+    return lse, O
+
+
+def decoder_bwd(x: Csr, U, E32, lse, O, grad_scale: float, want_du: bool = True):
+    nb, D = U.shape
+    recon_rows = torch.empty(nb, device=U.device)
+    dU = torch.empty(nb, D, device=U.device) if want_du else None
+    check(lib().hvae_decoder_bwd(x.ref, ptr(U), U.stride(0), ptr(E32), D, ptr(lse), ptr(O), float(grad_scale),
+                                 ptr(recon_rows), ptr(dU), stream_of(U)), "hvae_decoder_bwd")
+    return recon_rows, dU
+
+
+def nll_rows_fwd(S, X):
+    require_hip(S, X)
+    nb, N = S.shape
+    lse = torch.empty(nb, device=S.device)
+    recon = torch.empty(nb, device=S.device)
+    check(lib().hvae_nll_rows_fwd(ptr(S), S.stride(0), ptr(X), X.stride(0), nb, N, ptr(lse), ptr(recon),
+                                  stream_of(S)), "hvae_nll_rows_fwd")
+    return lse, recon
+
+
+def nll_rows_bwd(S, X, lse, scale: float):
+    nb, N = S.shape
+    dS = torch.empty(nb, N, device=S.device)
+    check(lib().hvae_nll_rows_bwd(ptr(S), S.stride(0), ptr(X), X.stride(0), ptr(lse), nb, N, float(scale), ptr(dS),
+                                  dS.stride(0), stream_of(S)), "hvae_nll_rows_bwd")
+    return dS
+
+
+def loss_finalize(recon_rows, kl_rows, beta: float, out3=None, accum3=None):
+    nb = recon_rows.numel()
+    if out3 is None:
+        out3 = torch.empty(3, device=recon_rows.device)
+    check(lib().hvae_loss_finalize(ptr(recon_rows), ptr(kl_rows), nb, float(beta), ptr(out3), ptr(accum3),
+                                   stream_of(recon_rows)), "hvae_loss_finalize")
+    return out3
+
+
+# ---------------------------------------------------------------- optimiser --
+def clip_grad_norm(g_dense: torch.Tensor | None, rg: RowGradBuffers | None, max_norm: float,
+                   norm_out=None, coef_out=None):
+    dev = (g_dense if g_dense is not None else rg.rows).device
+    if norm_out is None:
+        norm_out = torch.empty(1, device=dev)
+        coef_out = torch.empty(1, device=dev)
+    n = g_dense.numel() if g_dense is not None else 0
+    need = lib().hvae_clip_grad_norm_workspace(n, rg.cap if rg else 0, rg.H if rg else 0)
+    ws = workspace(dev, need)
+    check(lib().hvae_clip_grad_norm(ptr(g_dense), n, rg.ref if rg else None, rg.H if rg else 0, float(max_norm),
+                                    ptr(norm_out), ptr(coef_out), ptr(ws), ws.numel(), torch.cuda.current_stream(
+                                        dev).cuda_stream), "hvae_clip_grad_norm")
+    return norm_out, coef_out
+
+
+def adam_config(lr, betas, eps, weight_decay, step_dev, coef_dev=None) -> Adam:
+    return Adam(float(lr), float(betas[0]), float(betas[1]), float(eps), float(weight_decay), ptr(step_dev),
+                ptr(coef_dev))
+
+
+def adam_dense(cfg: Adam, p, m, v, g):
+    check(lib().hvae_adam_dense(C.byref(cfg), ptr(p), ptr(m), ptr(v), ptr(g), p.numel(), stream_of(p)),
+          "hvae_adam_dense")
+
+
+def adam_rows(cfg: Adam, p, m, v, rg: RowGradBuffers):
+    N, H = p.shape
+    check(lib().hvae_adam_rows(C.byref(cfg), ptr(p), ptr(m), ptr(v), rg.ref, N, H, stream_of(p)), "hvae_adam_rows")
+
+
+def counter_add(c: torch.Tensor, delta: int = 1):
+    check(lib().hvae_counter_add(ptr(c), int(delta), stream_of(c)), "hvae_counter_add")
+
+
+# --------------------------------------------------------------------- eval --
+def score_candidates(U, user_row, E32, cand):
+    require_hip(U, user_row, E32, cand)
+    R, Cn = cand.shape
+    scores = torch.empty(R, Cn, device=U.device)
+    check(lib().hvae_score_candidates(ptr(U), U.stride(0), ptr(user_row), ptr(E32), E32.shape[1], ptr(cand), R, Cn,
+                                      ptr(scores), stream_of(U)), "hvae_score_candidates")
+    return scores
+
+
+def rank_first(scores):
+    R, Cn = scores.shape
+    rank = torch.empty(R, dtype=torch.int32, device=scores.device)
+    check(lib().hvae_rank_first(ptr(scores), R, Cn, ptr(rank), stream_of(scores)), "hvae_rank_first")
+    return rank
+
+
+def topk(scores: torch.Tensor, k: int, exclude: Csr | None = None):
+    """Exact top-k per row (score desc, ties -> larger index first); masks `exclude` in place."""
+    require_hip(scores)
+    R, N = scores.shape
+    idx = torch.empty(R, k, dtype=torch.int32, device=scores.device)
+    val = torch.empty(R, k, device=scores.device)
+    check(lib().hvae_topk(ptr(scores), R, N, scores.stride(0), exclude.ref if exclude is not None else None, k,
+                          ptr(idx), ptr(val), stream_of(scores)), "hvae_topk")
+    return idx, val
