@@ -1,0 +1,306 @@
+"""Per-kernel parity of libhvae (through the C ABI) against CPU fp32 references.
+
+Each HIP op is compared with a plain fp32 PyTorch-on-CPU statement of the same
+op (the oracle's building blocks). Integer/index work is checked bit-exact.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from gen import synth_csr, synth_embeddings
+from oracle import ref_cpu as R
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops(hip_device):
+    from hvae import ops
+    return ops
+
+
+def _maxrel(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / max(b.abs().max().item(), 1e-30))
+
+
+# ------------------------------------------------------------------ GEMM ---
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (7, 13, 5), (64, 64, 64), (130, 67, 300), (37, 384, 4096),
+                                   (384, 384, 4096), (4096, 128, 512)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+def test_gemm_f32(ops, hip_device, M, N, K, ta, tb):
+    g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn(M, K, generator=g)
+    B = torch.randn(K, N, generator=g)
+    Ad = (A.t().contiguous().to(hip_device).t() if ta else A.to(hip_device))
+    Bd = (B.t().contiguous().to(hip_device).t() if tb else B.to(hip_device))
+    C0 = torch.randn(M, N, generator=g)
+    out = C0.to(hip_device).clone()
+    ops.gemm(Ad, Bd, out=out, alpha=0.5, beta=0.25)
+    ref = 0.5 * (A.double() @ B.double()) + 0.25 * C0.double()
+    assert _maxrel(out, ref) < 2e-5 * max(1.0, math.sqrt(K) / 8)
+
+
+def test_gemm_epilogues(ops, hip_device):
+    from hvae import _lib
+    g = torch.Generator().manual_seed(3)
+    M, N, K = 50, 70, 33
+    A, W, bias = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)
+    mult = ((torch.rand(M, N, generator=g) >= 0.3).float() / 0.7)
+    Ad, Wd, bd, md = (t.to(hip_device) for t in (A, W, bias, mult))
+    pre = torch.empty(M, N, device=hip_device)
+    epi = ops.epilogue(_lib.EPI_BIAS_GELU_DROP, bias=bd, pre_out=pre, p_drop=0.3, drop_mult=md, train=True)
+    out = ops.gemm(Ad, Wd.t(), epi=epi)
+    ref_pre = A @ W.t() + bias
+    assert _maxrel(pre, ref_pre) < 1e-5
+    assert _maxrel(out, R.gelu(ref_pre) * mult) < 1e-5
+    # backward epilogue: c * mult * gelu'(pre)
+    G, W2 = torch.randn(M, 40, generator=g), torch.randn(40, N, generator=g)
+    epi2 = ops.epilogue(_lib.EPI_GELU_DROP_BWD, pre_in=pre, p_drop=0.3, drop_mult=md, train=True)
+    out2 = ops.gemm(G.to(hip_device), W2.to(hip_device), epi=epi2)
+    x = ref_pre.clone().requires_grad_(True)
+    (R.gelu(x) * mult * (G @ W2)).sum().backward()
+    assert _maxrel(out2, x.grad) < 1e-5
+
+
+def test_colsum(ops, hip_device):
+    X = torch.randn(3000, 77)
+    out = ops.colsum(X.to(hip_device))
+    assert _maxrel(out, X.double().sum(0)) < 1e-5
+
+
+# --------------------------------------------------------------- encoder ---
+def _csr_dev(ops, X, device):
+    return ops.csr_from_scipy(X, device)
+
+
+@pytest.mark.parametrize("H", [64, 128, 512, 600])
+def test_encoder_fwd_bwd(ops, hip_device, H):
+    X = synth_csr(37, 500, lam=6.0, seed=1)
+    x = torch.as_tensor(X.toarray(), dtype=torch.float32)
+    g = torch.Generator().manual_seed(H)
+    W1 = torch.randn(H, 500, generator=g) * 0.05
+    b1, lw, lb = torch.randn(H, generator=g), 1 + 0.1 * torch.randn(H, generator=g), torch.randn(H, generator=g)
+    mult = ((torch.rand(37, H, generator=g) >= 0.25).float() / 0.75)
+    xd = _csr_dev(ops, X, hip_device)
+    w1t = W1.t().contiguous().to(hip_device)
+    dv = lambda t: t.to(hip_device)
+    h, xhat, rstd = ops.encoder_fwd(xd, w1t, dv(b1), dv(lw), dv(lb), 0.25, True, 0, drop_mult=dv(mult))
+    a = (x @ W1.t() + b1).requires_grad_(True)
+    ref = R.gelu(R.layer_norm(a, lw, lb)) * mult
+    assert _maxrel(h, ref) < 2e-5
+    # backward through LN/GELU/dropout + row-sparse W1 grad
+    dh = torch.randn(37, H, generator=g)
+    lw_ = lw.clone().requires_grad_(True)
+    lb_ = lb.clone().requires_grad_(True)
+    (R.gelu(R.layer_norm(a, lw_, lb_)) * mult * dh).sum().backward()
+    da, dlw, dlb = ops.ln_gelu_drop_bwd(dv(dh), xhat, rstd, dv(lw), dv(lb), 0.25, True, 0, 0, drop_mult=dv(mult))
+    assert _maxrel(da, a.grad) < 5e-5
+    assert _maxrel(dlw, lw_.grad) < 5e-5 and _maxrel(dlb, lb_.grad) < 5e-5
+    rg = ops.RowGradBuffers(500, H, int(X.nnz), hip_device)
+    ops.w1_rowgrad(xd, da, rg)
+    dense = torch.zeros(500, H, device=hip_device)
+    ops.rowgrad_to_dense(rg, dense)
+    ref_w1 = (a.grad.t() @ x).t()  # [N, H]
+    assert _maxrel(dense, ref_w1) < 5e-5
+    # slots are the touched items in ascending order, bit-exact
+    nu = int(rg.n_unique.item())
+    touched = np.unique(X.indices)
+    assert nu == len(touched)
+    np.testing.assert_array_equal(rg.item_of[:nu].cpu().numpy(), touched)
+    assert int(rg.cnt.abs().sum()) == 0 and int(rg.fill.abs().sum()) == 0
+    # determinism: a second run is bitwise identical
+    rows1 = rg.rows[:nu].clone()
+    ops.w1_rowgrad(xd, da, rg)
+    assert torch.equal(rows1, rg.rows[:nu])
+
+
+def test_philox_dropout_statistics(ops, hip_device):
+    X = synth_csr(256, 300, seed=2)
+    xd = _csr_dev(ops, X, hip_device)
+    H = 512
+    w1t = torch.randn(300, H, device=hip_device) * 0.05
+    one, zero = torch.ones(H, device=hip_device), torch.zeros(H, device=hip_device)
+    step = torch.zeros(1, dtype=torch.int64, device=hip_device)
+    h0, _, _ = ops.encoder_fwd(xd, w1t, zero, one, zero, 0.0, True, 7, step=step)
+    h1, _, _ = ops.encoder_fwd(xd, w1t, zero, one, zero, 0.3, True, 7, step=step)
+    keep = (h1 != 0) | (h0 == 0)
+    frac = keep.float().mean().item()
+    assert abs(frac - 0.7) < 0.01
+    kept = h1[(h1 != 0)]
+    assert torch.allclose(kept, h0[(h1 != 0)] / 0.7, rtol=1e-5, atol=1e-6)
+    # same (seed, step) -> same mask; next step -> a different one
+    h2, _, _ = ops.encoder_fwd(xd, w1t, zero, one, zero, 0.3, True, 7, step=step)
+    assert torch.equal(h1, h2)
+    step += 1
+    h3, _, _ = ops.encoder_fwd(xd, w1t, zero, one, zero, 0.3, True, 7, step=step)
+    assert not torch.equal(h1, h3)
+
+
+def test_dense_to_csr(ops, hip_device):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(9, 1000, generator=g) * (torch.rand(9, 1000, generator=g) < 0.05)
+    x[3] = 0
+    c = ops.dense_to_csr(x.to(hip_device))
+    rp = c.row_ptr.cpu().numpy()
+    nz = [np.nonzero(r)[0] for r in x.numpy()]
+    np.testing.assert_array_equal(np.diff(rp), [len(z) for z in nz])
+    np.testing.assert_array_equal(c.col_idx[: rp[-1]].cpu().numpy(), np.concatenate(nz))
+    np.testing.assert_array_equal(c.vals[: rp[-1]].cpu().numpy(), x.numpy()[x.numpy() != 0])
+
+
+# ---------------------------------------------------------------- latent ---
+def test_reparam_kl(ops, hip_device):
+    g = torch.Generator().manual_seed(5)
+    B, L = 33, 64
+    heads = torch.randn(B, 2 * L, generator=g)
+    eps = torch.randn(B, L, generator=g)
+    hd = heads.to(hip_device)
+    mu, lv = hd[:, :L], hd[:, L:]
+    z, eps_o, kl_rows = ops.reparam_kl_fwd(mu, lv, True, 0, eps_in=eps.to(hip_device))
+    m_, l_ = heads[:, :L].clone().requires_grad_(True), heads[:, L:].clone().requires_grad_(True)
+    zr = m_ + eps * torch.exp(0.5 * l_)
+    klr = -0.5 * (1 + l_ - m_ ** 2 - l_.exp()).sum(1)
+    assert _maxrel(z, zr) < 1e-6 and _maxrel(kl_rows, klr) < 1e-5
+    dz = torch.randn(B, L, generator=g)
+    beta = 0.2
+    (zr * dz).sum().add(beta * klr.sum() / B).backward()
+    dmu, dlv = ops.reparam_kl_bwd(dz.to(hip_device), mu, lv, eps_o, beta / B, True)
+    assert _maxrel(dmu, m_.grad) < 1e-5 and _maxrel(dlv, l_.grad) < 1e-5
+
+
+# --------------------------------------------------------------- decoder ---
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("nb,N,D", [(3, 50, 384), (64, 890, 384), (200, 12101, 384), (130, 1000, 128),
+                                    (17, 333, 64), (300, 5000, 256)])
+def test_decoder(ops, hip_device, dtype, nb, N, D):
+    E = torch.as_tensor(synth_embeddings(N, D, seed=N))
+    g = torch.Generator().manual_seed(nb)
+    U = torch.randn(nb, D, generator=g) * 3.0
+    Ed = E.to(hip_device)
+    Ek = ops.cast_bf16(Ed) if dtype == "bf16" else Ed
+    if dtype == "bf16":
+        Ur, Er = U.bfloat16().float(), Ek.float().cpu()
+    else:
+        Ur, Er = U, E
+    enorm = ops.row_norm_max(Ek)
+    lse, O = ops.decoder_fwd(U.to(hip_device), Ek, enorm)
+    S = Ur.double() @ Er.double().t()
+    lse_ref = torch.logsumexp(S, 1)
+    O_ref = torch.softmax(S, 1) @ Er.double()
+    tol = 1e-5 if dtype == "f32" else 2e-3
+    assert (lse.double().cpu() - lse_ref).abs().max() < tol * max(1.0, lse_ref.abs().max().item())
+    assert _maxrel(O, O_ref) < (1e-5 if dtype == "f32" else 1e-2)
+    lse2, _ = ops.decoder_fwd(U.to(hip_device), Ek, enorm, with_o=False)
+    assert torch.allclose(lse2, lse, rtol=0, atol=1e-5)
+
+
+def test_decoder_large_norm_fixup(ops, hip_device):
+    """|u| in the hundreds: the fixed-offset bf16 path must flag and fix underflowing users."""
+    N, D = 4000, 128
+    E = torch.as_tensor(synth_embeddings(N, D, seed=9))
+    g = torch.Generator().manual_seed(1)
+    U = torch.randn(8, D, generator=g)
+    U = U / U.norm(dim=1, keepdim=True) * torch.tensor([1, 10, 50, 100, 200, 400, 800, 1500.0])[:, None]
+    Ek = ops.cast_bf16(E.to(hip_device))
+    lse, O = ops.decoder_fwd(U.to(hip_device), Ek, ops.row_norm_max(Ek))
+    S = U.bfloat16().double() @ Ek.float().cpu().double().t()
+    assert torch.isfinite(lse).all() and torch.isfinite(O).all()
+    rel = ((lse.double().cpu() - torch.logsumexp(S, 1)).abs() / torch.logsumexp(S, 1).abs().clamp(min=1))
+    assert rel.max() < 2e-3
+
+
+def test_decoder_bwd_sparse(ops, hip_device):
+    X = synth_csr(40, 700, lam=5.0, seed=4)
+    x = torch.as_tensor(X.toarray(), dtype=torch.float32)
+    D = 384
+    E = torch.as_tensor(synth_embeddings(700, D, seed=3))
+    U = torch.randn(40, D) * 2
+    xd = ops.csr_from_scipy(X, hip_device)
+    Ed = E.to(hip_device)
+    lse, O = ops.decoder_fwd(U.to(hip_device), Ed, None)
+    recon_rows, dU = ops.decoder_bwd(xd, U.to(hip_device), Ed, lse, O, 1.0 / 40)
+    u_ = U.clone().requires_grad_(True)
+    S = u_ @ E.t()
+    rr = -(x * torch.log_softmax(S, 1)).sum(1)
+    rr.mean().backward()
+    assert _maxrel(recon_rows, rr) < 1e-5
+    assert _maxrel(dU, u_.grad) < 1e-4
+
+
+def test_nll_rows(ops, hip_device):
+    g = torch.Generator().manual_seed(2)
+    S = torch.randn(6, 77, generator=g) * 3
+    X = torch.randn(6, 77, generator=g)  # reference tests feed randn inputs
+    lse, rr = ops.nll_rows_fwd(S.to(hip_device), X.to(hip_device))
+    s_ = S.clone().requires_grad_(True)
+    ref = -(X * torch.log_softmax(s_, 1)).sum(1)
+    ref.mean().backward()
+    assert _maxrel(rr, ref) < 1e-5
+    dS = ops.nll_rows_bwd(S.to(hip_device), X.to(hip_device), lse, 1.0 / 6)
+    assert _maxrel(dS, s_.grad) < 1e-5
+
+
+# ------------------------------------------------------------- optimiser ---
+def test_clip_and_adam(ops, hip_device):
+    g = torch.Generator().manual_seed(4)
+    N, H = 300, 64
+    small = torch.randn(5000, generator=g)
+    X = synth_csr(20, N, seed=5)
+    xd = ops.csr_from_scipy(X, hip_device)
+    da = torch.randn(20, H, generator=g)
+    rg = ops.RowGradBuffers(N, H, int(X.nnz), hip_device)
+    ops.w1_rowgrad(xd, da.to(hip_device), rg)
+    dense = torch.zeros(N, H, device=hip_device)
+    ops.rowgrad_to_dense(rg, dense)
+    w1g = dense.cpu()
+    total_ref = math.sqrt(float((small.double() ** 2).sum() + (w1g.double() ** 2).sum()))
+    norm, coef = ops.clip_grad_norm(small.to(hip_device), rg, 5.0)
+    assert abs(norm.item() - total_ref) < 1e-5 * total_ref
+    assert abs(coef.item() - min(1.0, 5.0 / (total_ref + 1e-6))) < 1e-6
+    # Adam: dense segment and row-sparse W1t, 3 steps, vs the oracle's torch.optim.Adam restatement
+    step = torch.zeros(1, dtype=torch.int64, device=hip_device)
+    cfg = ops.adam_config(1e-3, (0.9, 0.999), 1e-8, 0.0, step, coef)
+    p_s, p_w = torch.randn(5000, generator=g), torch.randn(N, H, generator=g)
+    ps_d, pw_d = p_s.to(hip_device), p_w.to(hip_device)
+    ms, vs = torch.zeros_like(ps_d), torch.zeros_like(ps_d)
+    mw, vw = torch.zeros_like(pw_d), torch.zeros_like(pw_d)
+    rms, rvs, rmw, rvw = (torch.zeros_like(t) for t in (p_s, p_s, p_w, p_w))
+    c = coef.item()
+    for t in range(1, 4):
+        ops.adam_dense(cfg, ps_d, ms, vs, small.to(hip_device))
+        ops.adam_rows(cfg, pw_d, mw, vw, rg)
+        ops.counter_add(step, 1)
+        R.adam_update(p_s, small * c, rms, rvs, t)
+        R.adam_update(p_w, w1g * c, rmw, rvw, t)
+    assert _maxrel(ps_d, p_s) < 1e-6 and _maxrel(pw_d, p_w) < 1e-6
+    assert _maxrel(mw, rmw) < 1e-6 and _maxrel(vw, rvw) < 1e-5
+
+
+# ------------------------------------------------------------------ eval ---
+def test_candidates_rank_topk(ops, hip_device):
+    N, D, R_ = 2000, 384, 50
+    E = torch.as_tensor(synth_embeddings(N, D, seed=8))
+    g = torch.Generator().manual_seed(8)
+    U = torch.randn(R_, D, generator=g)
+    cand = torch.stack([torch.randperm(N, generator=g)[:100] for _ in range(R_)]).int()
+    Ed = E.to(hip_device)
+    sc = ops.score_candidates(U.to(hip_device), torch.arange(R_, dtype=torch.int32, device=hip_device), Ed,
+                              cand.to(hip_device))
+    ref = (U.double() @ E.double().t()).gather(1, cand.long())
+    assert _maxrel(sc, ref) < 1e-5
+    rank = ops.rank_first(sc).cpu().numpy()
+    s = sc.cpu().numpy()
+    for r in range(R_):
+        ranked = R.rank_candidates(s[r], np.arange(100))
+        assert int(np.where(ranked == 0)[0][0]) == rank[r]
+    # exact top-k on given scores, ties included (bit-exact indices)
+    S = torch.randn(7, N, generator=g).round(decimals=1)  # many exact ties
+    X = synth_csr(7, N, seed=9)
+    idx, val = ops.topk(S.to(hip_device).clone(), 20, exclude=ops.csr_from_scipy(X, hip_device))
+    for r in range(7):
+        ref_idx = R.topk_exclude_seen(S[r].numpy(), X[r].indices, 20)
+        np.testing.assert_array_equal(idx[r].cpu().numpy(), ref_idx)
