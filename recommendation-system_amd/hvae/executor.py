@@ -1,0 +1,508 @@
+"""Fused, graph-captured HybridVAE train/validation step on MI355X.
+
+Replaces the body of VAETrainer.train_epoch / validate (src/ml/train.py:81-124):
+per batch the reference densifies every user row on the host, copies a dense
+[B, N] batch to the device, runs ~60 eager aten ops through autograd, clips
+with clip_grad_norm_, steps torch.optim.Adam and syncs three times with
+.item(). Here one step is a fixed sequence of ~30 libhvae launches over
+device-resident data, captured once per batch size into a hipGraph (through
+torch.cuda.CUDAGraph) and replayed:
+
+  * the interaction CSR lives in HBM; a batch is a window of a permuted
+    user-id array whose start is a device counter (rows_offset), advanced by
+    the graph itself -- no host work per step besides the replay;
+  * parameters, gradients and Adam moments live in flat fp32 buffers; the
+    module's nn.Parameters are rebound to views of the flat parameter buffer,
+    so state_dict() and checkpoints always see the current values;
+  * the first-layer weight is stored item-major (W1t [N, H]) -- the
+    ``encoder.0.weight`` parameter is its [H, N] transposed view -- and its
+    gradient is row-sparse (only the batch's items);
+  * dropout masks and reparameterisation noise are Philox streams keyed by
+    (seed, device step counter), so replays draw fresh randomness;
+  * losses accumulate on the device in fp64 and are read once per epoch.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import _lib, ops
+from ._lib import CsrBatch, Epilogue, check, lib, ptr
+
+ALIGN = 4  # floats: every flat segment starts 16-B aligned
+
+
+def _align(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+@dataclass
+class Seg:
+    name: str
+    offset: int
+    shape: tuple
+    numel: int
+
+
+class FlatLayout:
+    """Parameter layout: W1t [N, H1] first, then the small parameters.
+
+    Small parameters keep the reference's parameter order (src/ml/model.py
+    modules() order) except that fc_mu/fc_logvar weights (and biases) are
+    adjacent, so that the two heads run as one [2L, H] GEMM.
+    """
+
+    def __init__(self, model):
+        self.n_items = model.n_items
+        self.hidden = list(model.hidden_dims)
+        self.L = model.latent_dim
+        self.d = model.embedding_dim
+        self.has_proj = self.L != self.d
+        segs: list[Seg] = []
+        off = 0
+
+        def add(name, shape, align=True):
+            nonlocal off
+            n = int(np.prod(shape))
+            segs.append(Seg(name, off, tuple(shape), n))
+            off = off + (_align(n) if align else n)
+
+        add("w1t", (self.n_items, self.hidden[0]))
+        self.small_offset = off
+        prev = self.hidden[0]
+        for k, hd in enumerate(self.hidden):
+            i = 4 * k
+            if k > 0:
+                add(f"encoder.{i}.weight", (hd, prev))
+            add(f"encoder.{i}.bias", (hd,))
+            add(f"encoder.{i + 1}.weight", (hd,))
+            add(f"encoder.{i + 1}.bias", (hd,))
+            prev = hd
+        add("fc_mu.weight", (self.L, prev), align=False)
+        add("fc_logvar.weight", (self.L, prev))
+        add("fc_mu.bias", (self.L,), align=False)
+        add("fc_logvar.bias", (self.L,))
+        if self.has_proj:
+            add("projection_layer.0.weight", (self.d, self.L))
+            add("projection_layer.0.bias", (self.d,))
+            add("projection_layer.3.weight", (self.d, self.d))
+            add("projection_layer.3.bias", (self.d,))
+        self.total = off
+        self.n_small = off - self.small_offset
+        self.segs = {s.name: s for s in segs}
+
+    def view(self, buf: torch.Tensor, name: str, base: int = 0) -> torch.Tensor:
+        s = self.segs[name]
+        return buf[s.offset - base: s.offset - base + s.numel].view(s.shape)
+
+    def heads(self, buf: torch.Tensor, base: int = 0):
+        """(W_heads [2L, H], b_heads [2L]) views spanning fc_mu and fc_logvar."""
+        w, b = self.segs["fc_mu.weight"], self.segs["fc_mu.bias"]
+        H = w.shape[1]
+        W = buf[w.offset - base: w.offset - base + 2 * self.L * H].view(2 * self.L, H)
+        B = buf[b.offset - base: b.offset - base + 2 * self.L]
+        return W, B
+
+
+@dataclass
+class DeviceData:
+    """Interaction CSR resident in HBM + the user ids a loader iterates over."""
+    row_ptr: torch.Tensor
+    col_idx: torch.Tensor
+    vals: torch.Tensor
+    users: torch.Tensor       # int32 [n] (rows of the matrix this dataset yields)
+    n_items: int
+    row_nnz: np.ndarray       # host copy of nnz per listed user (capacity planning)
+    perm: torch.Tensor = field(default=None)  # int32 [n] current epoch order
+
+    @staticmethod
+    def from_scipy(mat, users, device) -> "DeviceData":
+        mat = mat.tocsr()
+        mat.sum_duplicates()
+        users = np.asarray(users, dtype=np.int64)
+        rp = mat.indptr.astype(np.int64)
+        users_d = torch.as_tensor(users.astype(np.int32), device=device)
+        return DeviceData(
+            row_ptr=torch.as_tensor(rp, device=device),
+            col_idx=torch.as_tensor(mat.indices.astype(np.int32), device=device),
+            vals=torch.as_tensor(mat.data.astype(np.float32), device=device),
+            users=users_d,
+            n_items=mat.shape[1],
+            row_nnz=(rp[users + 1] - rp[users]) if len(users) else np.zeros(0, np.int64),
+            perm=users_d.clone(),  # fixed address: captured graphs read the epoch order from here
+        )
+
+    def max_batch_nnz(self, B: int) -> int:
+        if len(self.row_nnz) == 0:
+            return 1
+        top = np.sort(self.row_nnz)[::-1][:B]
+        return max(int(top.sum()), 1)
+
+
+class _StepBuffers:
+    """Activations / gradients for one batch size (graph-static pointers)."""
+
+    def __init__(self, ex: "FusedTrainer", B: int, cap: int, train: bool):
+        dev, lay = ex.device, ex.layout
+        f = lambda *s: torch.empty(*s, device=dev)
+        self.B = B
+        H = lay.hidden
+        L, d = lay.L, lay.d
+        self.h = [f(B, hd) for hd in H]
+        self.xhat = [f(B, hd) for hd in H]
+        self.rstd = [f(B) for _ in H]
+        self.a = [None] + [f(B, hd) for hd in H[1:]]
+        self.heads = f(B, 2 * L)
+        self.z = f(B, L)
+        self.eps = f(B, L)
+        self.kl_rows = f(B)
+        self.p1 = f(B, d) if lay.has_proj else None
+        self.q = f(B, d) if lay.has_proj else None
+        self.u = f(B, d) if lay.has_proj else self.z
+        self.lse = f(B)
+        self.O = f(B, d)
+        self.recon_rows = f(B)
+        self.dU = f(B, d)
+        self.dp1 = f(B, d) if lay.has_proj else None
+        self.dz = f(B, L) if lay.has_proj else self.dU
+        self.dheads = f(B, 2 * L)
+        self.dh = [f(B, hd) for hd in H]
+        self.da = [f(B, hd) for hd in H]
+        self.loss3 = f(3)
+        self.rg = ops.RowGradBuffers(lay.n_items, H[0], cap, dev) if train else None
+        L_ = lib()
+        need = [
+            L_.hvae_decoder_workspace(ex.dec_dtype, B, lay.n_items, d),
+            L_.hvae_clip_grad_norm_workspace(lay.n_small, cap, H[0]),
+        ]
+        dims = [(B, hd) for hd in H] + [(B, 2 * L), (B, d), (B, L)]
+        for (_, n) in dims:
+            need.append(L_.hvae_colsum_workspace(B, n))
+        for hd in H:
+            need.append(L_.hvae_ln_gelu_drop_bwd_workspace(B, hd))
+        gemms = [(2 * L, H[-1], B), (B, H[-1], 2 * L)]
+        if lay.has_proj:
+            gemms += [(d, d, B), (d, L, B), (B, d, d), (B, L, d)]
+        for k in range(1, len(H)):
+            gemms += [(H[k], H[k - 1], B), (B, H[k - 1], H[k])]
+        for (m_, n_, k_) in gemms:
+            need.append(L_.hvae_gemm_f32_workspace(m_, n_, k_))
+        self.ws = torch.empty(max(int(max(need)), 256), dtype=torch.uint8, device=dev)
+        self.graph = None
+
+
+class FusedTrainer:
+    """Owns the flat parameter/optimizer state of one HybridVAE on one device."""
+
+    def __init__(self, model, device, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
+                 eps: float = 1e-8, max_norm: float = 5.0, precision: str | None = None, seed: int | None = None,
+                 use_graphs: bool = True):
+        if device.type != "cuda":
+            raise RuntimeError("FusedTrainer runs the MI355X HIP path only (device must be the HIP device)")
+        lib()  # fail loudly now if libhvae.so is missing
+        self.model = model
+        self.device = device
+        self.layout = lay = FlatLayout(model)
+        self.lr, self.wd, self.betas, self.eps, self.max_norm = lr, weight_decay, betas, eps, max_norm
+        self.use_graphs = use_graphs
+        if getattr(model, "item_embeddings_trainable", False):
+            raise NotImplementedError("fused trainer: trainable item embeddings (freeze_embeddings=False) "
+                                      "are not supported; the reference trains with a frozen E")
+        self.seed = int(seed if seed is not None else torch.randint(0, 2 ** 62, (1,)).item())
+        # ---- flat state
+        self.flat = torch.zeros(lay.total, device=device)
+        self.m = torch.zeros(lay.total, device=device)
+        self.v = torch.zeros(lay.total, device=device)
+        self.g_small = torch.zeros(lay.n_small, device=device)
+        self._adopt_parameters()
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=device)
+        self.boff = torch.zeros(1, dtype=torch.int64, device=device)
+        self.norm = torch.zeros(1, device=device)
+        self.coef = torch.ones(1, device=device)
+        self.accum_train = torch.zeros(3, dtype=torch.float64, device=device)
+        self.accum_val = torch.zeros(3, dtype=torch.float64, device=device)
+        self.host_step = 0
+        # ---- frozen embeddings: fp32 (sparse terms, eval) + bf16 copy (decoder MFMA)
+        self.E32 = model.item_embeddings.detach().contiguous()
+        if self.E32.device != device:
+            raise RuntimeError("model must be moved to the device before building the trainer")
+        d = lay.d
+        if precision is None:
+            precision = "bf16" if ops.decoder_supported(_lib.HVAE_BF16, d) else "fp32"
+        if precision == "bf16":
+            if not ops.decoder_supported(_lib.HVAE_BF16, d):
+                raise NotImplementedError(f"no bf16 streaming decoder for embedding dim {d}")
+            self.dec_dtype = _lib.HVAE_BF16
+            self.E_dec = ops.cast_bf16(self.E32)
+        elif precision == "fp32":
+            if not ops.decoder_supported(_lib.HVAE_F32, d):
+                raise NotImplementedError(f"no fp32 streaming decoder for embedding dim {d}")
+            self.dec_dtype = _lib.HVAE_F32
+            self.E_dec = self.E32
+        else:
+            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision!r}")
+        self.precision = precision
+        self.enorm = ops.row_norm_max(self.E_dec)
+        self._bufs: dict[tuple, _StepBuffers] = {}
+        self._views()
+
+    # ------------------------------------------------------------ state ---
+    def _adopt_parameters(self):
+        """Copy the module's parameters into the flat buffer and rebind them as views."""
+        lay, model = self.layout, self.model
+        named = dict(model.named_parameters())
+        with torch.no_grad():
+            w1 = named["encoder.0.weight"]  # [H, N] (a view of item-major storage)
+            w1t = lay.view(self.flat, "w1t")
+            w1t.copy_(w1.detach().t())
+            w1.data = w1t.t()
+            for name, seg in lay.segs.items():
+                if name == "w1t":
+                    continue
+                p = named[name]
+                v = lay.view(self.flat, name)
+                v.copy_(p.detach().reshape(seg.shape))
+                p.data = v
+        self.param_views = {n: p for n, p in named.items()}
+
+    def _views(self):
+        lay, f = self.layout, self.flat
+        base = lay.small_offset
+        V = lambda buf, n, b=0: lay.view(buf, n, b)
+        self.w1t = V(f, "w1t")
+        self.m_w1t, self.v_w1t = V(self.m, "w1t"), V(self.v, "w1t")
+        self.small = f[base:]
+        self.m_small, self.v_small = self.m[base:], self.v[base:]
+        H = lay.hidden
+        self.P = {}
+        self.G = {}
+        for k in range(len(H)):
+            i = 4 * k
+            names = [f"encoder.{i}.bias", f"encoder.{i + 1}.weight", f"encoder.{i + 1}.bias"]
+            if k > 0:
+                names.append(f"encoder.{i}.weight")
+            for n in names:
+                self.P[n] = V(f, n)
+                self.G[n] = V(self.g_small, n, base)
+        self.W_heads, self.b_heads = lay.heads(f)
+        self.gW_heads, self.gb_heads = lay.heads(self.g_small, base)
+        if lay.has_proj:
+            for n in ("projection_layer.0.weight", "projection_layer.0.bias", "projection_layer.3.weight",
+                      "projection_layer.3.bias"):
+                self.P[n] = V(f, n)
+                self.G[n] = V(self.g_small, n, base)
+
+    def grad_of(self, name: str) -> torch.Tensor:
+        """Current gradient of a small parameter (after the last step)."""
+        return self.G[name]
+
+    # ------------------------------------------------------------- data ---
+    def device_data(self, mat, users) -> DeviceData:
+        return DeviceData.from_scipy(mat, users, self.device)
+
+    # ------------------------------------------------------------- step ---
+    def _buffers(self, B: int, cap: int, train: bool) -> _StepBuffers:
+        key = (B, train)
+        b = self._bufs.get(key)
+        if b is None or (train and b.rg.cap < cap):
+            b = _StepBuffers(self, B, cap, train)
+            self._bufs[key] = b
+        return b
+
+    def _csr(self, data: DeviceData, B: int, rows: torch.Tensor | None, offset: torch.Tensor | None) -> CsrBatch:
+        return CsrBatch(ptr(data.row_ptr), ptr(data.col_idx), ptr(data.vals), ptr(rows), ptr(offset), B,
+                        data.n_items)
+
+    def _launch(self, bf: _StepBuffers, csr: CsrBatch, train: bool, beta: float, p_drop: float,
+                ext: dict | None = None):
+        """Enqueue one full step on the current stream (captured into a graph by the caller)."""
+        L_, lay = lib(), self.layout
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        B, H, Lt, d = bf.B, lay.hidden, lay.L, lay.d
+        ws, wsn = ptr(bf.ws), bf.ws.numel()
+        seed, step = self.seed, ptr(self.step_dev)
+        tr = int(train)
+        ext = ext or {}
+        encm = ext.get("enc_masks", [None] * len(H))
+        csr_ref = C.byref(csr)
+
+        def gemm(ta, tb, M, N, K, A, lda, Bm, ldb, Cm, ldc, epi=None, beta_=0.0):
+            check(L_.hvae_gemm_f32(ta, tb, M, N, K, 1.0, A, lda, Bm, ldb, beta_, Cm, ldc,
+                                   C.byref(epi) if epi is not None else None, ws, wsn, st), "gemm")
+
+        # ------------------------------------------------------ forward ---
+        check(L_.hvae_encoder_fwd(csr_ref, ptr(self.w1t), ptr(self.P["encoder.0.bias"]),
+                                  ptr(self.P["encoder.1.weight"]), ptr(self.P["encoder.1.bias"]), H[0], p_drop,
+                                  ptr(encm[0]), seed, step, tr, ptr(bf.h[0]), ptr(bf.xhat[0]), ptr(bf.rstd[0]),
+                                  st), "encoder_fwd")
+        for k in range(1, len(H)):
+            i = 4 * k
+            W = self.P[f"encoder.{i}.weight"]
+            epi = Epilogue(_lib.EPI_BIAS, ptr(self.P[f"encoder.{i}.bias"]), None, None, 0.0, None, 0, None, 0, 0)
+            gemm(0, 1, B, H[k], H[k - 1], ptr(bf.h[k - 1]), H[k - 1], ptr(W), H[k - 1], ptr(bf.a[k]), H[k], epi)
+            check(L_.hvae_ln_gelu_drop_fwd(ptr(bf.a[k]), ptr(self.P[f"encoder.{i + 1}.weight"]),
+                                           ptr(self.P[f"encoder.{i + 1}.bias"]), B, H[k], p_drop, ptr(encm[k]), seed,
+                                           step, k, tr, ptr(bf.h[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]), st),
+                  "ln_gelu_drop_fwd")
+        Hl = H[-1]
+        epi_b = Epilogue(_lib.EPI_BIAS, ptr(self.b_heads), None, None, 0.0, None, 0, None, 0, 0)
+        gemm(0, 1, B, 2 * Lt, Hl, ptr(bf.h[-1]), Hl, ptr(self.W_heads), Hl, ptr(bf.heads), 2 * Lt, epi_b)
+        mu, lv = bf.heads, bf.heads[:, Lt:]
+        check(L_.hvae_reparam_kl_fwd(ptr(mu), ptr(lv), 2 * Lt, B, Lt, tr, ptr(ext.get("eps")), seed, step,
+                                     ptr(bf.z), ptr(bf.eps), ptr(bf.kl_rows), st), "reparam_kl_fwd")
+        if lay.has_proj:
+            Wa, ba = self.P["projection_layer.0.weight"], self.P["projection_layer.0.bias"]
+            Wb, bb = self.P["projection_layer.3.weight"], self.P["projection_layer.3.bias"]
+            epi1 = Epilogue(_lib.EPI_BIAS_GELU_DROP, ptr(ba), ptr(bf.p1), None, p_drop, ptr(ext.get("proj_mask")),
+                            seed, step, _lib.TAG_PROJ_DROP, tr)
+            gemm(0, 1, B, d, Lt, ptr(bf.z), Lt, ptr(Wa), Lt, ptr(bf.q), d, epi1)
+            epi2 = Epilogue(_lib.EPI_BIAS, ptr(bb), None, None, 0.0, None, 0, None, 0, 0)
+            gemm(0, 1, B, d, d, ptr(bf.q), d, ptr(Wb), d, ptr(bf.u), d, epi2)
+        check(L_.hvae_decoder_fwd(self.dec_dtype, ptr(bf.u), d, ptr(self.E_dec), ptr(self.enorm), B, lay.n_items, d,
+                                  ptr(bf.lse), ptr(bf.O) if train else None, ws, wsn, st), "decoder_fwd")
+        check(L_.hvae_decoder_bwd(csr_ref, ptr(bf.u), d, ptr(self.E32), d, ptr(bf.lse), ptr(bf.O) if train else None,
+                                  1.0 / B, ptr(bf.recon_rows), ptr(bf.dU) if train else None, st), "decoder_bwd")
+        accum = self.accum_train if train else self.accum_val
+        check(L_.hvae_loss_finalize(ptr(bf.recon_rows), ptr(bf.kl_rows), B, beta, ptr(bf.loss3), ptr(accum), st),
+              "loss_finalize")
+        if not train:
+            return
+        # ----------------------------------------------------- backward ---
+        G = self.G
+        if lay.has_proj:
+            gemm(1, 0, d, d, B, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d)
+            check(L_.hvae_colsum(ptr(bf.dU), B, d, d, 0.0, ptr(G["projection_layer.3.bias"]), ws, wsn, st), "colsum")
+            epi3 = Epilogue(_lib.EPI_GELU_DROP_BWD, None, None, ptr(bf.p1), p_drop, ptr(ext.get("proj_mask")), seed,
+                            step, _lib.TAG_PROJ_DROP, tr)
+            gemm(0, 0, B, d, d, ptr(bf.dU), d, ptr(Wb), d, ptr(bf.dp1), d, epi3)
+            gemm(1, 0, d, Lt, B, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt)
+            check(L_.hvae_colsum(ptr(bf.dp1), B, d, d, 0.0, ptr(G["projection_layer.0.bias"]), ws, wsn, st),
+                  "colsum")
+            gemm(0, 0, B, Lt, d, ptr(bf.dp1), d, ptr(Wa), Lt, ptr(bf.dz), Lt)
+        dmu, dlv = bf.dheads, bf.dheads[:, Lt:]
+        check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B, tr,
+                                     ptr(dmu), ptr(dlv), 2 * Lt, st), "reparam_kl_bwd")
+        gemm(1, 0, 2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl)
+        check(L_.hvae_colsum(ptr(bf.dheads), B, 2 * Lt, 2 * Lt, 0.0, ptr(self.gb_heads), ws, wsn, st), "colsum")
+        gemm(0, 0, B, Hl, 2 * Lt, ptr(bf.dheads), 2 * Lt, ptr(self.W_heads), Hl, ptr(bf.dh[-1]), Hl)
+        for k in range(len(H) - 1, -1, -1):
+            i = 4 * k
+            check(L_.hvae_ln_gelu_drop_bwd(ptr(bf.dh[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]),
+                                           ptr(self.P[f"encoder.{i + 1}.weight"]), ptr(self.P[f"encoder.{i + 1}.bias"]),
+                                           B, H[k], p_drop, ptr(encm[k]), seed, step, k, tr, ptr(bf.da[k]),
+                                           ptr(G[f"encoder.{i + 1}.weight"]), ptr(G[f"encoder.{i + 1}.bias"]), ws,
+                                           wsn, st), "ln_gelu_drop_bwd")
+            check(L_.hvae_colsum(ptr(bf.da[k]), B, H[k], H[k], 0.0, ptr(G[f"encoder.{i}.bias"]), ws, wsn, st),
+                  "colsum")
+            if k > 0:
+                W = self.P[f"encoder.{i}.weight"]
+                gemm(1, 0, H[k], H[k - 1], B, ptr(bf.da[k]), H[k], ptr(bf.h[k - 1]), H[k - 1],
+                     ptr(G[f"encoder.{i}.weight"]), H[k - 1])
+                gemm(0, 0, B, H[k - 1], H[k], ptr(bf.da[k]), H[k], ptr(W), H[k - 1], ptr(bf.dh[k - 1]), H[k - 1])
+        check(L_.hvae_w1_rowgrad(csr_ref, ptr(bf.da[0]), H[0], bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st),
+              "w1_rowgrad")
+        # ------------------------------------------------ clip + Adam ---
+        check(L_.hvae_clip_grad_norm(ptr(self.g_small), lay.n_small, bf.rg.ref, H[0], self.max_norm,
+                                     ptr(self.norm), ptr(self.coef), ws, wsn, st), "clip_grad_norm")
+        cfg = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, self.coef)
+        check(L_.hvae_adam_rows(C.byref(cfg), ptr(self.w1t), ptr(self.m_w1t), ptr(self.v_w1t), bf.rg.ref,
+                                lay.n_items, H[0], st), "adam_rows")
+        check(L_.hvae_adam_dense(C.byref(cfg), ptr(self.small), ptr(self.m_small), ptr(self.v_small),
+                                 ptr(self.g_small), lay.n_small, st), "adam_dense")
+        check(L_.hvae_counter_add(step, 1, st), "counter_add")
+
+    def _advance(self, B: int):
+        check(lib().hvae_counter_add(ptr(self.boff), B, torch.cuda.current_stream(self.device).cuda_stream),
+              "counter_add")
+
+    # -------------------------------------------------------- public API ---
+    def step_batch(self, data: DeviceData, rows: torch.Tensor | None, B: int, beta: float, p_drop: float,
+                   train: bool = True, ext: dict | None = None) -> torch.Tensor:
+        """One eager step over `rows` (int32 device user ids, or None: rows 0..B-1). Returns loss3."""
+        cap = int(data.row_ptr[-1].item()) if rows is None else data.max_batch_nnz(B)
+        bf = self._buffers(B, cap, train)
+        csr = self._csr(data, B, rows, None)
+        self._launch(bf, csr, train, beta, p_drop, ext)
+        if train:
+            self.host_step += 1
+        return bf.loss3
+
+    def run_epoch(self, data: DeviceData, batch_size: int, shuffle: bool, beta_fn, p_drop: float,
+                  train: bool = True, drop_last: bool = False, generator: torch.Generator | None = None) -> dict:
+        """Iterate the dataset in batches (DataLoader semantics: shuffle, drop_last=False).
+
+        beta_fn(step_index) -> beta; a constant beta lets every full batch replay one graph.
+        Returns the mean of the per-batch losses (VAETrainer.train_epoch's metric).
+        """
+        n = int(data.users.numel())
+        if n == 0:
+            return {"total_loss": float("nan"), "recon_loss": float("nan"), "kl_loss": float("nan")}
+        if shuffle:
+            order = torch.randperm(n, generator=generator)
+            data.perm.copy_(data.users[order.to(self.device)])
+        else:
+            data.perm.copy_(data.users)
+        accum = self.accum_train if train else self.accum_val
+        accum.zero_()
+        self.boff.zero_()
+        n_full, tail = divmod(n, batch_size)
+        if drop_last:
+            tail = 0
+        n_batches = n_full + (1 if tail else 0)
+        const_beta = getattr(beta_fn, "constant", None)
+        B = batch_size
+        for bi in range(n_full):
+            beta = beta_fn(bi)
+            bf = self._buffers(B, data.max_batch_nnz(B), train)
+            if self.use_graphs and const_beta is not None:
+                if bf.graph is None or bf.graph_key != (id(data), beta, p_drop):
+                    if bi == 0 and bf.graph is None:
+                        # first use: run eagerly (loads kernels, sets attributes), capture afterwards
+                        self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop)
+                        self._advance(B)
+                        if train:
+                            self.host_step += 1
+                        continue
+                    self._capture(bf, data, train, beta, p_drop)
+                bf.graph.replay()
+            else:
+                self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop)
+                self._advance(B)
+            if train:
+                self.host_step += 1
+        if tail:
+            beta = beta_fn(n_full)
+            bf = self._buffers(tail, data.max_batch_nnz(tail), train)
+            self._launch(bf, self._csr(data, tail, data.perm, self.boff), train, beta, p_drop)
+            self._advance(tail)
+            if train:
+                self.host_step += 1
+        sums = accum.cpu().tolist()  # the one host sync of the epoch
+        return {"total_loss": sums[0] / n_batches, "recon_loss": sums[1] / n_batches, "kl_loss": sums[2] / n_batches}
+
+    def _capture(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float):
+        g = torch.cuda.CUDAGraph()
+        csr = self._csr(data, bf.B, data.perm, self.boff)
+        bf.csr_keepalive = csr
+        torch.cuda.synchronize(self.device)
+        with torch.cuda.graph(g):
+            self._launch(bf, csr, train, beta, p_drop)
+            self._advance(bf.B)
+        bf.graph = g
+        bf.graph_key = (id(data), beta, p_drop)
+
+    def sync_state_to_model(self):
+        """Parameters are views of the flat buffer already; nothing to copy."""
+        return None
+
+
+class ConstBeta:
+    def __init__(self, beta: float):
+        self.constant = float(beta)
+
+    def __call__(self, _i):
+        return self.constant

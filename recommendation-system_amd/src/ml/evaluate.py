@@ -1,0 +1,330 @@
+"""Evaluation on MI355X -- drop-in for the reference's src/ml/evaluate.py.
+
+Same metrics, protocols, evaluator API, checkpoint loader and CLI as the
+reference (src/ml/evaluate.py:32-374). The per-test-row Python loop with a
+1 x N decode per row (:187-215) becomes batched device work: user vectors for
+a batch of test rows through the HIP encoder, then either the 100 candidate
+scores per row (99-negative protocol; hvae_score_candidates + hvae_rank_first)
+or the full fp32 score matrix + exact top-K with seen items masked
+(full-ranking protocol; hvae_gemm_f32 + hvae_topk). Negatives are drawn with
+np.random.choice(available, n, replace=False) exactly as the reference does
+(:159-170), so the protocol's sampling distribution is unchanged.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+from pathlib import Path
+
+import numpy as np
+import pandas as pd
+import torch
+from scipy.sparse import csr_matrix
+
+from hvae import ops
+
+from ..config import config
+from ..preprocessing.embeddings import load_embeddings
+from .model import HybridVAE, create_hybrid_vae
+from .train import load_training_data
+
+logging.basicConfig(level=logging.INFO)
+logger = logging.getLogger(__name__)
+
+
+# =============================================================================
+# Metrics (reference: evaluate.py:32-54)
+# =============================================================================
+
+
+def recall_at_k(recommended: np.ndarray, relevant: np.ndarray, k: int) -> float:
+    if len(relevant) == 0:
+        return 0.0
+    hits = len(np.intersect1d(recommended[:k], relevant))
+    return hits / len(relevant)
+
+
+def ndcg_at_k(recommended: np.ndarray, relevant: np.ndarray, k: int) -> float:
+    if len(relevant) == 0:
+        return 0.0
+    dcg = sum(1.0 / np.log2(i + 2) for i, item in enumerate(recommended[:k]) if item in relevant)
+    idcg = sum(1.0 / np.log2(i + 2) for i in range(min(len(relevant), k)))
+    return dcg / idcg if idcg > 0 else 0.0
+
+
+def hit_ratio_at_k(recommended: np.ndarray, relevant: np.ndarray, k: int) -> float:
+    if len(relevant) == 0:
+        return 0.0
+    return 1.0 if len(np.intersect1d(recommended[:k], relevant)) > 0 else 0.0
+
+
+def metrics_from_rank(rank: np.ndarray, k_values: list[int]) -> dict[int, dict[str, np.ndarray]]:
+    """Per-row metrics for ONE relevant item at 0-based `rank` (vectorised form of the above)."""
+    out = {}
+    for k in k_values:
+        hit = (rank < k).astype(np.float64)
+        out[k] = {"recall": hit, "ndcg": np.where(rank < k, 1.0 / np.log2(rank + 2.0), 0.0), "hit_ratio": hit}
+    return out
+
+
+# =============================================================================
+# Helpers
+# =============================================================================
+
+
+def _get_device(device: str | None = None) -> torch.device:
+    if device:
+        return torch.device(device)
+    if torch.cuda.is_available():
+        return torch.device("cuda")
+    raise RuntimeError("The MI355X HybridVAE path needs a HIP device; there is no CPU fallback.")
+
+
+def _build_input_matrix(train_df: pd.DataFrame, val_df: pd.DataFrame, user_to_idx: dict, item_to_idx: dict,
+                        shape: tuple) -> csr_matrix:
+    """Train + val positives (reference: evaluate.py:73-87)."""
+    train_pos = train_df[train_df["binary_rating"] == 1] if "binary_rating" in train_df.columns else train_df
+    val_pos = val_df[val_df["binary_rating"] == 1] if "binary_rating" in val_df.columns else val_df
+    combined = pd.concat([train_pos, val_pos])
+    rows = combined["user_id"].map(user_to_idx)
+    cols = combined["asin"].map(item_to_idx)
+    return csr_matrix((np.ones(len(combined)), (rows, cols)), shape=shape)
+
+
+def _aggregate_metrics(all_metrics: dict, k_values: list[int]) -> dict[int, dict[str, float]]:
+    return {
+        k: {m: float(np.mean(all_metrics[k][m])) if len(all_metrics[k][m]) else 0.0
+            for m in ["recall", "ndcg", "hit_ratio"]}
+        for k in k_values
+    }
+
+
+# =============================================================================
+# Evaluator
+# =============================================================================
+
+
+class RecommendationEvaluator:
+    """Leave-one-out evaluator (reference: evaluate.py:106-265), batched on the device."""
+
+    def __init__(self, model: HybridVAE, interaction_matrix: csr_matrix, user_to_idx: dict[str, int],
+                 item_to_idx: dict[str, int], device: torch.device, batch_size: int = 1024):
+        self.model = model.to(device)
+        self.model.eval()
+        self.device = device
+        self.interaction_matrix = interaction_matrix.tocsr()
+        self.user_to_idx = user_to_idx
+        self.item_to_idx = item_to_idx
+        self.n_items = interaction_matrix.shape[1]
+        self.batch_size = batch_size
+        self._csr = ops.csr_from_scipy(self.interaction_matrix, device)
+        self._E = self.model.item_embeddings.detach().contiguous()
+
+    # ---- device helpers
+    def _user_vectors(self, users: np.ndarray) -> torch.Tensor:
+        rows = torch.as_tensor(np.asarray(users, np.int32), device=self.device)
+        csr = ops.Csr(self._csr.row_ptr, self._csr.col_idx, self._csr.vals, self.n_items, rows=rows)
+        return self.model.user_vectors(csr)
+
+    def _scores(self, users: np.ndarray) -> torch.Tensor:
+        """fp32 [len(users), N] scores = decode(get_user_embedding(x)) (reference: evaluate.py:125-135)."""
+        u = self._user_vectors(users)
+        return ops.gemm(u, self._E.t())
+
+    # ---- reference per-user API
+    def _get_user_scores(self, user_idx: int) -> np.ndarray:
+        with torch.no_grad():
+            return self._scores(np.array([user_idx]))[0].cpu().numpy()
+
+    def get_user_recommendations(self, user_idx: int, top_k: int = 100, exclude_seen: bool = True):
+        idx, val = self._topk(np.array([user_idx]), top_k, exclude_seen)
+        return idx[0], val[0]
+
+    def _topk(self, users: np.ndarray, k: int, exclude_seen: bool = True):
+        with torch.no_grad():
+            S = self._scores(users)
+            excl = None
+            if exclude_seen:
+                rows = torch.as_tensor(np.asarray(users, np.int32), device=self.device)
+                excl = ops.Csr(self._csr.row_ptr, self._csr.col_idx, self._csr.vals, self.n_items, rows=rows)
+            idx, val = ops.topk(S, k, exclude=excl)
+        return idx.cpu().numpy().astype(np.int64), val.cpu().numpy()
+
+    def evaluate_user_with_negatives(self, user_idx: int, test_item_idx: int, n_negatives: int = 99,
+                                     k_values: list[int] | None = None) -> dict[int, dict[str, float]]:
+        k_values = k_values or [5, 10, 20]
+        negs = self._sample_negatives(user_idx, test_item_idx, n_negatives)
+        rank = self._ranks(np.array([user_idx]), np.array([test_item_idx]), [negs])
+        m = metrics_from_rank(rank, k_values)
+        return {k: {n: float(v[0]) for n, v in m[k].items()} for k in k_values}
+
+    def _sample_negatives(self, user_idx: int, test_item_idx: int, n_negatives: int) -> np.ndarray:
+        """The reference's sampler (evaluate.py:159-170), unchanged."""
+        seen = set(self.interaction_matrix[user_idx].indices)
+        mask = np.ones(self.n_items, dtype=bool)
+        mask[list(seen)] = False
+        mask[test_item_idx] = False
+        available = np.where(mask)[0]
+        return available if len(available) < n_negatives else np.random.choice(available, n_negatives, replace=False)
+
+    def _ranks(self, users: np.ndarray, tests: np.ndarray, negatives: list[np.ndarray]) -> np.ndarray:
+        """0-based rank of the test item among [test] + negatives, per row (batched on the device)."""
+        C = 1 + max((len(n) for n in negatives), default=0)
+        R = len(users)
+        cand = np.empty((R, C), np.int32)
+        pad = np.zeros(R, bool)
+        for r, (t, n) in enumerate(zip(tests, negatives)):
+            cand[r, 0] = t
+            cand[r, 1:1 + len(n)] = n
+            if len(n) < C - 1:  # fewer available items than requested: pad with the test item (never outranks)
+                cand[r, 1 + len(n):] = t
+                pad[r] = True
+        out = np.empty(R, np.int64)
+        with torch.no_grad():
+            for s in range(0, R, self.batch_size):
+                e = min(R, s + self.batch_size)
+                u = self._user_vectors(users[s:e])
+                cd = torch.as_tensor(cand[s:e], device=self.device)
+                sc = ops.score_candidates(u, torch.arange(e - s, dtype=torch.int32, device=self.device), self._E, cd)
+                if pad[s:e].any():
+                    scn = sc.cpu().numpy()
+                    for r in np.nonzero(pad[s:e])[0]:
+                        n = len(negatives[s + r])
+                        row = scn[r, : 1 + n]
+                        out[s + r] = int((row[1:] > row[0]).sum() + (row[1:] == row[0]).sum())
+                    rk = ops.rank_first(sc).cpu().numpy()
+                    for r in range(e - s):
+                        if not pad[s + r]:
+                            out[s + r] = rk[r]
+                else:
+                    out[s:e] = ops.rank_first(sc).cpu().numpy()
+        return out
+
+    def evaluate_dataset_with_negatives(self, test_df: pd.DataFrame, n_negatives: int = 99,
+                                        k_values: list[int] | None = None) -> dict[int, dict[str, float]]:
+        """99-negative protocol over every known (user, item) test row (reference: evaluate.py:187-215)."""
+        k_values = k_values or [5, 10, 20]
+        logger.info(f"Evaluating with negative sampling ({n_negatives} negatives)...")
+        users, tests, negs = [], [], []
+        for user_id, item_id in zip(test_df["user_id"].tolist(), test_df["asin"].tolist()):
+            if user_id not in self.user_to_idx or item_id not in self.item_to_idx:
+                continue
+            u, t = self.user_to_idx[user_id], self.item_to_idx[item_id]
+            users.append(u)
+            tests.append(t)
+            negs.append(self._sample_negatives(u, t, n_negatives))
+        all_metrics = {k: {"recall": [], "ndcg": [], "hit_ratio": []} for k in k_values}
+        if users:
+            rank = self._ranks(np.array(users), np.array(tests), negs)
+            m = metrics_from_rank(rank, k_values)
+            for k in k_values:
+                for name in ("recall", "ndcg", "hit_ratio"):
+                    all_metrics[k][name] = list(m[k][name])
+        logger.info(f"Evaluated {len(users)} users")
+        return _aggregate_metrics(all_metrics, k_values)
+
+    def evaluate_user(self, user_id: str, test_items: list[str], k_values: list[int] | None = None):
+        k_values = k_values or [5, 10, 20]
+        if user_id not in self.user_to_idx:
+            return {}
+        test_indices = np.array([self.item_to_idx[i] for i in test_items if i in self.item_to_idx])
+        if len(test_indices) == 0:
+            return {}
+        recommended, _ = self.get_user_recommendations(self.user_to_idx[user_id], top_k=max(k_values))
+        return {k: {"recall": recall_at_k(recommended, test_indices, k), "ndcg": ndcg_at_k(recommended, test_indices, k),
+                    "hit_ratio": hit_ratio_at_k(recommended, test_indices, k)} for k in k_values}
+
+    def evaluate_dataset(self, test_df: pd.DataFrame, k_values: list[int] | None = None):
+        """Full-ranking protocol (reference: evaluate.py:243-265), batched top-K on the device."""
+        k_values = k_values or [5, 10, 20]
+        logger.info("Evaluating with full ranking...")
+        test_by_user = test_df.groupby("user_id")["asin"].apply(list).to_dict()
+        users, rels = [], []
+        for user_id, items in test_by_user.items():
+            if user_id not in self.user_to_idx:
+                continue
+            rel = np.array([self.item_to_idx[i] for i in items if i in self.item_to_idx])
+            if len(rel) == 0:
+                continue
+            users.append(self.user_to_idx[user_id])
+            rels.append(rel)
+        all_metrics = {k: {"recall": [], "ndcg": [], "hit_ratio": []} for k in k_values}
+        K = max(k_values)
+        for s in range(0, len(users), self.batch_size):
+            idx, _ = self._topk(np.array(users[s:s + self.batch_size]), K, True)
+            for r, rel in enumerate(rels[s:s + self.batch_size]):
+                for k in k_values:
+                    all_metrics[k]["recall"].append(recall_at_k(idx[r], rel, k))
+                    all_metrics[k]["ndcg"].append(ndcg_at_k(idx[r], rel, k))
+                    all_metrics[k]["hit_ratio"].append(hit_ratio_at_k(idx[r], rel, k))
+        logger.info(f"Evaluated {len(users)} users")
+        return _aggregate_metrics(all_metrics, k_values)
+
+
+# =============================================================================
+# Main Functions (reference: evaluate.py:273-370)
+# =============================================================================
+
+
+def load_model_from_checkpoint(checkpoint_path: str, item_embeddings: np.ndarray, device: torch.device) -> HybridVAE:
+    logger.info(f"Loading model from {checkpoint_path}")
+    # tensors + plain containers only: our own checkpoints (and the reference's) load without unpickling code
+    checkpoint = torch.load(checkpoint_path, map_location=device, weights_only=True)
+    cfg = checkpoint["model_config"]
+    model = create_hybrid_vae(n_items=cfg["n_items"], item_embeddings=item_embeddings, latent_dim=cfg["latent_dim"],
+                              hidden_dims=cfg.get("hidden_dims"), dropout=cfg.get("dropout", 0.5),
+                              beta=cfg.get("beta", 0.2))
+    model.load_state_dict(checkpoint["model_state_dict"])
+    logger.info(f"Loaded model from epoch {checkpoint['epoch']}")
+    return model
+
+
+def evaluate_recommendation_model(model_path: str, data_dir: str, embeddings_path: str,
+                                  k_values: list[int] | None = None, device: str | None = None,
+                                  n_negatives: int | None = None) -> dict:
+    k_values = k_values or [5, 10, 20]
+    device = _get_device(device)
+    full_matrix, train_df, val_df, mappings = load_training_data(data_dir)
+    user_to_idx, item_to_idx = mappings["user_to_idx"], mappings["item_to_idx"]
+    input_matrix = _build_input_matrix(train_df, val_df, user_to_idx, item_to_idx, full_matrix.shape)
+    test_df = pd.read_csv(Path(data_dir) / "test.csv")
+    embeddings, _, _ = load_embeddings(embeddings_path)
+    model = load_model_from_checkpoint(model_path, embeddings, device)
+    evaluator = RecommendationEvaluator(model, input_matrix, user_to_idx, item_to_idx, device)
+    if n_negatives is not None:
+        protocol = f"NEGATIVE SAMPLING ({n_negatives} negatives)"
+        results = evaluator.evaluate_dataset_with_negatives(test_df, n_negatives, k_values)
+    else:
+        protocol = "FULL RANKING (all items)"
+        results = evaluator.evaluate_dataset(test_df, k_values)
+    logger.info(f"\n{'=' * 70}\nHYBRID VAE EVALUATION RESULTS\nProtocol: {protocol}\n{'=' * 70}")
+    print(f"\n{'-' * 70}\n{'K':<5} | {'Recall':>12} | {'NDCG':>12} | {'Hit Ratio':>12}\n{'-' * 70}")
+    for k in k_values:
+        m = results[k]
+        print(f"@{k:<4} | {m['recall']:>12.4f} | {m['ndcg']:>12.4f} | {m['hit_ratio']:>12.4f}")
+    print("-" * 70)
+    return results
+
+
+def main() -> None:
+    parser = argparse.ArgumentParser(description="Evaluate recommendation model (MI355X)")
+    parser.add_argument("--model", default=config.MODEL_FILE)
+    parser.add_argument("--data", default=str(config.DATA_DIR))
+    parser.add_argument("--embeddings", default=config.EMBEDDINGS_FILE)
+    parser.add_argument("--k-values", type=int, nargs="+", default=[5, 10, 20])
+    parser.add_argument("--device", choices=["cuda", "cpu", "mps"])
+    parser.add_argument("--output", help="Path to save results (JSON)")
+    parser.add_argument("--n-negatives", type=int, default=99, help="Negatives count (0 for full ranking)")
+    args = parser.parse_args()
+    n_negatives = args.n_negatives if args.n_negatives > 0 else None
+    results = evaluate_recommendation_model(model_path=args.model, data_dir=args.data, embeddings_path=args.embeddings,
+                                            k_values=args.k_values, device=args.device, n_negatives=n_negatives)
+    if args.output:
+        with open(args.output, "w") as f:
+            json.dump(results, f, indent=2)
+        logger.info(f"Results saved to {args.output}")
+
+
+if __name__ == "__main__":
+    main()
