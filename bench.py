@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""HybridVAE train throughput (users/sec) on MI355X -- the BASELINE.json metric.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload all_beauty|appliances|syn1m]
+
+One "step" = one fused train step (encoder -> reparam/KL -> projection ->
+streaming decoder + multinomial loss -> backward -> clip 5.0 -> Adam) over
+one batch of users of a synthetic interaction matrix shaped like the named
+workload (default: BASELINE.json configs[1], All_Beauty 22,363 x 12,101,
+d=384, latent 128, hidden [512], batch 64, bf16 decoder MFMA). Inputs (CSR,
+weights, frozen E) are resident in HBM before the timed region. N > 1 runs
+one process per GPU (torchrun), user-batch data parallel with the gradient
+exchange over RCCL (weak scaling: B users per GPU per step).
+
+Prints ONE JSON line on rank 0, with a live roofline for the dominant kernel
+(HIP events around its launches on the stream it runs on) and the CPU
+oracle (oracle/ref_cpu.py, a pinned restatement of the reference trainer)
+timed on this host's cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path[:0] = [str(ROOT / "recommendation-system_amd"), str(ROOT), str(ROOT / "tests" / "golden")]
+
+import torch  # noqa: E402
+
+WORKLOADS = {
+    # BASELINE.json configs[1]: All_Beauty (22,363 x 12,101, d=384, latent=128), best config hidden [512],
+    # dropout 0.3, beta 0.2, lr 1e-3, batch 64 (config.BATCH_SIZE used by `make train-best`)
+    "all_beauty": dict(users=22363, items=12101, d=384, latent=128, hidden=[512], batch=64, lam=3.0,
+                       dropout=0.3, beta=0.2, lr=1e-3),
+    # configs[0]: Appliances (2,072 x 890, d=384, latent=64)
+    "appliances": dict(users=2072, items=890, d=384, latent=64, hidden=[512], batch=64, lam=3.0,
+                       dropout=0.3, beta=0.2, lr=1e-3),
+    # configs[2]: synthetic 1M users x 100K items, d=384, batch 4096 (hidden [512], latent 128)
+    "syn1m": dict(users=1_000_000, items=100_000, d=384, latent=128, hidden=[512], batch=4096, lam=15.0,
+                  dropout=0.3, beta=0.2, lr=1e-3),
+}
+
+PEAK_HBM_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md, spec)
+PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA
+PEAK_F32_TFLOPS = 157.3    # f32 MFMA = f32 vector rate
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_data(w: dict, rank: int, world: int):
+    from gen import synth_csr, synth_embeddings
+    X = synth_csr(w["users"], w["items"], lam=w["lam"], seed=0)
+    E = synth_embeddings(w["items"], w["d"], seed=1)
+    users = np.arange(rank, w["users"], world)  # each rank owns a disjoint user shard
+    return X, E, users
+
+
+def cpu_baseline(w: dict, X, E, seconds: float) -> dict:
+    """The pinned CPU restatement of the reference trainer on this host's cores.
+
+    Per batch: the reference loader's per-row densification (UserInteractionDataset
+    .__getitem__ + collate, src/ml/train.py:45-47) then one train step
+    (fwd, loss, backward, clip 5.0, Adam) -- the work of one GPU step.
+    """
+    from oracle import ref_cpu as R
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    B = w["batch"]
+    p = R.init_params(w["items"], E, w["latent"], w["hidden"], seed=0)
+    state = {}
+    rng = np.random.default_rng(0)
+    order = rng.permutation(X.shape[0])
+
+    def one(i):
+        rows = order[(i * B) % (len(order) - B):][:B]
+        x = torch.stack([torch.FloatTensor(X[int(u)].toarray().flatten()) for u in rows])
+        enc = [(torch.rand(B, h) >= w["dropout"]).float() / (1 - w["dropout"]) for h in w["hidden"]]
+        proj = (torch.rand(B, w["d"]) >= w["dropout"]).float() / (1 - w["dropout"])
+        eps = torch.randn(B, w["latent"])
+        R.train_step(p, state, x, w["beta"], lr=w["lr"], enc_masks=enc, proj_mask=proj, eps=eps)
+
+    for i in range(2):
+        one(i)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one(n + 2)
+        n += 1
+        el = time.perf_counter() - t0
+        if (el >= seconds and n >= 3) or n >= 5000:
+            break
+    return {"value": round(n * B / el, 2), "unit": "users/s", "cores": threads, "kind": "port",
+            "sample": f"{n} steps x {B} users of the same synthetic workload (per-row densifying loader + "
+                      f"fwd/bwd/clip/Adam), {el:.1f} s, torch fp32 on CPU"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--workload", default="all_beauty", choices=sorted(WORKLOADS))
+    ap.add_argument("--batch-size", type=int, default=None)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe-steps", type=int, default=50)
+    args = ap.parse_args()
+
+    w = dict(WORKLOADS[args.workload])
+    if args.batch_size:
+        w["batch"] = args.batch_size
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+        group = dist.group.WORLD
+
+    from hvae.executor import ConstBeta, FusedTrainer
+    from src.ml.model import HybridVAE
+
+    X, E, users = make_data(w, rank, world)
+    torch.manual_seed(0)
+    model = HybridVAE(w["items"], E, latent_dim=w["latent"], hidden_dims=w["hidden"], dropout=w["dropout"],
+                      beta=w["beta"]).to(device)
+    fused = FusedTrainer(model, device, lr=w["lr"], precision=args.precision, seed=1234, use_graphs=True,
+                         process_group=group)
+    data = fused.device_data(X, users)
+    B = w["batch"]
+    n_per_epoch = len(users) // B
+    beta = ConstBeta(w["beta"])
+    gen = torch.Generator().manual_seed(rank)
+
+    def run(nsteps):
+        done = 0
+        while done < nsteps:
+            k = min(nsteps - done, n_per_epoch)
+            fused.run_epoch(data, B, True, beta, w["dropout"], generator=gen, max_batches=k)
+            done += k
+
+    run(args.warmup)
+    if group is not None:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    if group is not None:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if group is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+
+    # ---- live per-kernel timing: HIP events around the kernel's launches (eager steps, same stream)
+    N, H, D = w["items"], w["hidden"][0], w["d"]
+    kernels = {}
+    fused.use_graphs = False
+    for name in ("adam_rows", "decoder_fwd"):
+        fused.probe = {"kernel": name, "events": []}
+        run(args.probe_steps)
+        torch.cuda.synchronize()
+        ts = [a.elapsed_time(b) * 1e-3 for a, b in fused.probe["events"]]
+        fused.probe = None
+        kernels[name] = float(np.mean(ts))
+    fused.use_graphs = True
+    adam_bytes = 24.0 * N * H + 4.0 * N                      # read+write p, m, v; slot lookup
+    dec_flops = 4.0 * B * N * D                               # S = U E^T and O = P E
+    dec_peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+    roof = {
+        "adam_rows": {"bound": "hbm", "achieved": adam_bytes / kernels["adam_rows"] / 1e9, "peak": PEAK_HBM_GBS,
+                      "unit": "GB/s", "alg_per_launch": adam_bytes, "avg_launch_us": kernels["adam_rows"] * 1e6},
+        "decoder_fwd": {"bound": "mfma", "achieved": dec_flops / kernels["decoder_fwd"] / 1e12, "peak": dec_peak,
+                        "unit": "TFLOP/s", "alg_per_launch": dec_flops, "avg_launch_us": kernels["decoder_fwd"] * 1e6},
+    }
+    dom = max(kernels, key=kernels.get)
+    r = roof[dom]
+    traffic = None
+    pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get(dom, {}).get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+    roofline = {"bound": r["bound"], "achieved": round(r["achieved"], 2), "peak": r["peak"], "unit": r["unit"],
+                "frac": round(r["achieved"] / r["peak"], 4), "traffic": traffic, "kernel": dom,
+                "avg_launch_us": round(r["avg_launch_us"], 2)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(w, X, E, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": "HybridVAE train users/sec",
+            "value": round(value, 1),
+            "unit": "users/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (Zipf(0.8) items, 5+Poisson rows, L2-normalised random E; random-init weights)",
+            "config": {"workload": args.workload, "users": w["users"], "items": w["items"], "emb_dim": D,
+                       "latent": w["latent"], "hidden": w["hidden"], "global_batch": B * world,
+                       "batch_per_gpu": B, "parallelism": f"dp{world}", "decoder": args.precision},
+            "roofline": roofline,
+            "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                        for k, v in roof.items()},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if group is not None:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

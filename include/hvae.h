@@ -93,12 +93,15 @@ int hvae_ln_gelu_drop_fwd(const float* a, const float* ln_w, const float* ln_b, 
                           float* xhat_out, float* rstd_out, void* stream);
 
 /* Backward of Dropout(GELU(LayerNorm(a))): dh -> da, and d(ln_w), d(ln_b)
- * (written, not accumulated). Deterministic column sums through ws. */
+ * (written, not accumulated) and, if d_bias != NULL, d_bias = sum_b da[b, :]
+ * (the bias gradient of the Linear that produced `a`, fused here instead of a
+ * separate column-sum pass). Deterministic column sums through ws. */
 int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const float* rstd,
                           const float* ln_w, const float* ln_b, int64_t nb, int64_t H,
                           float p_drop, const float* drop_mult, uint64_t seed,
                           const int64_t* step_dev, uint32_t layer, int train, float* da,
-                          float* d_ln_w, float* d_ln_b, void* ws, size_t ws_bytes, void* stream);
+                          float* d_ln_w, float* d_ln_b, float* d_bias, void* ws, size_t ws_bytes,
+                          void* stream);
 size_t hvae_ln_gelu_drop_bwd_workspace(int64_t nb, int64_t H);
 
 /* Row-sparse gradient of the item-major first-layer weight W1t [N, H]:
@@ -154,6 +157,9 @@ typedef struct hvae_epilogue {
   const int64_t* step_dev;
   uint32_t tag;           /* Philox stream tag (see hvae_common.h)                 */
   int train;              /* 0 => dropout is identity                              */
+  float* opa_rowsum;      /* [M] or NULL: sum_k op(A)[m, k] (x alpha), computed from */
+                          /* the A tiles the GEMM already stages: the bias gradient */
+                          /* of a Linear alongside its weight gradient dY^T X       */
 } hvae_epilogue;
 int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
                   const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,

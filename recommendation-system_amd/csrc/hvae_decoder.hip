@@ -416,32 +416,36 @@ __global__ void __launch_bounds__(256) k_dec_f32(const float* __restrict__ U, in
   }
 }
 
-// Combine the per-split (m, l, O) partials: one wave per user.
+// Combine the per-split (m, l, O) partials: one block per user; the split
+// weights exp(m_s - M) live in LDS, threads run over D (coalesced rows).
+constexpr int kMaxSplits = 4096;
+
 __global__ void __launch_bounds__(256) k_dec_merge(const float* __restrict__ pm, const float* __restrict__ pl,
                                                    const float* __restrict__ pO, int splits, int64_t nb,
                                                    int64_t D, float* __restrict__ lse, float* __restrict__ O) {
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= nb) return;
+  __shared__ float wsh[kMaxSplits];
+  __shared__ float red[4];
+  const int64_t b = blockIdx.x;
   float M = -INFINITY;
-  for (int s = lane; s < splits; s += 64) M = fmaxf(M, pm[(int64_t)s * nb + b]);
+  for (int s = threadIdx.x; s < splits; s += 256) M = fmaxf(M, pm[(int64_t)s * nb + b]);
   M = wave_max(M);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = M;
+  __syncthreads();
+  M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   float L = 0.f;
-  for (int s = lane; s < splits; s += 64) {
+  for (int s = threadIdx.x; s < splits; s += 256) {
     const float ms = pm[(int64_t)s * nb + b];
-    L += (ms == -INFINITY) ? 0.f : pl[(int64_t)s * nb + b] * __expf(ms - M);
+    const float wv = (ms == -INFINITY) ? 0.f : __expf(ms - M);
+    wsh[s] = wv;
+    L += wv * pl[(int64_t)s * nb + b];
   }
-  L = wave_sum(L);
-  if (lane == 0) lse[b] = M + logf(L);
+  L = block_sum<256>(L, red);  // (its barriers also publish wsh)
+  if (threadIdx.x == 0) lse[b] = M + logf(L);
   if (!O) return;
   const float inv = 1.0f / L;
-  for (int64_t d = lane; d < D; d += 64) {
+  for (int64_t d = threadIdx.x; d < D; d += 256) {
     float acc = 0.f;
-    for (int s = 0; s < splits; ++s) {
-      const float ms = pm[(int64_t)s * nb + b];
-      if (ms == -INFINITY) continue;
-      acc += __expf(ms - M) * pO[((int64_t)s * nb + b) * D + d];
-    }
+    for (int s = 0; s < splits; ++s) acc += wsh[s] * pO[((int64_t)s * nb + b) * D + d];
     O[b * D + d] = acc * inv;
   }
 }
@@ -595,7 +599,7 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 2));
   s = std::min<int64_t>(s, std::max<int64_t>(1, N / std::max<int64_t>(1, 2 * nb)));
   if (s >= 8) s = s / 8 * 8;
-  s = std::max<int64_t>(1, std::min<int64_t>(s, 4096));
+  s = std::max<int64_t>(1, std::min<int64_t>(s, kMaxSplits));
   DecPlan p;
   p.tiles_per_split = cdiv(tiles, s);
   p.splits = (int)cdiv(tiles, p.tiles_per_split);
@@ -738,7 +742,7 @@ extern "C" int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const vo
              : dispatch<false>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st);
   if (rc) return rc;
   if (p.splits > 1) {
-    k_dec_merge<<<(unsigned)cdiv(nb, 4), 256, 0, st>>>(o.m, o.l, o.O, p.splits, nb, D, lse, O);
+    k_dec_merge<<<(unsigned)nb, 256, 0, st>>>(o.m, o.l, o.O, p.splits, nb, D, lse, O);
     HVAE_LAUNCH_CHECK("k_dec_merge");
   }
   if (dtype == HVAE_BF16) {

@@ -168,14 +168,14 @@ __global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
     const float* __restrict__ ln_w, const float* __restrict__ ln_b, int64_t nb, int64_t H,
     float p_drop, float scale, const float* __restrict__ drop_mult, uint64_t seed,
     const int64_t* __restrict__ step_dev, uint32_t tag, int train, float* __restrict__ da,
-    float* __restrict__ part /* [nblocks][2][H] */) {
-  extern __shared__ __attribute__((aligned(16))) float lds_part[];  // [4 waves][2][H]
+    float* __restrict__ part /* [nblocks][3][H] */) {
+  extern __shared__ __attribute__((aligned(16))) float lds_part[];  // [4 waves][3][H]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t step = load_step(step_dev);
   const float invH = 1.0f / (float)H;
-  float4 pg[NV], pb[NV];
+  float4 pg[NV], pb[NV], pa[NV];
 #pragma unroll
-  for (int k = 0; k < NV; ++k) { pg[k] = make_float4(0.f, 0.f, 0.f, 0.f); pb[k] = pg[k]; }
+  for (int k = 0; k < NV; ++k) { pg[k] = make_float4(0.f, 0.f, 0.f, 0.f); pb[k] = pg[k]; pa[k] = pg[k]; }
 
   for (int rr = 0; rr < kLnBwdRows / 4; ++rr) {
     const int64_t b = (int64_t)blockIdx.x * kLnBwdRows + rr * 4 + w;
@@ -220,6 +220,7 @@ __global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
       o.z = rs * (dxh[k].z - m1 - xh[k].z * m2);
       o.w = rs * (dxh[k].w - m1 - xh[k].w * m2);
       *reinterpret_cast<float4*>(da + b * H + e) = o;
+      pa[k].x += o.x; pa[k].y += o.y; pa[k].z += o.z; pa[k].w += o.w;
     }
   }
   // combine the 4 waves' column partials in a fixed order
@@ -227,24 +228,28 @@ __global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
   for (int k = 0; k < NV; ++k) {
     const int64_t e = 4 * (int64_t)(lane + 64 * k);
     if (e >= H) continue;
-    *reinterpret_cast<float4*>(lds_part + (w * 2 + 0) * H + e) = pg[k];
-    *reinterpret_cast<float4*>(lds_part + (w * 2 + 1) * H + e) = pb[k];
+    *reinterpret_cast<float4*>(lds_part + (w * 3 + 0) * H + e) = pg[k];
+    *reinterpret_cast<float4*>(lds_part + (w * 3 + 1) * H + e) = pb[k];
+    *reinterpret_cast<float4*>(lds_part + (w * 3 + 2) * H + e) = pa[k];
   }
   __syncthreads();
-  for (int64_t i = threadIdx.x; i < 2 * H; i += blockDim.x) {
-    const float v = ((lds_part[i] + lds_part[2 * H + i]) + lds_part[4 * H + i]) + lds_part[6 * H + i];
-    part[(int64_t)blockIdx.x * 2 * H + i] = v;
+  for (int64_t i = threadIdx.x; i < 3 * H; i += blockDim.x) {
+    const float v = ((lds_part[i] + lds_part[3 * H + i]) + lds_part[6 * H + i]) + lds_part[9 * H + i];
+    part[(int64_t)blockIdx.x * 3 * H + i] = v;
   }
 }
 
-// Sum the per-block partials [nparts][2][H] -> (d_ln_w, d_ln_b), fixed order.
+// Sum the per-block partials [nparts][3][H] -> (d_ln_w, d_ln_b, d_bias), fixed order.
 __global__ void k_ln_part_reduce(const float* __restrict__ part, int64_t nparts, int64_t H,
-                                 float* __restrict__ d_ln_w, float* __restrict__ d_ln_b) {
+                                 float* __restrict__ d_ln_w, float* __restrict__ d_ln_b,
+                                 float* __restrict__ d_bias) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * H) return;
+  if (i >= 3 * H) return;
   float s = 0.f;
-  for (int64_t p = 0; p < nparts; ++p) s += part[p * 2 * H + i];
-  if (i < H) d_ln_w[i] = s; else d_ln_b[i - H] = s;
+  for (int64_t p = 0; p < nparts; ++p) s += part[p * 3 * H + i];
+  if (i < H) d_ln_w[i] = s;
+  else if (i < 2 * H) d_ln_b[i - H] = s;
+  else if (d_bias) d_bias[i - 2 * H] = s;
 }
 
 // --------------------------------------------------------------------------
@@ -583,14 +588,14 @@ extern "C" int hvae_ln_gelu_drop_fwd(const float* a, const float* ln_w, const fl
 }
 
 extern "C" size_t hvae_ln_gelu_drop_bwd_workspace(int64_t nb, int64_t H) {
-  return (size_t)cdiv(nb, kLnBwdRows) * 2 * (size_t)H * sizeof(float);
+  return (size_t)cdiv(nb, kLnBwdRows) * 3 * (size_t)H * sizeof(float);
 }
 
 extern "C" int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const float* rstd,
                                      const float* ln_w, const float* ln_b, int64_t nb, int64_t H,
                                      float p_drop, const float* drop_mult, uint64_t seed,
                                      const int64_t* step_dev, uint32_t layer, int train, float* da,
-                                     float* d_ln_w, float* d_ln_b, void* ws, size_t ws_bytes,
+                                     float* d_ln_w, float* d_ln_b, float* d_bias, void* ws, size_t ws_bytes,
                                      void* stream) {
   HVAE_REQUIRE(dh && xhat && rstd && ln_w && ln_b && da && d_ln_w && d_ln_b,
                "hvae_ln_gelu_drop_bwd: null arg");
@@ -598,6 +603,7 @@ extern "C" int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const f
   if (nb == 0) {
     HVAE_HIP(hipMemsetAsync(d_ln_w, 0, H * sizeof(float), as_stream(stream)));
     HVAE_HIP(hipMemsetAsync(d_ln_b, 0, H * sizeof(float), as_stream(stream)));
+    if (d_bias) HVAE_HIP(hipMemsetAsync(d_bias, 0, H * sizeof(float), as_stream(stream)));
     return HVAE_OK;
   }
   const size_t need = hvae_ln_gelu_drop_bwd_workspace(nb, H);
@@ -605,14 +611,14 @@ extern "C" int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const f
     HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_ln_gelu_drop_bwd: workspace %zu < %zu", ws_bytes, need);
   const float scale = (p_drop < 1.f) ? 1.0f / (1.0f - p_drop) : 0.f;
   const int64_t nparts = cdiv(nb, kLnBwdRows);
-  const size_t lds = (size_t)8 * H * sizeof(float);
-  HVAE_REQUIRE(lds <= 64 * 1024, "hvae_ln_gelu_drop_bwd: H too large");
+  const size_t lds = (size_t)12 * H * sizeof(float);
+  HVAE_REQUIRE(lds <= 64 * 1024, "hvae_ln_gelu_drop_bwd: H too large (<= 1364)");
   HVAE_NV_DISPATCH(H, (k_ln_gelu_drop_bwd<NV><<<(unsigned)nparts, 256, lds, as_stream(stream)>>>(
                           dh, xhat, rstd, ln_w, ln_b, nb, H, p_drop, scale, drop_mult, seed,
                           step_dev, kTagEncDrop + layer, train, da, (float*)ws)));
   HVAE_LAUNCH_CHECK("k_ln_gelu_drop_bwd");
-  k_ln_part_reduce<<<(unsigned)cdiv(2 * H, 256), 256, 0, as_stream(stream)>>>((const float*)ws, nparts,
-                                                                               H, d_ln_w, d_ln_b);
+  k_ln_part_reduce<<<(unsigned)cdiv(3 * H, 256), 256, 0, as_stream(stream)>>>((const float*)ws, nparts,
+                                                                               H, d_ln_w, d_ln_b, d_bias);
   HVAE_LAUNCH_CHECK("k_ln_part_reduce");
   return HVAE_OK;
 }

@@ -31,6 +31,7 @@ struct EpiArgs {
   const int64_t* step_dev;
   uint32_t tag;
   int train;
+  float* opa_rowsum;  // [M]: sum_k op(A)[m, k] (bias gradient alongside dY^T X)
 };
 
 __device__ __forceinline__ float epi_apply(const EpiArgs& ep, int64_t step, int64_t row, int64_t col,
@@ -97,6 +98,8 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   float4 ra, rb;
+  const bool do_rowsum = ep.opa_rowsum != nullptr && blockIdx.x == 0;
+  float rowsum = 0.f;  // thread t < 64: sum over this block's k range of op(A)[m0 + t][k]
   auto gload = [&](int64_t k0) {
     if (!TA) {  // A[m][k] at A[m*lda + k]
       const int64_t m = m0 + (t >> 2), k = k0 + (t & 3) * 4;
@@ -139,6 +142,10 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
     for (int64_t k0 = kb; k0 < ke; k0 += GBK) {
       const bool more = k0 + GBK < ke;
       if (more) gload(k0 + GBK);
+      if (do_rowsum && t < GBM) {
+#pragma unroll
+        for (int k = 0; k < GBK; ++k) rowsum += sA[k * GLDA + t];
+      }
 #pragma unroll
       for (int kk = 0; kk < GBK / 4; ++kk) {
         const int kr = 4 * kk + (lane >> 4);
@@ -161,6 +168,10 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
     }
   }
 
+  if (do_rowsum && t < GBM && m0 + t < M) {
+    if (slab) slab[(int64_t)gridDim.z * M * N + (int64_t)blockIdx.z * M + m0 + t] = rowsum;
+    else ep.opa_rowsum[m0 + t] = alpha * rowsum;
+  }
   const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP) ? load_step(ep.step_dev) : 0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -185,6 +196,11 @@ __global__ void k_gemm_splitk_reduce(int64_t M, int64_t N, int splits, float alp
                                      const float* __restrict__ slab, float beta, float* __restrict__ C,
                                      int64_t ldc, EpiArgs ep) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ep.opa_rowsum && i < M) {
+    float r = 0.f;
+    for (int z = 0; z < splits; ++z) r += slab[(int64_t)splits * M * N + (int64_t)z * M + i];
+    ep.opa_rowsum[i] = alpha * r;
+  }
   if (i >= M * N) return;
   const int64_t row = i / N, col = i % N;
   float s = 0.f;
@@ -235,7 +251,7 @@ using namespace hvae;
 
 extern "C" size_t hvae_gemm_f32_workspace(int64_t M, int64_t N, int64_t K) {
   const int s = gemm_splits(M, N, K);
-  return s > 1 ? (size_t)s * M * N * sizeof(float) : 0;
+  return s > 1 ? (size_t)s * (M * N + M) * sizeof(float) : 0;
 }
 
 extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
@@ -263,6 +279,7 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
     ep.step_dev = epi->step_dev;
     ep.tag = epi->tag;
     ep.train = epi->train;
+    ep.opa_rowsum = epi->opa_rowsum;
     HVAE_REQUIRE(ep.kind >= 0 && ep.kind <= HVAE_EPI_DROP_BWD, "hvae_gemm_f32: bad epilogue");
     HVAE_REQUIRE(ep.kind != HVAE_EPI_BIAS || ep.bias, "hvae_gemm_f32: BIAS without bias");
     HVAE_REQUIRE(ep.kind != HVAE_EPI_BIAS_GELU_DROP || ep.pre_out, "hvae_gemm_f32: no pre_out");
@@ -271,7 +288,7 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
   hipStream_t st = as_stream(stream);
   int splits = gemm_splits(M, N, K);
   if (splits > 1) {
-    const int64_t fit = ws ? (int64_t)(ws_bytes / ((size_t)M * N * sizeof(float))) : 0;
+    const int64_t fit = ws ? (int64_t)(ws_bytes / ((size_t)(M * N + M) * sizeof(float))) : 0;
     splits = (int)std::min<int64_t>(splits, fit);
     if (splits < 2) splits = 1;
   }
@@ -295,8 +312,8 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
 #undef HVAE_GEMM_CALL
   HVAE_LAUNCH_CHECK("k_gemm_f32");
   if (slab) {
-    k_gemm_splitk_reduce<<<(unsigned)cdiv(M * N, 256), 256, 0, st>>>(M, N, splits, alpha, slab, beta,
-                                                                     C, ldc, ep);
+    k_gemm_splitk_reduce<<<(unsigned)cdiv(std::max(M * N, M), 256), 256, 0, st>>>(M, N, splits, alpha, slab,
+                                                                                  beta, C, ldc, ep);
     HVAE_LAUNCH_CHECK("k_gemm_splitk_reduce");
   }
   return HVAE_OK;

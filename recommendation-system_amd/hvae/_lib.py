@@ -53,6 +53,7 @@ class Epilogue(C.Structure):
     _fields_ = [
         ("kind", cint), ("bias", vp), ("pre_out", vp), ("pre_in", vp), ("p_drop", f32),
         ("drop_mult", vp), ("seed", u64), ("step_dev", vp), ("tag", u32), ("train", cint),
+        ("opa_rowsum", vp),
     ]
 
 
@@ -73,7 +74,7 @@ SIGNATURES = {
     "hvae_encoder_fwd": (cint, [P(CsrBatch), vp, vp, vp, vp, i64, f32, vp, u64, vp, cint, vp, vp, vp, vp]),
     "hvae_ln_gelu_drop_fwd": (cint, [vp, vp, vp, i64, i64, f32, vp, u64, vp, u32, cint, vp, vp, vp, vp]),
     "hvae_ln_gelu_drop_bwd": (cint, [vp, vp, vp, vp, vp, i64, i64, f32, vp, u64, vp, u32, cint, vp, vp, vp,
-                                     vp, sz, vp]),
+                                     vp, vp, sz, vp]),
     "hvae_ln_gelu_drop_bwd_workspace": (sz, [i64, i64]),
     "hvae_w1_rowgrad": (cint, [P(CsrBatch), vp, i64, P(RowGrad), vp, sz, vp]),
     "hvae_w1_rowgrad_workspace": (sz, [i64]),

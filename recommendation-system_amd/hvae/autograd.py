@@ -41,8 +41,8 @@ class EncoderFirstFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh):
         xhat, rstd, ln_w, ln_b = ctx.saved_tensors
-        da, dlw, dlb = ops.ln_gelu_drop_bwd(dh, xhat, rstd, ln_w.detach(), ln_b.detach(), ctx.p, ctx.train, ctx.seed, 0)
-        db1 = ops.colsum(da)
+        da, dlw, dlb, db1 = ops.ln_gelu_drop_bwd(dh, xhat, rstd, ln_w.detach(), ln_b.detach(), ctx.p, ctx.train,
+                                                 ctx.seed, 0, want_dbias=True)
         dW1 = None
         if ctx.needs_input_grad[0]:
             H, N = ctx.W1_shape
@@ -80,8 +80,8 @@ class LinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         if ctx.act:
             x, W, pre = ctx.saved_tensors
-            # d(pre) = dy * dropout * GELU'(pre), fused into a 1x identity "GEMM" epilogue would cost a pass;
-            # instead apply it while forming dx below and for the weight grads use the same d(pre)
+            # d(pre) = dy * dropout * GELU'(pre): the GEMM epilogue applies it while copying dy through an
+            # identity product (module-API path only; the fused trainer folds it into the dq GEMM)
             eye_epi = ops.epilogue(_lib.EPI_GELU_DROP_BWD, pre_in=pre, p_drop=ctx.p, seed=ctx.seed,
                                    tag=_lib.TAG_PROJ_DROP, train=ctx.train)
             eye = torch.eye(dy.shape[1], device=dy.device)
@@ -90,8 +90,10 @@ class LinearFn(torch.autograd.Function):
             x, W = ctx.saved_tensors
             dpre = dy
         dx = ops.gemm(dpre, W.detach()) if ctx.needs_input_grad[0] else None
-        dW = ops.gemm(dpre.t(), x) if ctx.needs_input_grad[1] else None
-        db = ops.colsum(dpre) if ctx.needs_input_grad[2] else None
+        db = torch.empty(W.shape[0], device=dy.device) if ctx.needs_input_grad[2] else None
+        dW = ops.gemm(dpre.t(), x, epi=ops.epilogue(_lib.EPI_NONE, opa_rowsum=db))  # bias grad rides along
+        if not ctx.needs_input_grad[1]:
+            dW = None
         return dx, dW, db, None, None, None
 
 

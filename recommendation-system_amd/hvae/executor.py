@@ -200,7 +200,7 @@ class FusedTrainer:
 
     def __init__(self, model, device, lr: float = 1e-3, weight_decay: float = 0.0, betas=(0.9, 0.999),
                  eps: float = 1e-8, max_norm: float = 5.0, precision: str | None = None, seed: int | None = None,
-                 use_graphs: bool = True):
+                 use_graphs: bool = True, process_group=None):
         if device.type != "cuda":
             raise RuntimeError("FusedTrainer runs the MI355X HIP path only (device must be the HIP device)")
         lib()  # fail loudly now if libhvae.so is missing
@@ -249,6 +249,16 @@ class FusedTrainer:
         self.enorm = ops.row_norm_max(self.E_dec)
         self._bufs: dict[tuple, _StepBuffers] = {}
         self._views()
+        self.dp = None
+        if process_group is not None and torch.distributed.get_world_size(process_group) > 1:
+            from .dist import DPExchange
+            self.dp = DPExchange(process_group, device, lay.n_items, lay.hidden[0])
+            # replicas start from rank 0's parameters (identical seeds make this a no-op, but be explicit)
+            torch.distributed.broadcast(self.flat, 0, group=process_group)
+            seed_t = torch.tensor([self.seed], dtype=torch.int64, device=device)
+            torch.distributed.broadcast(seed_t, 0, group=process_group)
+            # per-rank dropout streams must differ (each rank sees different users)
+            self.seed = int(seed_t.item()) + 7919 * torch.distributed.get_rank(process_group)
 
     # ------------------------------------------------------------ state ---
     def _adopt_parameters(self):
@@ -320,6 +330,17 @@ class FusedTrainer:
     def _launch(self, bf: _StepBuffers, csr: CsrBatch, train: bool, beta: float, p_drop: float,
                 ext: dict | None = None):
         """Enqueue one full step on the current stream (captured into a graph by the caller)."""
+        self._launch_fwd_bwd(bf, csr, train, beta, p_drop, ext)
+        if train:
+            if self.dp is None:
+                self._launch_update(bf.rg, bf)
+            else:
+                self.dp.all_reduce_dense(self.g_small)
+                merged = self.dp.merged_rows(bf.rg.n_unique, bf.rg.item_of, bf.rg.rows)
+                self._launch_update(merged, bf)
+
+    def _launch_fwd_bwd(self, bf: _StepBuffers, csr: CsrBatch, train: bool, beta: float, p_drop: float,
+                        ext: dict | None = None):
         L_, lay = lib(), self.layout
         st = torch.cuda.current_stream(self.device).cuda_stream
         B, H, Lt, d = bf.B, lay.hidden, lay.L, lay.d
@@ -330,7 +351,9 @@ class FusedTrainer:
         encm = ext.get("enc_masks", [None] * len(H))
         csr_ref = C.byref(csr)
 
-        def gemm(ta, tb, M, N, K, A, lda, Bm, ldb, Cm, ldc, epi=None, beta_=0.0):
+        def gemm(ta, tb, M, N, K, A, lda, Bm, ldb, Cm, ldc, epi=None, beta_=0.0, rowsum=None):
+            if rowsum is not None:  # bias gradient = sum_k op(A)[m, k], fused into the weight-gradient GEMM
+                epi = Epilogue(_lib.EPI_NONE, None, None, None, 0.0, None, 0, None, 0, 0, ptr(rowsum))
             check(L_.hvae_gemm_f32(ta, tb, M, N, K, 1.0, A, lda, Bm, ldb, beta_, Cm, ldc,
                                    C.byref(epi) if epi is not None else None, ws, wsn, st), "gemm")
 
@@ -342,14 +365,14 @@ class FusedTrainer:
         for k in range(1, len(H)):
             i = 4 * k
             W = self.P[f"encoder.{i}.weight"]
-            epi = Epilogue(_lib.EPI_BIAS, ptr(self.P[f"encoder.{i}.bias"]), None, None, 0.0, None, 0, None, 0, 0)
+            epi = Epilogue(_lib.EPI_BIAS, ptr(self.P[f"encoder.{i}.bias"]), None, None, 0.0, None, 0, None, 0, 0, None)
             gemm(0, 1, B, H[k], H[k - 1], ptr(bf.h[k - 1]), H[k - 1], ptr(W), H[k - 1], ptr(bf.a[k]), H[k], epi)
             check(L_.hvae_ln_gelu_drop_fwd(ptr(bf.a[k]), ptr(self.P[f"encoder.{i + 1}.weight"]),
                                            ptr(self.P[f"encoder.{i + 1}.bias"]), B, H[k], p_drop, ptr(encm[k]), seed,
                                            step, k, tr, ptr(bf.h[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]), st),
                   "ln_gelu_drop_fwd")
         Hl = H[-1]
-        epi_b = Epilogue(_lib.EPI_BIAS, ptr(self.b_heads), None, None, 0.0, None, 0, None, 0, 0)
+        epi_b = Epilogue(_lib.EPI_BIAS, ptr(self.b_heads), None, None, 0.0, None, 0, None, 0, 0, None)
         gemm(0, 1, B, 2 * Lt, Hl, ptr(bf.h[-1]), Hl, ptr(self.W_heads), Hl, ptr(bf.heads), 2 * Lt, epi_b)
         mu, lv = bf.heads, bf.heads[:, Lt:]
         check(L_.hvae_reparam_kl_fwd(ptr(mu), ptr(lv), 2 * Lt, B, Lt, tr, ptr(ext.get("eps")), seed, step,
@@ -358,12 +381,14 @@ class FusedTrainer:
             Wa, ba = self.P["projection_layer.0.weight"], self.P["projection_layer.0.bias"]
             Wb, bb = self.P["projection_layer.3.weight"], self.P["projection_layer.3.bias"]
             epi1 = Epilogue(_lib.EPI_BIAS_GELU_DROP, ptr(ba), ptr(bf.p1), None, p_drop, ptr(ext.get("proj_mask")),
-                            seed, step, _lib.TAG_PROJ_DROP, tr)
+                            seed, step, _lib.TAG_PROJ_DROP, tr, None)
             gemm(0, 1, B, d, Lt, ptr(bf.z), Lt, ptr(Wa), Lt, ptr(bf.q), d, epi1)
-            epi2 = Epilogue(_lib.EPI_BIAS, ptr(bb), None, None, 0.0, None, 0, None, 0, 0)
+            epi2 = Epilogue(_lib.EPI_BIAS, ptr(bb), None, None, 0.0, None, 0, None, 0, 0, None)
             gemm(0, 1, B, d, d, ptr(bf.q), d, ptr(Wb), d, ptr(bf.u), d, epi2)
+        self._probe_begin("decoder_fwd")
         check(L_.hvae_decoder_fwd(self.dec_dtype, ptr(bf.u), d, ptr(self.E_dec), ptr(self.enorm), B, lay.n_items, d,
                                   ptr(bf.lse), ptr(bf.O) if train else None, ws, wsn, st), "decoder_fwd")
+        self._probe_end("decoder_fwd")
         check(L_.hvae_decoder_bwd(csr_ref, ptr(bf.u), d, ptr(self.E32), d, ptr(bf.lse), ptr(bf.O) if train else None,
                                   1.0 / B, ptr(bf.recon_rows), ptr(bf.dU) if train else None, st), "decoder_bwd")
         accum = self.accum_train if train else self.accum_val
@@ -374,30 +399,27 @@ class FusedTrainer:
         # ----------------------------------------------------- backward ---
         G = self.G
         if lay.has_proj:
-            gemm(1, 0, d, d, B, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d)
-            check(L_.hvae_colsum(ptr(bf.dU), B, d, d, 0.0, ptr(G["projection_layer.3.bias"]), ws, wsn, st), "colsum")
+            gemm(1, 0, d, d, B, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d,
+                 rowsum=G["projection_layer.3.bias"])
             epi3 = Epilogue(_lib.EPI_GELU_DROP_BWD, None, None, ptr(bf.p1), p_drop, ptr(ext.get("proj_mask")), seed,
-                            step, _lib.TAG_PROJ_DROP, tr)
+                            step, _lib.TAG_PROJ_DROP, tr, None)
             gemm(0, 0, B, d, d, ptr(bf.dU), d, ptr(Wb), d, ptr(bf.dp1), d, epi3)
-            gemm(1, 0, d, Lt, B, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt)
-            check(L_.hvae_colsum(ptr(bf.dp1), B, d, d, 0.0, ptr(G["projection_layer.0.bias"]), ws, wsn, st),
-                  "colsum")
+            gemm(1, 0, d, Lt, B, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt,
+                 rowsum=G["projection_layer.0.bias"])
             gemm(0, 0, B, Lt, d, ptr(bf.dp1), d, ptr(Wa), Lt, ptr(bf.dz), Lt)
         dmu, dlv = bf.dheads, bf.dheads[:, Lt:]
         check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B, tr,
                                      ptr(dmu), ptr(dlv), 2 * Lt, st), "reparam_kl_bwd")
-        gemm(1, 0, 2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl)
-        check(L_.hvae_colsum(ptr(bf.dheads), B, 2 * Lt, 2 * Lt, 0.0, ptr(self.gb_heads), ws, wsn, st), "colsum")
+        gemm(1, 0, 2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl,
+             rowsum=self.gb_heads)
         gemm(0, 0, B, Hl, 2 * Lt, ptr(bf.dheads), 2 * Lt, ptr(self.W_heads), Hl, ptr(bf.dh[-1]), Hl)
         for k in range(len(H) - 1, -1, -1):
             i = 4 * k
             check(L_.hvae_ln_gelu_drop_bwd(ptr(bf.dh[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]),
                                            ptr(self.P[f"encoder.{i + 1}.weight"]), ptr(self.P[f"encoder.{i + 1}.bias"]),
                                            B, H[k], p_drop, ptr(encm[k]), seed, step, k, tr, ptr(bf.da[k]),
-                                           ptr(G[f"encoder.{i + 1}.weight"]), ptr(G[f"encoder.{i + 1}.bias"]), ws,
-                                           wsn, st), "ln_gelu_drop_bwd")
-            check(L_.hvae_colsum(ptr(bf.da[k]), B, H[k], H[k], 0.0, ptr(G[f"encoder.{i}.bias"]), ws, wsn, st),
-                  "colsum")
+                                           ptr(G[f"encoder.{i + 1}.weight"]), ptr(G[f"encoder.{i + 1}.bias"]),
+                                           ptr(G[f"encoder.{i}.bias"]), ws, wsn, st), "ln_gelu_drop_bwd")
             if k > 0:
                 W = self.P[f"encoder.{i}.weight"]
                 gemm(1, 0, H[k], H[k - 1], B, ptr(bf.da[k]), H[k], ptr(bf.h[k - 1]), H[k - 1],
@@ -405,15 +427,39 @@ class FusedTrainer:
                 gemm(0, 0, B, H[k - 1], H[k], ptr(bf.da[k]), H[k], ptr(W), H[k - 1], ptr(bf.dh[k - 1]), H[k - 1])
         check(L_.hvae_w1_rowgrad(csr_ref, ptr(bf.da[0]), H[0], bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st),
               "w1_rowgrad")
-        # ------------------------------------------------ clip + Adam ---
-        check(L_.hvae_clip_grad_norm(ptr(self.g_small), lay.n_small, bf.rg.ref, H[0], self.max_norm,
+
+    def _launch_update(self, rg, bf: _StepBuffers):
+        """clip_grad_norm_(5.0) + Adam over the flat state, then step += 1."""
+        L_, lay = lib(), self.layout
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        H = lay.hidden
+        ws, wsn = ptr(bf.ws), bf.ws.numel()
+        step = ptr(self.step_dev)
+        check(L_.hvae_clip_grad_norm(ptr(self.g_small), lay.n_small, rg.ref, H[0], self.max_norm,
                                      ptr(self.norm), ptr(self.coef), ws, wsn, st), "clip_grad_norm")
         cfg = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, self.coef)
-        check(L_.hvae_adam_rows(C.byref(cfg), ptr(self.w1t), ptr(self.m_w1t), ptr(self.v_w1t), bf.rg.ref,
+        self._probe_begin("adam_rows")
+        check(L_.hvae_adam_rows(C.byref(cfg), ptr(self.w1t), ptr(self.m_w1t), ptr(self.v_w1t), rg.ref,
                                 lay.n_items, H[0], st), "adam_rows")
+        self._probe_end("adam_rows")
         check(L_.hvae_adam_dense(C.byref(cfg), ptr(self.small), ptr(self.m_small), ptr(self.v_small),
                                  ptr(self.g_small), lay.n_small, st), "adam_dense")
         check(L_.hvae_counter_add(step, 1, st), "counter_add")
+
+    # ----------------------------------------------- live kernel timing ---
+    probe: dict | None = None  # {"kernel": name, "events": [(start, end), ...]} (eager steps only)
+
+    def _probe_begin(self, name):
+        if self.probe is not None and self.probe["kernel"] == name:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream(self.device))
+            self.probe["_open"] = ev
+
+    def _probe_end(self, name):
+        if self.probe is not None and self.probe["kernel"] == name:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream(self.device))
+            self.probe["events"].append((self.probe.pop("_open"), ev))
 
     def _advance(self, B: int):
         check(lib().hvae_counter_add(ptr(self.boff), B, torch.cuda.current_stream(self.device).cuda_stream),
@@ -432,7 +478,8 @@ class FusedTrainer:
         return bf.loss3
 
     def run_epoch(self, data: DeviceData, batch_size: int, shuffle: bool, beta_fn, p_drop: float,
-                  train: bool = True, drop_last: bool = False, generator: torch.Generator | None = None) -> dict:
+                  train: bool = True, drop_last: bool = False, generator: torch.Generator | None = None,
+                  max_batches: int | None = None) -> dict:
         """Iterate the dataset in batches (DataLoader semantics: shuffle, drop_last=False).
 
         beta_fn(step_index) -> beta; a constant beta lets every full batch replay one graph.
@@ -452,13 +499,15 @@ class FusedTrainer:
         n_full, tail = divmod(n, batch_size)
         if drop_last:
             tail = 0
+        if max_batches is not None:  # bounded pass (benchmarks): full batches only
+            n_full, tail = min(n_full, max_batches), 0
         n_batches = n_full + (1 if tail else 0)
         const_beta = getattr(beta_fn, "constant", None)
         B = batch_size
         for bi in range(n_full):
             beta = beta_fn(bi)
             bf = self._buffers(B, data.max_batch_nnz(B), train)
-            if self.use_graphs and const_beta is not None:
+            if self.use_graphs and const_beta is not None and self.dp is None:
                 if bf.graph is None or bf.graph_key != (id(data), beta, p_drop):
                     if bi == 0 and bf.graph is None:
                         # first use: run eagerly (loads kernels, sets attributes), capture afterwards

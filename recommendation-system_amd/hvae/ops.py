@@ -101,19 +101,22 @@ def ln_gelu_drop_fwd(a, ln_w, ln_b, p_drop, train, seed, layer, step=None, drop_
     return h, xhat, rstd
 
 
-def ln_gelu_drop_bwd(dh, xhat, rstd, ln_w, ln_b, p_drop, train, seed, layer, step=None, drop_mult=None):
+def ln_gelu_drop_bwd(dh, xhat, rstd, ln_w, ln_b, p_drop, train, seed, layer, step=None, drop_mult=None,
+                     want_dbias=False):
+    """-> (da, d_ln_w, d_ln_b) or, with want_dbias, (da, d_ln_w, d_ln_b, sum_rows(da))."""
     require_hip(dh, xhat, rstd, ln_w, ln_b)
     dh = dh.contiguous()
     nb, H = dh.shape
     da = torch.empty_like(dh)
     dw = torch.empty(H, device=dh.device)
     db = torch.empty(H, device=dh.device)
+    dbias = torch.empty(H, device=dh.device) if want_dbias else None
     need = lib().hvae_ln_gelu_drop_bwd_workspace(nb, H)
     ws = workspace(dh.device, need)
     check(lib().hvae_ln_gelu_drop_bwd(ptr(dh), ptr(xhat), ptr(rstd), ptr(ln_w), ptr(ln_b), nb, H, float(p_drop),
                                       ptr(drop_mult), seed, ptr(step), layer, int(train), ptr(da), ptr(dw), ptr(db),
-                                      ptr(ws), ws.numel(), stream_of(dh)), "hvae_ln_gelu_drop_bwd")
-    return da, dw, db
+                                      ptr(dbias), ptr(ws), ws.numel(), stream_of(dh)), "hvae_ln_gelu_drop_bwd")
+    return (da, dw, db, dbias) if want_dbias else (da, dw, db)
 
 
 class RowGradBuffers:
@@ -190,9 +193,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, alph
 
 
 def epilogue(kind, bias=None, pre_out=None, pre_in=None, p_drop=0.0, drop_mult=None, seed=0, step=None,
-             tag=0, train=False) -> Epilogue:
+             tag=0, train=False, opa_rowsum=None) -> Epilogue:
     return Epilogue(kind, ptr(bias), ptr(pre_out), ptr(pre_in), float(p_drop), ptr(drop_mult), int(seed), ptr(step),
-                    int(tag), int(train))
+                    int(tag), int(train), ptr(opa_rowsum))
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor | None = None, beta=0.0):

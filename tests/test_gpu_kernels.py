@@ -66,6 +66,18 @@ def test_gemm_epilogues(ops, hip_device):
     assert _maxrel(out2, x.grad) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(384, 384, 64), (256, 512, 4096), (70, 33, 5)])
+def test_gemm_tn_bias_rowsum(ops, hip_device, M, N, K):
+    """dW = dY^T X with the bias gradient sum_k dY[k, m] computed from the same staged tiles."""
+    from hvae import _lib
+    g = torch.Generator().manual_seed(M + K)
+    dY, X = torch.randn(K, M, generator=g), torch.randn(K, N, generator=g)
+    rs = torch.empty(M, device=hip_device)
+    out = ops.gemm(dY.to(hip_device).t(), X.to(hip_device), epi=ops.epilogue(_lib.EPI_NONE, opa_rowsum=rs))
+    assert _maxrel(out, dY.double().t() @ X.double()) < 2e-5 * max(1.0, math.sqrt(K) / 8)
+    assert _maxrel(rs, dY.double().sum(0)) < 1e-5
+
+
 def test_colsum(ops, hip_device):
     X = torch.randn(3000, 77)
     out = ops.colsum(X.to(hip_device))
@@ -97,8 +109,10 @@ def test_encoder_fwd_bwd(ops, hip_device, H):
     lw_ = lw.clone().requires_grad_(True)
     lb_ = lb.clone().requires_grad_(True)
     (R.gelu(R.layer_norm(a, lw_, lb_)) * mult * dh).sum().backward()
-    da, dlw, dlb = ops.ln_gelu_drop_bwd(dv(dh), xhat, rstd, dv(lw), dv(lb), 0.25, True, 0, 0, drop_mult=dv(mult))
+    da, dlw, dlb, dbias = ops.ln_gelu_drop_bwd(dv(dh), xhat, rstd, dv(lw), dv(lb), 0.25, True, 0, 0,
+                                               drop_mult=dv(mult), want_dbias=True)
     assert _maxrel(da, a.grad) < 5e-5
+    assert _maxrel(dbias, a.grad.sum(0)) < 5e-5
     assert _maxrel(dlw, lw_.grad) < 5e-5 and _maxrel(dlb, lb_.grad) < 5e-5
     rg = ops.RowGradBuffers(500, H, int(X.nnz), hip_device)
     ops.w1_rowgrad(xd, da, rg)
