@@ -254,6 +254,8 @@ int hvae_adam_rows(const hvae_adam* cfg, float* p, float* m, float* v, const hva
                    int64_t N, int64_t H, void* stream);
 /* *counter += delta (device-side step/batch counters for graph replay). */
 int hvae_counter_add(int64_t* counter, int64_t delta, void* stream);
+/* *a += da and, if b != NULL, *b += db, in one launch (end of a train step). */
+int hvae_counters_add(int64_t* a, int64_t da, int64_t* b, int64_t db, void* stream);
 
 /* ------------------------------------------------------------ eval (K16) -- */
 /* scores[r, c] = U[user_row[r], :] . E32[cand[r, c], :]   (fp32)

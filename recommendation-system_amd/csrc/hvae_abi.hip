@@ -16,8 +16,11 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
-__global__ void k_counter_add(int64_t* c, int64_t d) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) *c += d;
+__global__ void k_counter_add(int64_t* c, int64_t d, int64_t* c2, int64_t d2) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    *c += d;
+    if (c2) *c2 += d2;
+  }
 }
 
 __global__ void k_cast_bf16(const float* __restrict__ x, bf16_t* __restrict__ y, int64_t n) {
@@ -49,7 +52,14 @@ extern "C" int hvae_last_error(char* buf, size_t len) {
 
 extern "C" int hvae_counter_add(int64_t* counter, int64_t delta, void* stream) {
   HVAE_REQUIRE(counter, "hvae_counter_add: null counter");
-  k_counter_add<<<1, 64, 0, as_stream(stream)>>>(counter, delta);
+  k_counter_add<<<1, 64, 0, as_stream(stream)>>>(counter, delta, nullptr, 0);
+  HVAE_LAUNCH_CHECK("k_counter_add");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_counters_add(int64_t* a, int64_t da, int64_t* b, int64_t db, void* stream) {
+  HVAE_REQUIRE(a, "hvae_counters_add: null counter");
+  k_counter_add<<<1, 64, 0, as_stream(stream)>>>(a, da, b, db);
   HVAE_LAUNCH_CHECK("k_counter_add");
   return HVAE_OK;
 }

@@ -51,7 +51,7 @@ constexpr float kOffsetSpan = 60.0f;
 constexpr float kUnderflowSpan = 70.0f;
 
 struct DecOut {
-  int* flag;    // [nb] set when a user's result must be recomputed exactly (bf16 path)
+  int* flag;    // [nb] (direct) / [splits][nb] (partial): 1 = recompute this user exactly (bf16 path)
   float* m;     // [splits][nb] running max      (partial mode)
   float* l;     // [splits][nb] sum exp(s - m)   (partial mode)
   float* O;     // [splits][nb][D] partial O, or final O [nb][D] (direct mode)
@@ -240,8 +240,12 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
   if (!wave_active) return;
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
   if (user >= nb) return;
-  // the max term itself may have lost precision: exact recompute by k_dec_fixup
-  if (h == 0 && t_beg < t_end && !(mtrue >= m - kUnderflowSpan && ltot > 0.f)) out.flag[user] = 1;
+  // the max term itself may have lost precision: exact recompute (k_dec_fixup / k_dec_merge).
+  // Written for every user every call, so the flags need no clearing pass.
+  if (h == 0) {
+    const int f = !(mtrue >= m - kUnderflowSpan && ltot > 0.f);
+    out.flag[out.direct ? user : (int64_t)split * nb + user] = f;
+  }
   if (out.direct) {
     const float inv = 1.0f / ltot;
     if (h == 0) out.lse[user] = m + logf(ltot);
@@ -420,17 +424,36 @@ __global__ void __launch_bounds__(256) k_dec_f32(const float* __restrict__ U, in
 // weights exp(m_s - M) live in LDS, threads run over D (coalesced rows).
 constexpr int kMaxSplits = 4096;
 
+__device__ void exact_user(int64_t b, const float* __restrict__ U, int64_t ldu, const bf16_t* __restrict__ E,
+                           int64_t N, int64_t D, float* __restrict__ lse, float* __restrict__ O, float* red,
+                           float* pbuf);
+
 __global__ void __launch_bounds__(256) k_dec_merge(const float* __restrict__ pm, const float* __restrict__ pl,
-                                                   const float* __restrict__ pO, int splits, int64_t nb,
-                                                   int64_t D, float* __restrict__ lse, float* __restrict__ O) {
+                                                   const float* __restrict__ pO, const int* __restrict__ pflag,
+                                                   int splits, int64_t nb, int64_t D, float* __restrict__ lse,
+                                                   float* __restrict__ O, const float* __restrict__ U, int64_t ldu,
+                                                   const bf16_t* __restrict__ E, int64_t N) {
   __shared__ float wsh[kMaxSplits];
   __shared__ float red[4];
+  __shared__ float pbuf[256];
+  __shared__ int any_flag;
   const int64_t b = blockIdx.x;
+  if (threadIdx.x == 0) any_flag = 0;
   float M = -INFINITY;
-  for (int s = threadIdx.x; s < splits; s += 256) M = fmaxf(M, pm[(int64_t)s * nb + b]);
+  int fl = 0;
+  for (int s = threadIdx.x; s < splits; s += 256) {
+    M = fmaxf(M, pm[(int64_t)s * nb + b]);
+    if (pflag) fl |= pflag[(int64_t)s * nb + b];
+  }
   M = wave_max(M);
+  __syncthreads();
+  if (fl) any_flag = 1;
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = M;
   __syncthreads();
+  if (any_flag) {  // rare: exact two-pass recompute of this user (uniform branch)
+    exact_user(b, U, ldu, E, N, D, lse, O, red, pbuf);
+    return;
+  }
   M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
   float L = 0.f;
   for (int s = threadIdx.x; s < splits; s += 256) {
@@ -450,17 +473,12 @@ __global__ void __launch_bounds__(256) k_dec_merge(const float* __restrict__ pm,
   }
 }
 
-// Exact recompute of the users flagged by k_dec_bf16 (their max score sits
-// more than kUnderflowSpan below the fixed offset: only possible for |u| in
-// the hundreds). Two passes in fp32 over the bf16 E, one block per flagged
-// user; blocks of unflagged users exit at once.
-__global__ void __launch_bounds__(256) k_dec_fixup(const int* __restrict__ flag, const float* __restrict__ U,
-                                                   int64_t ldu, const bf16_t* __restrict__ E, int64_t N,
-                                                   int64_t D, float* __restrict__ lse, float* __restrict__ O) {
-  __shared__ float red[4];
-  __shared__ float pbuf[256];
-  const int64_t b = blockIdx.x;
-  if (!flag[b]) return;
+// Exact recompute of one user flagged by k_dec_bf16 (its max score sits more
+// than kUnderflowSpan below the fixed offset: only possible for |u| in the
+// hundreds). Two passes in fp32 over the bf16 E by one 256-thread block.
+__device__ void exact_user(int64_t b, const float* __restrict__ U, int64_t ldu, const bf16_t* __restrict__ E,
+                           int64_t N, int64_t D, float* __restrict__ lse, float* __restrict__ O, float* red,
+                           float* pbuf) {
   const float* u = U + b * ldu;
   auto score = [&](int64_t i) {
     float s = 0.f;
@@ -470,6 +488,7 @@ __global__ void __launch_bounds__(256) k_dec_fixup(const int* __restrict__ flag,
   float mx = -INFINITY;
   for (int64_t i = threadIdx.x; i < N; i += 256) mx = fmaxf(mx, score(i));
   mx = wave_max(mx);
+  __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
   __syncthreads();
   mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
@@ -500,6 +519,16 @@ __global__ void __launch_bounds__(256) k_dec_fixup(const int* __restrict__ flag,
       if (d < D) O[b * D + d] = oacc[k] / l;
     }
   }
+}
+
+// Direct (single-split) mode: one block per user, flagged users only do work.
+__global__ void __launch_bounds__(256) k_dec_fixup(const int* __restrict__ flag, const float* __restrict__ U,
+                                                   int64_t ldu, const bf16_t* __restrict__ E, int64_t N,
+                                                   int64_t D, float* __restrict__ lse, float* __restrict__ O) {
+  __shared__ float red[4];
+  __shared__ float pbuf[256];
+  if (!flag[blockIdx.x]) return;
+  exact_user(blockIdx.x, U, ldu, E, N, D, lse, O, red, pbuf);
 }
 
 // max_i ||E_i||_2 over an fp32 or bf16 [N, D] matrix (score bound of the bf16 path).
@@ -614,7 +643,7 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
 }
 
 static size_t dec_ws_bytes(int splits, int64_t nb, int64_t D) {
-  const size_t flags = (size_t)cdiv(nb * sizeof(int), 256) * 256;
+  const size_t flags = (size_t)cdiv((int64_t)splits * nb * sizeof(int), 256) * 256;
   return flags + (splits > 1 ? (size_t)splits * nb * (D + 2) * sizeof(float) : 0);
 }
 
@@ -711,22 +740,22 @@ extern "C" int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const vo
   HVAE_REQUIRE(N < (1ll << 31), "hvae_decoder_fwd: N too large");
   if (nb == 0) return HVAE_OK;
   hipStream_t st = as_stream(stream);
-  const size_t flag_bytes = (size_t)cdiv(nb * sizeof(int), 256) * 256;
-  if (!ws || ws_bytes < flag_bytes)
-    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_decoder_fwd: workspace %zu < %zu", ws_bytes, flag_bytes);
   DecPlan p = dec_plan(dtype, nb, N, D);
+  if (!ws || ws_bytes < dec_ws_bytes(1, nb, D))
+    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_decoder_fwd: workspace %zu < %zu", ws_bytes, dec_ws_bytes(1, nb, D));
   if (p.splits > 1 && ws_bytes < dec_ws_bytes(p.splits, nb, D)) {
     // fall back to fewer splits that fit the given workspace
-    int64_t fit = (int64_t)((ws_bytes - flag_bytes) / ((size_t)nb * (D + 2) * sizeof(float)));
+    int64_t fit = (int64_t)(ws_bytes / ((size_t)nb * ((D + 2) * sizeof(float) + sizeof(int)))) - 1;
     const int64_t tiles = cdiv(N, dtype == HVAE_BF16 ? kBfTI : kF32TI);
     if (fit < 2) fit = 1;
+    fit = std::min<int64_t>(fit, kMaxSplits);
     p.tiles_per_split = cdiv(tiles, fit);
     p.splits = (int)cdiv(tiles, p.tiles_per_split);
     p.blocks = cdiv(nb, dtype == HVAE_BF16 ? kBfUsersPerBlock : kF32UsersPerBlock) * p.splits;
   }
+  const size_t flag_bytes = (size_t)cdiv((int64_t)p.splits * nb * sizeof(int), 256) * 256;
   DecOut o{};
   o.flag = (int*)ws;
-  HVAE_HIP(hipMemsetAsync(o.flag, 0, nb * sizeof(int), st));
   if (p.splits == 1) {
     o.direct = 1;
     o.lse = lse;
@@ -741,12 +770,13 @@ extern "C" int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const vo
   int rc = O ? dispatch<true>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st)
              : dispatch<false>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st);
   if (rc) return rc;
+  const bool bf = dtype == HVAE_BF16;
+  HVAE_REQUIRE(!bf || D <= 1024, "hvae_decoder_fwd: D too large for the exact fixup");
   if (p.splits > 1) {
-    k_dec_merge<<<(unsigned)nb, 256, 0, st>>>(o.m, o.l, o.O, p.splits, nb, D, lse, O);
+    k_dec_merge<<<(unsigned)nb, 256, 0, st>>>(o.m, o.l, o.O, bf ? o.flag : nullptr, p.splits, nb, D, lse, O, U,
+                                             ldu, (const bf16_t*)E, N);
     HVAE_LAUNCH_CHECK("k_dec_merge");
-  }
-  if (dtype == HVAE_BF16) {
-    HVAE_REQUIRE(D <= 1024, "hvae_decoder_fwd: D too large for the fixup");
+  } else if (bf) {
     k_dec_fixup<<<(unsigned)nb, 256, 0, st>>>(o.flag, U, ldu, (const bf16_t*)E, N, D, lse, O);
     HVAE_LAUNCH_CHECK("k_dec_fixup");
   }

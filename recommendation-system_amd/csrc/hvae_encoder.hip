@@ -436,6 +436,74 @@ __global__ void __launch_bounds__(256) k_rg_scan3(int32_t* __restrict__ cnt, int
   }
 }
 
+// Small catalogs (N <= kSmallScanItems): scan1 + scan2 + scan3 in one block,
+// chunk by chunk with a running carry (one launch instead of three).
+constexpr int64_t kSmallScanItems = 64 * 1024;
+
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// 1024 threads x 4 items per chunk; wave shuffles + one LDS pass per chunk.
+__global__ void __launch_bounds__(1024) k_rg_scan_small(int32_t* __restrict__ cnt, int64_t N,
+                                                        int32_t* __restrict__ slot_of, int32_t* __restrict__ item_of,
+                                                        int32_t* __restrict__ seg_off, int64_t cap,
+                                                        int32_t* __restrict__ n_unique) {
+  __shared__ int wf[16], wc[16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t carry_f = 0, carry_c = 0;
+  for (int64_t base0 = 0; base0 < N; base0 += 4096) {
+    const int64_t base = base0 + threadIdx.x * 4;
+    int c[4];
+    int nf = 0, nc = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t j = base + i;
+      c[i] = (j < N) ? cnt[j] : 0;
+      nf += c[i] > 0;
+      nc += c[i];
+    }
+    const int xf = wave_incl_scan(nf, lane), xc = wave_incl_scan(nc, lane);
+    if (lane == 63) { wf[w] = xf; wc[w] = xc; }
+    __syncthreads();
+    int pf = 0, pc = 0, tf = 0, tc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (k < w) { pf += wf[k]; pc += wc[k]; }
+      tf += wf[k];
+      tc += wc[k];
+    }
+    int64_t slot = carry_f + pf + xf - nf;
+    int64_t off = carry_c + pc + xc - nc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (c[i] > 0) {
+        const int64_t j = base + i;
+        if (slot < cap) {
+          slot_of[j] = (int32_t)slot;
+          item_of[slot] = (int32_t)j;
+          seg_off[slot] = (int32_t)off;
+        }
+        cnt[j] = 0;
+        ++slot;
+        off += c[i];
+      }
+    }
+    carry_f += tf;
+    carry_c += tc;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    *n_unique = (int32_t)carry_f;
+    if (carry_f <= cap) seg_off[carry_f] = (int32_t)carry_c;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_rg_scatter(const int64_t* __restrict__ row_ptr,
                                                     const int32_t* __restrict__ col_idx,
                                                     const float* __restrict__ vals,
@@ -668,15 +736,20 @@ extern "C" int hvae_w1_rowgrad(const hvae_csr_batch* x, const float* da, int64_t
   const unsigned rgrid = (unsigned)cdiv(x->nb, 4);
   k_rg_count<<<rgrid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->rows, x->rows_offset, x->nb, rg->cnt);
   HVAE_LAUNCH_CHECK("k_rg_count");
-  const int64_t nblk = cdiv(N, kScanItemsPerBlock);
-  int64_t* blocktot = (int64_t*)ws;
-  k_rg_scan1<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, blocktot);
-  HVAE_LAUNCH_CHECK("k_rg_scan1");
-  k_rg_scan2<<<1, 1024, 0, st>>>(blocktot, nblk, rg->n_unique, rg->seg_off, rg->cap);
-  HVAE_LAUNCH_CHECK("k_rg_scan2");
-  k_rg_scan3<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, blocktot, rg->slot_of, rg->item_of,
-                                             rg->seg_off, rg->cap);
-  HVAE_LAUNCH_CHECK("k_rg_scan3");
+  if (N <= kSmallScanItems) {
+    k_rg_scan_small<<<1, 1024, 0, st>>>(rg->cnt, N, rg->slot_of, rg->item_of, rg->seg_off, rg->cap, rg->n_unique);
+    HVAE_LAUNCH_CHECK("k_rg_scan_small");
+  } else {
+    const int64_t nblk = cdiv(N, kScanItemsPerBlock);
+    int64_t* blocktot = (int64_t*)ws;
+    k_rg_scan1<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, blocktot);
+    HVAE_LAUNCH_CHECK("k_rg_scan1");
+    k_rg_scan2<<<1, 1024, 0, st>>>(blocktot, nblk, rg->n_unique, rg->seg_off, rg->cap);
+    HVAE_LAUNCH_CHECK("k_rg_scan2");
+    k_rg_scan3<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, blocktot, rg->slot_of, rg->item_of, rg->seg_off,
+                                               rg->cap);
+    HVAE_LAUNCH_CHECK("k_rg_scan3");
+  }
   k_rg_scatter<<<rgrid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->vals, x->rows, x->rows_offset, x->nb, rg->slot_of,
                                       rg->seg_off, rg->fill, rg->contrib_row, rg->contrib_val,
                                       rg->cap);

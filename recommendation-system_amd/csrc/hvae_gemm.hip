@@ -16,9 +16,15 @@ namespace hvae {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int GBM = 64, GBN = 64, GBK = 16;
-constexpr int GLDA = GBM + 16;  // row stride of the k-major LDS images (see header)
-constexpr int GLDB = GBN + 16;
+constexpr int GBM = 64, GBN = 64, GBK = 32;
+// LDS images keep each operand in its memory order (no transposing stores):
+//   row-major A[m][k] / B^T[n][k]  -> [64 rows][GBK + 2] (float2 stores; fragment reads
+//                                     hit banks 2*row + k: conflict-free for ds_read_b32)
+//   k-major A^T[k][m] / B[k][n]    -> [GBK rows][64 + 16] (float4 stores; rows 16 banks apart)
+constexpr int GSR = GBK + 2;   // stride of row-major images
+constexpr int GSK = 64 + 16;   // stride of k-major images
+constexpr int GIMG = (64 * GSR > GBK * GSK) ? 64 * GSR : GBK * GSK;
+constexpr int GLD4 = (64 * GBK / 4) / 256;  // float4 staged per thread per operand
 
 struct EpiArgs {
   int kind;
@@ -83,8 +89,8 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
                                                   float* __restrict__ C, int64_t ldc,
                                                   float* __restrict__ slab, EpiArgs ep, bool vec_a,
                                                   bool vec_b) {
-  __shared__ __attribute__((aligned(16))) float sA[GBK * GLDA];
-  __shared__ __attribute__((aligned(16))) float sB[GBK * GLDB];
+  __shared__ __attribute__((aligned(16))) float sA[GIMG];
+  __shared__ __attribute__((aligned(16))) float sB[GIMG];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
   const int64_t kb = (int64_t)blockIdx.z * k_per_split;
@@ -97,43 +103,55 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float4 ra, rb;
+  float4 ra[GLD4], rb[GLD4];
   const bool do_rowsum = ep.opa_rowsum != nullptr && blockIdx.x == 0;
   float rowsum = 0.f;  // thread t < 64: sum over this block's k range of op(A)[m0 + t][k]
+  // Operand element (r = m or n, k): row-major sources stage f -> (r = f / (GBK/4), k = 4 (f % (GBK/4)));
+  // k-major sources stage f -> (k = f / 16, r = 4 (f % 16)).
+  constexpr int KQ = GBK / 4;
   auto gload = [&](int64_t k0) {
-    if (!TA) {  // A[m][k] at A[m*lda + k]
-      const int64_t m = m0 + (t >> 2), k = k0 + (t & 3) * 4;
-      ra = (m < M) ? load4(A + m * lda + k, k, ke, vec_a) : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {    // A[m][k] at A[k*lda + m]
-      const int64_t k = k0 + (t >> 4), m = m0 + (t & 15) * 4;
-      ra = (k < ke) ? load4(A + k * lda + m, m, M, vec_a) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    if (!TB) {  // B[k][n] at B[k*ldb + n]
-      const int64_t k = k0 + (t >> 4), n = n0 + (t & 15) * 4;
-      rb = (k < ke) ? load4(B + k * ldb + n, n, N, vec_b) : make_float4(0.f, 0.f, 0.f, 0.f);
-    } else {    // B[k][n] at B[n*ldb + k]
-      const int64_t n = n0 + (t >> 2), k = k0 + (t & 3) * 4;
-      rb = (n < N) ? load4(B + n * ldb + k, k, ke, vec_b) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int i = 0; i < GLD4; ++i) {
+      const int f = t + 256 * i;
+      if (!TA) {
+        const int64_t m = m0 + f / KQ, k = k0 + (f % KQ) * 4;
+        ra[i] = (m < M) ? load4(A + m * lda + k, k, ke, vec_a) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const int64_t k = k0 + (f >> 4), m = m0 + (f & 15) * 4;
+        ra[i] = (k < ke) ? load4(A + k * lda + m, m, M, vec_a) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if (!TB) {
+        const int64_t k = k0 + (f >> 4), n = n0 + (f & 15) * 4;
+        rb[i] = (k < ke) ? load4(B + k * ldb + n, n, N, vec_b) : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        const int64_t n = n0 + f / KQ, k = k0 + (f % KQ) * 4;
+        rb[i] = (n < N) ? load4(B + n * ldb + k, k, ke, vec_b) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
     }
   };
   auto lstore = [&]() {
-    if (!TA) {
-      const int m = t >> 2, k = (t & 3) * 4;
-      sA[(k + 0) * GLDA + m] = ra.x; sA[(k + 1) * GLDA + m] = ra.y;
-      sA[(k + 2) * GLDA + m] = ra.z; sA[(k + 3) * GLDA + m] = ra.w;
-    } else {
-      const int k = t >> 4, m = (t & 15) * 4;
-      *reinterpret_cast<float4*>(&sA[k * GLDA + m]) = ra;
-    }
-    if (!TB) {
-      const int k = t >> 4, n = (t & 15) * 4;
-      *reinterpret_cast<float4*>(&sB[k * GLDB + n]) = rb;
-    } else {
-      const int n = t >> 2, k = (t & 3) * 4;
-      sB[(k + 0) * GLDB + n] = rb.x; sB[(k + 1) * GLDB + n] = rb.y;
-      sB[(k + 2) * GLDB + n] = rb.z; sB[(k + 3) * GLDB + n] = rb.w;
+#pragma unroll
+    for (int i = 0; i < GLD4; ++i) {
+      const int f = t + 256 * i;
+      if (!TA) {
+        float* d = &sA[(f / KQ) * GSR + (f % KQ) * 4];
+        *reinterpret_cast<float2*>(d) = make_float2(ra[i].x, ra[i].y);
+        *reinterpret_cast<float2*>(d + 2) = make_float2(ra[i].z, ra[i].w);
+      } else {
+        *reinterpret_cast<float4*>(&sA[(f >> 4) * GSK + (f & 15) * 4]) = ra[i];
+      }
+      if (!TB) {
+        *reinterpret_cast<float4*>(&sB[(f >> 4) * GSK + (f & 15) * 4]) = rb[i];
+      } else {
+        float* d = &sB[(f / KQ) * GSR + (f % KQ) * 4];
+        *reinterpret_cast<float2*>(d) = make_float2(rb[i].x, rb[i].y);
+        *reinterpret_cast<float2*>(d + 2) = make_float2(rb[i].z, rb[i].w);
+      }
     }
   };
+  // op(A)[m][k] / op(B)[k][n] as staged
+  auto a_at = [&](int m, int k) -> float { return TA ? sA[k * GSK + m] : sA[m * GSR + k]; };
+  auto b_at = [&](int k, int n) -> float { return TB ? sB[n * GSR + k] : sB[k * GSK + n]; };
 
   if (kb < ke) {
     gload(kb);
@@ -144,16 +162,16 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
       if (more) gload(k0 + GBK);
       if (do_rowsum && t < GBM) {
 #pragma unroll
-        for (int k = 0; k < GBK; ++k) rowsum += sA[k * GLDA + t];
+        for (int k = 0; k < GBK; ++k) rowsum += a_at(t, k);
       }
 #pragma unroll
       for (int kk = 0; kk < GBK / 4; ++kk) {
         const int kr = 4 * kk + (lane >> 4);
         float af[2], bfr[2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = sA[kr * GLDA + wm + i * 16 + (lane & 15)];
+        for (int i = 0; i < 2; ++i) af[i] = a_at(wm + i * 16 + (lane & 15), kr);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) bfr[j] = sB[kr * GLDB + wn + j * 16 + (lane & 15)];
+        for (int j = 0; j < 2; ++j) bfr[j] = b_at(kr, wn + j * 16 + (lane & 15));
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll

@@ -99,6 +99,7 @@ SIGNATURES = {
     "hvae_adam_dense": (cint, [P(Adam), vp, vp, vp, vp, i64, vp]),
     "hvae_adam_rows": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp]),
     "hvae_counter_add": (cint, [vp, i64, vp]),
+    "hvae_counters_add": (cint, [vp, i64, vp, i64, vp]),
     "hvae_score_candidates": (cint, [vp, i64, vp, vp, i64, vp, i64, i64, vp, vp]),
     "hvae_rank_first": (cint, [vp, i64, i64, vp, vp]),
     "hvae_topk": (cint, [vp, i64, i64, i64, P(CsrBatch), i64, vp, vp, vp]),

@@ -328,16 +328,21 @@ class FusedTrainer:
                         data.n_items)
 
     def _launch(self, bf: _StepBuffers, csr: CsrBatch, train: bool, beta: float, p_drop: float,
-                ext: dict | None = None):
-        """Enqueue one full step on the current stream (captured into a graph by the caller)."""
+                ext: dict | None = None, advance: int = 0):
+        """Enqueue one full step on the current stream (captured into a graph by the caller).
+
+        advance > 0 also moves the device batch offset (rows_offset) by that many users.
+        """
         self._launch_fwd_bwd(bf, csr, train, beta, p_drop, ext)
         if train:
             if self.dp is None:
-                self._launch_update(bf.rg, bf)
+                self._launch_update(bf.rg, bf, advance)
             else:
                 self.dp.all_reduce_dense(self.g_small)
                 merged = self.dp.merged_rows(bf.rg.n_unique, bf.rg.item_of, bf.rg.rows)
-                self._launch_update(merged, bf)
+                self._launch_update(merged, bf, advance)
+        elif advance:
+            self._advance(advance)
 
     def _launch_fwd_bwd(self, bf: _StepBuffers, csr: CsrBatch, train: bool, beta: float, p_drop: float,
                         ext: dict | None = None):
@@ -428,7 +433,7 @@ class FusedTrainer:
         check(L_.hvae_w1_rowgrad(csr_ref, ptr(bf.da[0]), H[0], bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st),
               "w1_rowgrad")
 
-    def _launch_update(self, rg, bf: _StepBuffers):
+    def _launch_update(self, rg, bf: _StepBuffers, advance: int = 0):
         """clip_grad_norm_(5.0) + Adam over the flat state, then step += 1."""
         L_, lay = lib(), self.layout
         st = torch.cuda.current_stream(self.device).cuda_stream
@@ -444,7 +449,7 @@ class FusedTrainer:
         self._probe_end("adam_rows")
         check(L_.hvae_adam_dense(C.byref(cfg), ptr(self.small), ptr(self.m_small), ptr(self.v_small),
                                  ptr(self.g_small), lay.n_small, st), "adam_dense")
-        check(L_.hvae_counter_add(step, 1, st), "counter_add")
+        check(L_.hvae_counters_add(step, 1, ptr(self.boff) if advance else None, advance, st), "counters_add")
 
     # ----------------------------------------------- live kernel timing ---
     probe: dict | None = None  # {"kernel": name, "events": [(start, end), ...]} (eager steps only)
@@ -511,23 +516,20 @@ class FusedTrainer:
                 if bf.graph is None or bf.graph_key != (id(data), beta, p_drop):
                     if bi == 0 and bf.graph is None:
                         # first use: run eagerly (loads kernels, sets attributes), capture afterwards
-                        self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop)
-                        self._advance(B)
+                        self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
                         if train:
                             self.host_step += 1
                         continue
                     self._capture(bf, data, train, beta, p_drop)
                 bf.graph.replay()
             else:
-                self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop)
-                self._advance(B)
+                self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
             if train:
                 self.host_step += 1
         if tail:
             beta = beta_fn(n_full)
             bf = self._buffers(tail, data.max_batch_nnz(tail), train)
-            self._launch(bf, self._csr(data, tail, data.perm, self.boff), train, beta, p_drop)
-            self._advance(tail)
+            self._launch(bf, self._csr(data, tail, data.perm, self.boff), train, beta, p_drop, advance=tail)
             if train:
                 self.host_step += 1
         sums = accum.cpu().tolist()  # the one host sync of the epoch
@@ -539,8 +541,7 @@ class FusedTrainer:
         bf.csr_keepalive = csr
         torch.cuda.synchronize(self.device)
         with torch.cuda.graph(g):
-            self._launch(bf, csr, train, beta, p_drop)
-            self._advance(bf.B)
+            self._launch(bf, csr, train, beta, p_drop, advance=bf.B)
         bf.graph = g
         bf.graph_key = (id(data), beta, p_drop)
 
