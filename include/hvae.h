@@ -127,6 +127,13 @@ typedef struct hvae_rowgrad {
 int hvae_w1_rowgrad(const hvae_csr_batch* x, const float* da, int64_t H, const hvae_rowgrad* rg,
                     void* ws, size_t ws_bytes, void* stream);
 size_t hvae_w1_rowgrad_workspace(int64_t n_items);
+/* hvae_w1_rowgrad in two halves. _plan depends on the batch only (per-item
+ * counts, slots, segments, and each segment's contributions sorted by batch
+ * row), so a train step can run it on a side stream while the forward runs;
+ * _apply then gathers x * da into the rows. plan + apply == hvae_w1_rowgrad. */
+int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad* rg, void* ws, size_t ws_bytes,
+                         void* stream);
+int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowgrad* rg, void* stream);
 /* Scatter the row-sparse gradient into a dense, caller-zeroed buffer laid out
  * [N, ld] (item-major; ld >= H). */
 int hvae_rowgrad_to_dense(const hvae_rowgrad* rg, int64_t H, float* dense, int64_t ld, void* stream);
@@ -204,6 +211,13 @@ size_t hvae_decoder_workspace(int dtype, int64_t nb, int64_t N, int64_t D);
 int hvae_decoder_supported(int dtype, int64_t D);
 /* *out = max_i ||E_i||_2 of an fp32 / bf16 [N, D] matrix (computed once: E is frozen). */
 int hvae_row_norm_max(int dtype, const void* E, int64_t N, int64_t D, float* out, void* stream);
+/* The train-step form: the streaming sweep above plus, in the same finalize
+ * launch (one block per user, after the split merge), the sparse half of the
+ * loss and of d(u) against the fp32 E32 (see hvae_decoder_bwd). nb = x->nb,
+ * N = x->n_items. O may be NULL (kept internal); dU NULL => loss only. */
+int hvae_decoder_train(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
+                       const float* E32, const hvae_csr_batch* x, int64_t D, float grad_scale, float* lse,
+                       float* O, float* recon_rows, float* dU, void* ws, size_t ws_bytes, void* stream);
 /* Sparse half of the loss and of d(u), in fp32 against the fp32 E:
  *   recon_rows[b] = n_b * lse[b] - sum_{j in row b} x_bj (u_b . E_j),  n_b = sum_j x_bj
  *   dU[b,:]       = grad_scale * (n_b * O[b,:] - sum_{j in row b} x_bj E_j)
@@ -236,6 +250,14 @@ int hvae_clip_grad_norm(const float* g_dense, int64_t n_dense, const hvae_rowgra
                         float max_norm, float* norm_out, float* coef_out, void* ws,
                         size_t ws_bytes, void* stream);
 size_t hvae_clip_grad_norm_workspace(int64_t n_dense, int64_t cap, int64_t H);
+/* The same launch, also advancing the step counters once the norm is known:
+ * *step_snap = *step_dev; *step_dev += 1; *boff += advance (boff may be NULL
+ * when advance == 0). Give the Adam launches that follow step_dev = step_snap.
+ * Saves the separate counter launch at the end of every train step. */
+int hvae_clip_grad_norm_step(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg, int64_t H,
+                             float max_norm, float* norm_out, float* coef_out, int64_t* step_dev,
+                             int64_t* step_snap, int64_t* boff, int64_t advance, void* ws, size_t ws_bytes,
+                             void* stream);
 
 /* torch.optim.Adam (src/ml/train.py:63, 92; single-tensor semantics):
  *   g = coef * grad (+ wd * p); m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2

@@ -3,11 +3,30 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
+
 #include "hvae_common.h"
 
 namespace hvae {
 
 static thread_local char g_last_error[1024] = "";
+
+__device__ unsigned g_tickets[kTicketPool];
+
+unsigned* ticket_slice() {
+  static unsigned* pools[64] = {};  // per device: the symbol has one instance per device
+  static std::atomic<uint64_t> next{0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("ticket_slice: no current device");
+    return nullptr;
+  }
+  if (!pools[dev] && hipGetSymbolAddress((void**)&pools[dev], HIP_SYMBOL(g_tickets)) != hipSuccess) {
+    set_error("ticket_slice: hipGetSymbolAddress failed");
+    return nullptr;
+  }
+  return pools[dev] + (next.fetch_add(1) % (kTicketPool / kTicketSlice)) * kTicketSlice;
+}
 
 void set_error(const char* fmt, ...) {
   va_list ap;

@@ -49,6 +49,33 @@ void set_error(const char* fmt, ...);
   } while (0)
 
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// Arrival tickets for "last block finishes the reduction" kernels (one launch
+// instead of partials + a second reduce launch). The pool is a device global of
+// hvae_abi.hip (zero at code-object load); the last arriving block resets its
+// ticket, so tickets are zero between launches. Each launch takes a slice of
+// kTicketSlice tickets in rotation, so launches that may run concurrently on
+// different streams (the nodes of one captured graph) never share one.
+constexpr int kTicketPool = 1 << 16, kTicketSlice = 256;
+unsigned* ticket_slice();  // nullptr (error set) on failure
+
+// Called by every thread of a block after it wrote its partials: true in the
+// one block that arrives last at ticket *t (and then everything the other
+// blocks wrote before arriving is visible to it).
+__device__ __forceinline__ bool last_block_arrives(unsigned* t, unsigned n_blocks) {
+  __shared__ unsigned s_last;
+  __threadfence();  // release (L2 writeback: blocks of other XCDs read it)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = atomicAdd(t, 1u);
+    s_last = (old == n_blocks - 1);
+    if (s_last) *t = 0u;  // nobody else touches it again in this launch
+  }
+  __syncthreads();
+  const bool last = s_last;
+  if (last) __threadfence();  // acquire
+  return last;
+}
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // --------------------------------------------------------------- device ----

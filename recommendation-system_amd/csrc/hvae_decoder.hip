@@ -424,61 +424,132 @@ __global__ void __launch_bounds__(256) k_dec_f32(const float* __restrict__ U, in
 // weights exp(m_s - M) live in LDS, threads run over D (coalesced rows).
 constexpr int kMaxSplits = 4096;
 
-__device__ void exact_user(int64_t b, const float* __restrict__ U, int64_t ldu, const bf16_t* __restrict__ E,
-                           int64_t N, int64_t D, float* __restrict__ lse, float* __restrict__ O, float* red,
-                           float* pbuf);
+__device__ float exact_user(int64_t b, const float* __restrict__ U, int64_t ldu, const bf16_t* __restrict__ E,
+                            int64_t N, int64_t D, float (&o)[4], float* red, float* pbuf);
 
-__global__ void __launch_bounds__(256) k_dec_merge(const float* __restrict__ pm, const float* __restrict__ pl,
-                                                   const float* __restrict__ pO, const int* __restrict__ pflag,
-                                                   int splits, int64_t nb, int64_t D, float* __restrict__ lse,
-                                                   float* __restrict__ O, const float* __restrict__ U, int64_t ldu,
-                                                   const bf16_t* __restrict__ E, int64_t N) {
+// Per-user finalisation of the streaming decoder, one 256-thread block per user:
+//   1. combine the per-split (m, l, O) partials (or take the single-split result),
+//   2. recompute exactly if a split flagged the user (bf16 fixed-offset underflow),
+//   3. if a CSR batch is given, the sparse half of the loss and of d(u):
+//        recon_rows[b] = n_b lse_b - u_b . (sum_j x_bj E_j)
+//        dU[b]         = scale (n_b O_b - sum_j x_bj E_j)          (fp32 E)
+// Thread t owns d = t + 256 k (D <= 1024) throughout, so O never round-trips
+// through memory between the steps.
+struct FinArgs {
+  const float* pm; const float* pl; const float* pO;  // partial mode (splits > 1)
+  const int* flag;                                    // [splits][nb] / [nb] or NULL
+  int splits;
+  const float* lse_in; const float* O_in;             // direct mode (splits == 1)
+  const float* U; int64_t ldu; const bf16_t* Ebf;     // exact fixup inputs (bf16 path)
+  const float* E32; int64_t N; int64_t D; int64_t nb;
+  const int64_t* row_ptr; const int32_t* col_idx; const float* vals;
+  const int32_t* rows; const int64_t* rows_offset;    // CSR batch (nullable row_ptr => no sparse terms)
+  float scale;
+  float* lse_out; float* O_out; float* recon_rows; float* dU;
+};
+
+__global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   __shared__ float wsh[kMaxSplits];
   __shared__ float red[4];
   __shared__ float pbuf[256];
   __shared__ int any_flag;
   const int64_t b = blockIdx.x;
-  if (threadIdx.x == 0) any_flag = 0;
-  float M = -INFINITY;
-  int fl = 0;
-  for (int s = threadIdx.x; s < splits; s += 256) {
-    M = fmaxf(M, pm[(int64_t)s * nb + b]);
-    if (pflag) fl |= pflag[(int64_t)s * nb + b];
-  }
-  M = wave_max(M);
+  const int tid = threadIdx.x;
+  const int64_t D = a.D;
+  if (tid == 0) any_flag = 0;
   __syncthreads();
-  if (fl) any_flag = 1;
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = M;
-  __syncthreads();
-  if (any_flag) {  // rare: exact two-pass recompute of this user (uniform branch)
-    exact_user(b, U, ldu, E, N, D, lse, O, red, pbuf);
-    return;
+  float lse_b;
+  float o[4] = {0.f, 0.f, 0.f, 0.f};
+  if (a.splits > 1) {
+    float M = -INFINITY;
+    int fl = 0;
+    for (int s = tid; s < a.splits; s += 256) {
+      M = fmaxf(M, a.pm[(int64_t)s * a.nb + b]);
+      if (a.flag) fl |= a.flag[(int64_t)s * a.nb + b];
+    }
+    if (fl) any_flag = 1;
+    M = wave_max(M);
+    if ((tid & 63) == 0) red[tid >> 6] = M;
+    __syncthreads();
+    M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    float L = 0.f;
+    for (int s = tid; s < a.splits; s += 256) {
+      const float ms = a.pm[(int64_t)s * a.nb + b];
+      const float wv = (ms == -INFINITY) ? 0.f : __expf(ms - M);
+      wsh[s] = wv;
+      L += wv * a.pl[(int64_t)s * a.nb + b];
+    }
+    L = block_sum<256>(L, red);  // its barriers also publish wsh and any_flag
+    lse_b = M + logf(L);
+    const float inv = 1.0f / L;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t d = tid + 256 * k;
+      if (d >= D || !a.pO) continue;
+      float acc = 0.f;
+      for (int s = 0; s < a.splits; ++s) acc += wsh[s] * a.pO[((int64_t)s * a.nb + b) * D + d];
+      o[k] = acc * inv;
+    }
+  } else {
+    if (a.flag && a.flag[b]) any_flag = 1;
+    lse_b = a.lse_in[b];
+    if (a.O_in) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t d = tid + 256 * k;
+        if (d < D) o[k] = a.O_in[b * D + d];
+      }
+    }
+    __syncthreads();
   }
-  M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-  float L = 0.f;
-  for (int s = threadIdx.x; s < splits; s += 256) {
-    const float ms = pm[(int64_t)s * nb + b];
-    const float wv = (ms == -INFINITY) ? 0.f : __expf(ms - M);
-    wsh[s] = wv;
-    L += wv * pl[(int64_t)s * nb + b];
+  if (any_flag) lse_b = exact_user(b, a.U, a.ldu, a.Ebf, a.N, D, o, red, pbuf);  // rare, block-uniform
+  if (tid == 0) a.lse_out[b] = lse_b;
+  if (a.O_out) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t d = tid + 256 * k;
+      if (d < D) a.O_out[b * D + d] = o[k];
+    }
   }
-  L = block_sum<256>(L, red);  // (its barriers also publish wsh)
-  if (threadIdx.x == 0) lse[b] = M + logf(L);
-  if (!O) return;
-  const float inv = 1.0f / L;
-  for (int64_t d = threadIdx.x; d < D; d += 256) {
-    float acc = 0.f;
-    for (int s = 0; s < splits; ++s) acc += wsh[s] * pO[((int64_t)s * nb + b) * D + d];
-    O[b * D + d] = acc * inv;
+  if (!a.row_ptr) return;
+  // ---- sparse terms against the fp32 E
+  const int64_t r = batch_row(a.rows, a.rows_offset, b);
+  const int64_t beg = a.row_ptr[r], end = a.row_ptr[r + 1];
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float n = 0.f;
+  for (int64_t e = beg; e < end; ++e) {
+    const int64_t j = a.col_idx[e];
+    const float x = a.vals[e];
+    n += x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t d = tid + 256 * k;
+      if (d < D) acc[k] += x * a.E32[j * D + d];
+    }
+  }
+  float dot = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t d = tid + 256 * k;
+    if (d < D) dot += a.U[b * a.ldu + d] * acc[k];
+  }
+  dot = block_sum<256>(dot, red);
+  if (a.recon_rows && tid == 0) a.recon_rows[b] = n * lse_b - dot;
+  if (a.dU) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t d = tid + 256 * k;
+      if (d < D) a.dU[b * D + d] = a.scale * (n * o[k] - acc[k]);
+    }
   }
 }
 
 // Exact recompute of one user flagged by k_dec_bf16 (its max score sits more
 // than kUnderflowSpan below the fixed offset: only possible for |u| in the
 // hundreds). Two passes in fp32 over the bf16 E by one 256-thread block.
-__device__ void exact_user(int64_t b, const float* __restrict__ U, int64_t ldu, const bf16_t* __restrict__ E,
-                           int64_t N, int64_t D, float* __restrict__ lse, float* __restrict__ O, float* red,
-                           float* pbuf) {
+// Returns lse; o[k] = O[b, threadIdx.x + 256 k].
+__device__ float exact_user(int64_t b, const float* __restrict__ U, int64_t ldu, const bf16_t* __restrict__ E,
+                            int64_t N, int64_t D, float (&o)[4], float* red, float* pbuf) {
   const float* u = U + b * ldu;
   auto score = [&](int64_t i) {
     float s = 0.f;
@@ -511,24 +582,9 @@ __device__ void exact_user(int64_t b, const float* __restrict__ U, int64_t ldu, 
     __syncthreads();
   }
   l = block_sum<256>(l, red);
-  if (threadIdx.x == 0) lse[b] = mx + logf(l);
-  if (O) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t d = threadIdx.x + 256 * k;
-      if (d < D) O[b * D + d] = oacc[k] / l;
-    }
-  }
-}
-
-// Direct (single-split) mode: one block per user, flagged users only do work.
-__global__ void __launch_bounds__(256) k_dec_fixup(const int* __restrict__ flag, const float* __restrict__ U,
-                                                   int64_t ldu, const bf16_t* __restrict__ E, int64_t N,
-                                                   int64_t D, float* __restrict__ lse, float* __restrict__ O) {
-  __shared__ float red[4];
-  __shared__ float pbuf[256];
-  if (!flag[blockIdx.x]) return;
-  exact_user(blockIdx.x, U, ldu, E, N, D, lse, O, red, pbuf);
+  for (int k = 0; k < 4; ++k) o[k] = oacc[k] / l;
+  return mx + logf(l);
 }
 
 // max_i ||E_i||_2 over an fp32 or bf16 [N, D] matrix (score bound of the bf16 path).
@@ -545,70 +601,6 @@ __global__ void __launch_bounds__(256) k_row_norm_max(int dtype, const void* __r
     best = fmaxf(best, sqrtf(wave_sum(s)));
   }
   if (lane == 0) atomicMax(out_bits, __float_as_uint(best));  // non-negative floats order as uints
-}
-
-// Sparse half of the loss / gradient against the fp32 E (one wave per row):
-//   recon_rows[b] = n_b lse_b - sum_j x_bj (u_b . E_j)
-//   dU[b]         = scale (n_b O_b - sum_j x_bj E_j)
-template <int NV>
-__global__ void __launch_bounds__(256) k_dec_sparse(const int64_t* __restrict__ row_ptr,
-                                                    const int32_t* __restrict__ col_idx,
-                                                    const float* __restrict__ vals,
-                                                    const int32_t* __restrict__ rows,
-    const int64_t* __restrict__ rows_offset, int64_t nb,
-                                                    const float* __restrict__ U, int64_t ldu,
-                                                    const float* __restrict__ E, int64_t D,
-                                                    const float* __restrict__ lse,
-                                                    const float* __restrict__ O, float scale,
-                                                    float* __restrict__ recon_rows,
-                                                    float* __restrict__ dU) {
-  const int lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= nb) return;
-  const int64_t r = batch_row(rows, rows_offset, b);
-  const int64_t beg = row_ptr[r], end = row_ptr[r + 1];
-  float4 u[NV], acc[NV];
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int64_t e = 4 * (int64_t)(lane + 64 * k);
-    u[k] = (e < D) ? *reinterpret_cast<const float4*>(U + b * ldu + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-    acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  float n = 0.f;
-  for (int64_t base = beg; base < end; base += 64) {
-    const int64_t cnt = min((int64_t)64, end - base);
-    const int my_j = (lane < cnt) ? col_idx[base + lane] : 0;
-    const float my_x = (lane < cnt) ? vals[base + lane] : 0.f;
-    n += my_x;
-    for (int t = 0; t < cnt; ++t) {
-      const int j = __builtin_amdgcn_readlane(my_j, t);
-      const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), t));
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const int64_t e = 4 * (int64_t)(lane + 64 * k);
-        if (e >= D) continue;
-        const float4 ev = *reinterpret_cast<const float4*>(E + (int64_t)j * D + e);
-        acc[k].x += x * ev.x; acc[k].y += x * ev.y; acc[k].z += x * ev.z; acc[k].w += x * ev.w;
-      }
-    }
-  }
-  n = wave_sum(n);
-  float dot = 0.f;
-#pragma unroll
-  for (int k = 0; k < NV; ++k)
-    dot += (u[k].x * acc[k].x + u[k].y * acc[k].y) + (u[k].z * acc[k].z + u[k].w * acc[k].w);
-  dot = wave_sum(dot);
-  if (lane == 0) recon_rows[b] = n * lse[b] - dot;
-  if (!dU) return;
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int64_t e = 4 * (int64_t)(lane + 64 * k);
-    if (e >= D) continue;
-    const float4 ov = *reinterpret_cast<const float4*>(O + b * D + e);
-    *reinterpret_cast<float4*>(dU + b * D + e) =
-        make_float4(scale * (n * ov.x - acc[k].x), scale * (n * ov.y - acc[k].y),
-                    scale * (n * ov.z - acc[k].z), scale * (n * ov.w - acc[k].w));
-  }
 }
 
 // ------------------------------------------------------------- planning ---
@@ -642,9 +634,13 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   return p;
 }
 
+// workspace: flags [splits * nb] | partials (m, l, O) [splits * nb * (D + 2)] (splits > 1) | O scratch [nb * D]
+static size_t dec_flag_bytes(int splits, int64_t nb) {
+  return (size_t)cdiv((int64_t)splits * nb * sizeof(int), 256) * 256;
+}
 static size_t dec_ws_bytes(int splits, int64_t nb, int64_t D) {
-  const size_t flags = (size_t)cdiv((int64_t)splits * nb * sizeof(int), 256) * 256;
-  return flags + (splits > 1 ? (size_t)splits * nb * (D + 2) * sizeof(float) : 0);
+  return dec_flag_bytes(splits, nb) + (splits > 1 ? (size_t)splits * nb * (D + 2) * sizeof(float) : 0) +
+         (size_t)nb * D * sizeof(float);
 }
 
 template <int D, bool WO>
@@ -728,81 +724,112 @@ extern "C" size_t hvae_decoder_workspace(int dtype, int64_t nb, int64_t N, int64
   return dec_ws_bytes(p.splits, nb, D);
 }
 
-extern "C" int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
-                                int64_t nb, int64_t N, int64_t D, float* lse, float* O, void* ws,
-                                size_t ws_bytes, void* stream) {
-  HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32, "hvae_decoder_fwd: bad dtype");
-  HVAE_REQUIRE(U && E && lse && N > 0 && D > 0 && ldu >= D, "hvae_decoder_fwd: bad args");
-  HVAE_REQUIRE(dtype != HVAE_BF16 || e_maxnorm, "hvae_decoder_fwd: bf16 needs e_maxnorm");
+// flash sweep + finalize; csr / recon_rows / dU optional
+static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
+                       const float* E32, const hvae_csr_batch* x, int64_t nb, int64_t N, int64_t D, float scale,
+                       float* lse, float* O, float* recon_rows, float* dU, void* ws, size_t ws_bytes,
+                       hipStream_t st) {
+  HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32, "hvae decoder: bad dtype");
+  HVAE_REQUIRE(U && E && lse && N > 0 && D > 0 && ldu >= D, "hvae decoder: bad args");
+  HVAE_REQUIRE(dtype != HVAE_BF16 || e_maxnorm, "hvae decoder: bf16 needs e_maxnorm");
+  HVAE_REQUIRE(D <= 1024, "hvae decoder: D > 1024 unsupported");
   HVAE_REQUIRE(ldu % 4 == 0 && ((uintptr_t)U % 16) == 0 && ((uintptr_t)E % 16) == 0 &&
                    (!O || ((uintptr_t)O % 16) == 0),
-               "hvae_decoder_fwd: U/E/O must be 16-B aligned with ldu %% 4 == 0");
-  HVAE_REQUIRE(N < (1ll << 31), "hvae_decoder_fwd: N too large");
+               "hvae decoder: U/E/O must be 16-B aligned with ldu %% 4 == 0");
+  HVAE_REQUIRE(N < (1ll << 31), "hvae decoder: N too large");
+  HVAE_REQUIRE(!x || (E32 && x->row_ptr && x->nb == nb && x->n_items == N), "hvae decoder: bad CSR batch");
   if (nb == 0) return HVAE_OK;
-  hipStream_t st = as_stream(stream);
   DecPlan p = dec_plan(dtype, nb, N, D);
   if (!ws || ws_bytes < dec_ws_bytes(1, nb, D))
-    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_decoder_fwd: workspace %zu < %zu", ws_bytes, dec_ws_bytes(1, nb, D));
-  if (p.splits > 1 && ws_bytes < dec_ws_bytes(p.splits, nb, D)) {
-    // fall back to fewer splits that fit the given workspace
-    int64_t fit = (int64_t)(ws_bytes / ((size_t)nb * ((D + 2) * sizeof(float) + sizeof(int)))) - 1;
+    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae decoder: workspace %zu < %zu", ws_bytes, dec_ws_bytes(1, nb, D));
+  if (p.splits > 1 && ws_bytes < dec_ws_bytes(p.splits, nb, D)) {  // fewer splits that fit
+    int64_t fit = p.splits;
+    while (fit > 1 && ws_bytes < dec_ws_bytes((int)fit, nb, D)) fit = fit * 3 / 4;
     const int64_t tiles = cdiv(N, dtype == HVAE_BF16 ? kBfTI : kF32TI);
-    if (fit < 2) fit = 1;
-    fit = std::min<int64_t>(fit, kMaxSplits);
     p.tiles_per_split = cdiv(tiles, fit);
     p.splits = (int)cdiv(tiles, p.tiles_per_split);
     p.blocks = cdiv(nb, dtype == HVAE_BF16 ? kBfUsersPerBlock : kF32UsersPerBlock) * p.splits;
   }
-  const size_t flag_bytes = (size_t)cdiv((int64_t)p.splits * nb * sizeof(int), 256) * 256;
+  const bool bf = dtype == HVAE_BF16;
+  const bool want_o = O || dU;
+  char* w = (char*)ws;
   DecOut o{};
-  o.flag = (int*)ws;
+  o.flag = (int*)w;
+  w += dec_flag_bytes(p.splits, nb);
+  float* o_scratch = nullptr;
   if (p.splits == 1) {
     o.direct = 1;
     o.lse = lse;
-    o.O = O;
+    o.O = O ? O : (want_o ? (float*)w : nullptr);
+    o_scratch = o.O;
   } else {
-    float* base = (float*)((char*)ws + flag_bytes);
+    float* base = (float*)w;
     o.direct = 0;
     o.m = base;
     o.l = base + (size_t)p.splits * nb;
     o.O = base + (size_t)2 * p.splits * nb;
   }
-  int rc = O ? dispatch<true>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st)
-             : dispatch<false>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st);
+  int rc = want_o ? dispatch<true>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st)
+                  : dispatch<false>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st);
   if (rc) return rc;
-  const bool bf = dtype == HVAE_BF16;
-  HVAE_REQUIRE(!bf || D <= 1024, "hvae_decoder_fwd: D too large for the exact fixup");
-  if (p.splits > 1) {
-    k_dec_merge<<<(unsigned)nb, 256, 0, st>>>(o.m, o.l, o.O, bf ? o.flag : nullptr, p.splits, nb, D, lse, O, U,
-                                             ldu, (const bf16_t*)E, N);
-    HVAE_LAUNCH_CHECK("k_dec_merge");
-  } else if (bf) {
-    k_dec_fixup<<<(unsigned)nb, 256, 0, st>>>(o.flag, U, ldu, (const bf16_t*)E, N, D, lse, O);
-    HVAE_LAUNCH_CHECK("k_dec_fixup");
+  if (p.splits == 1 && !bf && !x) return HVAE_OK;  // fp32 single split: the sweep wrote lse / O already
+  FinArgs a{};
+  a.splits = p.splits;
+  if (p.splits > 1) { a.pm = o.m; a.pl = o.l; a.pO = want_o ? o.O : nullptr; }
+  else { a.lse_in = lse; a.O_in = o_scratch; }
+  a.flag = bf ? o.flag : nullptr;
+  a.U = U; a.ldu = ldu; a.Ebf = (const bf16_t*)E;
+  a.E32 = E32; a.N = N; a.D = D; a.nb = nb;
+  if (x) {
+    a.row_ptr = x->row_ptr; a.col_idx = x->col_idx; a.vals = x->vals; a.rows = x->rows;
+    a.rows_offset = x->rows_offset;
   }
+  a.scale = scale;
+  a.lse_out = lse;
+  a.O_out = O ? O : (p.splits == 1 ? o_scratch : nullptr);
+  a.recon_rows = recon_rows;
+  a.dU = dU;
+  k_dec_finalize<<<(unsigned)nb, 256, 0, st>>>(a);
+  HVAE_LAUNCH_CHECK("k_dec_finalize");
   return HVAE_OK;
+}
+
+extern "C" int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
+                                int64_t nb, int64_t N, int64_t D, float* lse, float* O, void* ws,
+                                size_t ws_bytes, void* stream) {
+  return decoder_run(dtype, U, ldu, E, e_maxnorm, nullptr, nullptr, nb, N, D, 0.f, lse, O, nullptr, nullptr, ws,
+                     ws_bytes, as_stream(stream));
+}
+
+extern "C" int hvae_decoder_train(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
+                                  const float* E32, const hvae_csr_batch* x, int64_t D, float grad_scale,
+                                  float* lse, float* O, float* recon_rows, float* dU, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  HVAE_REQUIRE(x && recon_rows, "hvae_decoder_train: needs the CSR batch and recon_rows");
+  return decoder_run(dtype, U, ldu, E, e_maxnorm, E32, x, x->nb, x->n_items, D, grad_scale, lse, O, recon_rows, dU,
+                     ws, ws_bytes, as_stream(stream));
 }
 
 extern "C" int hvae_decoder_bwd(const hvae_csr_batch* x, const float* U, int64_t ldu, const float* E32,
                                 int64_t D, const float* lse, const float* O, float grad_scale,
                                 float* recon_rows, float* dU, void* stream) {
-  HVAE_REQUIRE(x && x->row_ptr && U && E32 && lse && recon_rows && D > 0 && ldu >= D,
+  HVAE_REQUIRE(x && x->row_ptr && U && E32 && lse && recon_rows && D > 0 && D <= 1024 && ldu >= D,
                "hvae_decoder_bwd: bad args");
   HVAE_REQUIRE(!dU || O, "hvae_decoder_bwd: dU needs O");
-  HVAE_REQUIRE(D % 4 == 0 && ldu % 4 == 0, "hvae_decoder_bwd: D and ldu must be multiples of 4");
   if (x->nb == 0) return HVAE_OK;
-  const unsigned grid = (unsigned)cdiv(x->nb, 4);
-  hipStream_t st = as_stream(stream);
-  const int64_t nv = cdiv(D, 256);
-#define HVAE_DS(NV_)                                                                               \
-  k_dec_sparse<NV_><<<grid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->vals, x->rows, x->rows_offset, x->nb, U, ldu, \
-                                          E32, D, lse, O, grad_scale, recon_rows, dU)
-  if (nv <= 1) HVAE_DS(1);
-  else if (nv <= 2) HVAE_DS(2);
-  else if (nv <= 3) HVAE_DS(3);
-  else if (nv <= 4) HVAE_DS(4);
-  else HVAE_FAIL(HVAE_ERR_UNSUPPORTED, "hvae_decoder_bwd: D=%lld > 1024", (long long)D);
-#undef HVAE_DS
-  HVAE_LAUNCH_CHECK("k_dec_sparse");
+  FinArgs a{};
+  a.splits = 1;
+  a.lse_in = lse;
+  a.O_in = O;
+  a.U = U; a.ldu = ldu;
+  a.E32 = E32; a.N = x->n_items; a.D = D; a.nb = x->nb;
+  a.row_ptr = x->row_ptr; a.col_idx = x->col_idx; a.vals = x->vals; a.rows = x->rows;
+  a.rows_offset = x->rows_offset;
+  a.scale = grad_scale;
+  a.lse_out = const_cast<float*>(lse);  // rewritten with the same value
+  a.recon_rows = recon_rows;
+  a.dU = dU;
+  k_dec_finalize<<<(unsigned)x->nb, 256, 0, as_stream(stream)>>>(a);
+  HVAE_LAUNCH_CHECK("k_dec_finalize");
   return HVAE_OK;
 }

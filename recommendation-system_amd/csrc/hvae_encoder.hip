@@ -158,17 +158,20 @@ __global__ void __launch_bounds__(256) k_ln_gelu_drop_fwd(
                        train, h_out, xhat_out, rstd_out);
 }
 
-// Backward of Dropout(GELU(LN(a))). 16 rows per block (4 waves x 4 rows);
-// per-block column partials of d(ln_w) = sum dy * xhat and d(ln_b) = sum dy.
-constexpr int kLnBwdRows = 16;
+// Backward of Dropout(GELU(LN(a))). 4 waves x rpw rows per block (rpw = 1 for
+// the small train batches, so that the grid is wide; 4 for large ones, so that
+// the partial buffer stays short); per-block column partials of
+// d(ln_w) = sum dy * xhat, d(ln_b) = sum dy and d(bias) = sum da.
+static inline int ln_bwd_rows_per_wave(int64_t nb) { return nb <= 2048 ? 1 : 4; }
 
 template <int NV>
 __global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
     const float* __restrict__ dh, const float* __restrict__ xhat, const float* __restrict__ rstd,
     const float* __restrict__ ln_w, const float* __restrict__ ln_b, int64_t nb, int64_t H,
     float p_drop, float scale, const float* __restrict__ drop_mult, uint64_t seed,
-    const int64_t* __restrict__ step_dev, uint32_t tag, int train, float* __restrict__ da,
-    float* __restrict__ part /* [nblocks][3][H] */) {
+    const int64_t* __restrict__ step_dev, uint32_t tag, int train, int rpw, float* __restrict__ da,
+    float* __restrict__ part /* [nblocks][3][H] */, unsigned* __restrict__ ticket, float* __restrict__ d_ln_w,
+    float* __restrict__ d_ln_b, float* __restrict__ d_bias) {
   extern __shared__ __attribute__((aligned(16))) float lds_part[];  // [4 waves][3][H]
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t step = load_step(step_dev);
@@ -177,8 +180,8 @@ __global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
 #pragma unroll
   for (int k = 0; k < NV; ++k) { pg[k] = make_float4(0.f, 0.f, 0.f, 0.f); pb[k] = pg[k]; pa[k] = pg[k]; }
 
-  for (int rr = 0; rr < kLnBwdRows / 4; ++rr) {
-    const int64_t b = (int64_t)blockIdx.x * kLnBwdRows + rr * 4 + w;
+  for (int rr = 0; rr < rpw; ++rr) {
+    const int64_t b = ((int64_t)blockIdx.x * rpw + rr) * 4 + w;
     if (b >= nb) break;
     const float rs = rstd[b];
     float4 dxh[NV], xh[NV];
@@ -236,6 +239,15 @@ __global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
   for (int64_t i = threadIdx.x; i < 3 * H; i += blockDim.x) {
     const float v = ((lds_part[i] + lds_part[3 * H + i]) + lds_part[6 * H + i]) + lds_part[9 * H + i];
     part[(int64_t)blockIdx.x * 3 * H + i] = v;
+  }
+  // short grids: the last block to finish sums the partials (same order as k_ln_part_reduce)
+  if (!ticket || !last_block_arrives(ticket, gridDim.x)) return;
+  for (int64_t i = threadIdx.x; i < 3 * H; i += blockDim.x) {
+    float s = 0.f;
+    for (int64_t p = 0; p < (int64_t)gridDim.x; ++p) s += __builtin_nontemporal_load(&part[p * 3 * H + i]);
+    if (i < H) d_ln_w[i] = s;
+    else if (i < 2 * H) d_ln_b[i - H] = s;
+    else if (d_bias) d_bias[i - 2 * H] = s;
   }
 }
 
@@ -528,63 +540,122 @@ __global__ void __launch_bounds__(256) k_rg_scatter(const int64_t* __restrict__ 
   }
 }
 
-// One block per item segment (grid-stride): sort the segment's contributions
-// by batch row (bitonic in LDS), then sum x * da[b, :] in that order.
+// Sort every item segment's contributions by batch row (keys are unique within
+// a segment: a CSR row holds an item at most once), in place, and re-zero the
+// fill counters. Segments of <= 64: one wave, bitonic network in registers;
+// 64 < len <= kSegSortCap: one block, bitonic in LDS. Longer segments stay
+// unsorted; k_rg_apply sums those in key order by selection instead.
 constexpr int kSegSortCap = 4096;
-
-__global__ void __launch_bounds__(256) k_rg_rows(const int32_t* __restrict__ n_unique,
-                                                 const int32_t* __restrict__ seg_off,
-                                                 int32_t* __restrict__ fill,
-                                                 const int32_t* __restrict__ contrib_row,
-                                                 const float* __restrict__ contrib_val,
-                                                 const float* __restrict__ da, int64_t H,
-                                                 float* __restrict__ out_rows) {
+__global__ void __launch_bounds__(256) k_rg_sort(const int32_t* __restrict__ n_unique,
+                                                 const int32_t* __restrict__ seg_off, int32_t* __restrict__ fill,
+                                                 int32_t* __restrict__ contrib_row, float* __restrict__ contrib_val) {
   __shared__ int key[kSegSortCap];
   __shared__ float kval[kSegSortCap];
   const int nu = *n_unique;
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (int s = gw; s < nu; s += nw) {
+    const int beg = seg_off[s], len = seg_off[s + 1] - beg;
+    if (lane == 0) fill[s] = 0;
+    if (len <= 1 || len > 64) continue;
+    int k_ = lane < len ? contrib_row[beg + lane] : 0x7fffffff;
+    float v_ = lane < len ? contrib_val[beg + lane] : 0.f;
+#pragma unroll
+    for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int pk = __shfl_xor(k_, j);
+        const float pv = __shfl_xor(v_, j);
+        const bool keep_min = ((lane & k) == 0) == ((lane & j) == 0);
+        if (keep_min ? (pk < k_) : (pk > k_)) { k_ = pk; v_ = pv; }
+      }
+    if (lane < len) { contrib_row[beg + lane] = k_; contrib_val[beg + lane] = v_; }
+  }
   for (int s = blockIdx.x; s < nu; s += gridDim.x) {
     const int beg = seg_off[s], len = seg_off[s + 1] - beg;
-    const bool sorted_path = len <= kSegSortCap;
-    if (sorted_path && len > 1) {
-      int p2 = 1;
-      while (p2 < len) p2 <<= 1;
-      for (int i = threadIdx.x; i < p2; i += 256) {
-        key[i] = (i < len) ? contrib_row[beg + i] : 0x7fffffff;
-        kval[i] = (i < len) ? contrib_val[beg + i] : 0.f;
-      }
-      __syncthreads();
-      for (int k = 2; k <= p2; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-          for (int i = threadIdx.x; i < p2; i += 256) {
-            const int ixj = i ^ j;
-            if (ixj > i) {
-              const bool up = (i & k) == 0;
-              const int a = key[i], c = key[ixj];
-              if ((a > c) == up) {
-                key[i] = c; key[ixj] = a;
-                const float t = kval[i]; kval[i] = kval[ixj]; kval[ixj] = t;
-              }
+    if (len <= 64 || len > kSegSortCap) continue;  // block-uniform
+    int p2 = 128;
+    while (p2 < len) p2 <<= 1;
+    __syncthreads();
+    for (int i = threadIdx.x; i < p2; i += 256) {
+      key[i] = (i < len) ? contrib_row[beg + i] : 0x7fffffff;
+      kval[i] = (i < len) ? contrib_val[beg + i] : 0.f;
+    }
+    __syncthreads();
+    for (int k = 2; k <= p2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = threadIdx.x; i < p2; i += 256) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const bool up = (i & k) == 0;
+            const int a = key[i], c = key[ixj];
+            if ((a > c) == up) {
+              key[i] = c; key[ixj] = a;
+              const float t = kval[i]; kval[i] = kval[ixj]; kval[ixj] = t;
             }
           }
-          __syncthreads();
+        }
+        __syncthreads();
+      }
+    }
+    for (int i = threadIdx.x; i < len; i += 256) { contrib_row[beg + i] = key[i]; contrib_val[beg + i] = kval[i]; }
+  }
+}
+
+// One wave per item segment: rows[s, :] = sum over the segment (ascending batch
+// row) of x * da[b, :]. Each lane owns 4 consecutive columns per 256-column pass.
+__global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_unique,
+                                                  const int32_t* __restrict__ seg_off,
+                                                  const int32_t* __restrict__ contrib_row,
+                                                  const float* __restrict__ contrib_val,
+                                                  const float* __restrict__ da, int64_t H,
+                                                  float* __restrict__ out_rows) {
+  const int nu = *n_unique;
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (int s = gw; s < nu; s += nw) {
+    const int beg = seg_off[s], len = seg_off[s + 1] - beg;
+    for (int64_t c0 = 0; c0 < H; c0 += 256) {
+      const int64_t c = c0 + 4 * lane;
+      const bool on = c < H;
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (len <= kSegSortCap) {
+        for (int i0 = 0; i0 < len; i0 += 64) {
+          const int n = min(64, len - i0);
+          const int mb = lane < n ? contrib_row[beg + i0 + lane] : 0;
+          const float mx = lane < n ? contrib_val[beg + i0 + lane] : 0.f;
+          for (int i = 0; i < n; ++i) {
+            const int b = __shfl(mb, i);
+            const float x = __shfl(mx, i);
+            if (on) {
+              const float4 d = *reinterpret_cast<const float4*>(da + (int64_t)b * H + c);
+              acc.x += x * d.x; acc.y += x * d.y; acc.z += x * d.z; acc.w += x * d.w;
+            }
+          }
+        }
+      } else {  // unsorted long segment: visit contributions in ascending key order
+        int prev = -1;
+        for (int it = 0; it < len; ++it) {
+          int best = 0x7fffffff;
+          float bx = 0.f;
+          for (int i = lane; i < len; i += 64) {
+            const int k = contrib_row[beg + i];
+            if (k > prev && k < best) { best = k; bx = contrib_val[beg + i]; }
+          }
+          for (int o = 32; o > 0; o >>= 1) {
+            const int ok = __shfl_xor(best, o);
+            const float ox = __shfl_xor(bx, o);
+            if (ok < best) { best = ok; bx = ox; }
+          }
+          prev = best;
+          if (on) {
+            const float4 d = *reinterpret_cast<const float4*>(da + (int64_t)best * H + c);
+            acc.x += bx * d.x; acc.y += bx * d.y; acc.z += bx * d.z; acc.w += bx * d.w;
+          }
         }
       }
-    } else if (len == 1) {
-      if (threadIdx.x == 0) { key[0] = contrib_row[beg]; kval[0] = contrib_val[beg]; }
-      __syncthreads();
+      if (on) *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + c) = acc;
     }
-    for (int64_t c4 = threadIdx.x; 4 * c4 < H; c4 += 256) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int i = 0; i < len; ++i) {
-        const int b = sorted_path ? key[i] : contrib_row[beg + i];
-        const float x = sorted_path ? kval[i] : contrib_val[beg + i];
-        const float4 d = *reinterpret_cast<const float4*>(da + (int64_t)b * H + 4 * c4);
-        acc.x += x * d.x; acc.y += x * d.y; acc.z += x * d.z; acc.w += x * d.w;
-      }
-      *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + 4 * c4) = acc;
-    }
-    if (threadIdx.x == 0) fill[s] = 0;
-    __syncthreads();
   }
 }
 
@@ -656,7 +727,7 @@ extern "C" int hvae_ln_gelu_drop_fwd(const float* a, const float* ln_w, const fl
 }
 
 extern "C" size_t hvae_ln_gelu_drop_bwd_workspace(int64_t nb, int64_t H) {
-  return (size_t)cdiv(nb, kLnBwdRows) * 3 * (size_t)H * sizeof(float);
+  return (size_t)cdiv(nb, 4 * ln_bwd_rows_per_wave(nb)) * 3 * (size_t)H * sizeof(float);
 }
 
 extern "C" int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const float* rstd,
@@ -678,16 +749,22 @@ extern "C" int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const f
   if (ws_bytes < need || !ws)
     HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_ln_gelu_drop_bwd: workspace %zu < %zu", ws_bytes, need);
   const float scale = (p_drop < 1.f) ? 1.0f / (1.0f - p_drop) : 0.f;
-  const int64_t nparts = cdiv(nb, kLnBwdRows);
+  const int rpw = ln_bwd_rows_per_wave(nb);
+  const int64_t nparts = cdiv(nb, 4 * rpw);
   const size_t lds = (size_t)12 * H * sizeof(float);
+  unsigned* ticket = nullptr;  // fused final reduction when the partial count is small
+  if (nparts <= 64 && !(ticket = ticket_slice())) return HVAE_ERR_HIP;
   HVAE_REQUIRE(lds <= 64 * 1024, "hvae_ln_gelu_drop_bwd: H too large (<= 1364)");
   HVAE_NV_DISPATCH(H, (k_ln_gelu_drop_bwd<NV><<<(unsigned)nparts, 256, lds, as_stream(stream)>>>(
                           dh, xhat, rstd, ln_w, ln_b, nb, H, p_drop, scale, drop_mult, seed,
-                          step_dev, kTagEncDrop + layer, train, da, (float*)ws)));
+                          step_dev, kTagEncDrop + layer, train, rpw, da, (float*)ws, ticket, d_ln_w, d_ln_b,
+                          d_bias)));
   HVAE_LAUNCH_CHECK("k_ln_gelu_drop_bwd");
-  k_ln_part_reduce<<<(unsigned)cdiv(3 * H, 256), 256, 0, as_stream(stream)>>>((const float*)ws, nparts,
-                                                                               H, d_ln_w, d_ln_b, d_bias);
-  HVAE_LAUNCH_CHECK("k_ln_part_reduce");
+  if (!ticket) {
+    k_ln_part_reduce<<<(unsigned)cdiv(3 * H, 256), 256, 0, as_stream(stream)>>>((const float*)ws, nparts,
+                                                                                 H, d_ln_w, d_ln_b, d_bias);
+    HVAE_LAUNCH_CHECK("k_ln_part_reduce");
+  }
   return HVAE_OK;
 }
 
@@ -716,13 +793,21 @@ extern "C" size_t hvae_w1_rowgrad_workspace(int64_t n_items) {
   return (size_t)2 * cdiv(n_items, kScanItemsPerBlock) * sizeof(int64_t);
 }
 
-extern "C" int hvae_w1_rowgrad(const hvae_csr_batch* x, const float* da, int64_t H,
-                               const hvae_rowgrad* rg, void* ws, size_t ws_bytes, void* stream) {
-  HVAE_REQUIRE(x && x->row_ptr && da && rg, "hvae_w1_rowgrad: null arg");
-  HVAE_REQUIRE(rg->cnt && rg->slot_of && rg->item_of && rg->seg_off && rg->fill &&
-                   rg->contrib_row && rg->contrib_val && rg->rows && rg->n_unique,
+static int rg_check(const hvae_rowgrad* rg) {
+  HVAE_REQUIRE(rg && rg->cnt && rg->slot_of && rg->item_of && rg->seg_off && rg->fill && rg->contrib_row &&
+                   rg->contrib_val && rg->rows && rg->n_unique,
                "hvae_w1_rowgrad: null rowgrad buffer");
-  if (int rc = check_hidden(H)) return rc;
+  return HVAE_OK;
+}
+
+static unsigned rg_grid(const hvae_rowgrad* rg) {
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, 4), 2048));
+}
+
+extern "C" int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad* rg, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  HVAE_REQUIRE(x && x->row_ptr, "hvae_w1_rowgrad_plan: null batch");
+  if (int rc = rg_check(rg)) return rc;
   HVAE_REQUIRE(rg->n_items == x->n_items, "hvae_w1_rowgrad: n_items mismatch");
   const int64_t N = x->n_items;
   const size_t need = hvae_w1_rowgrad_workspace(N);
@@ -754,11 +839,28 @@ extern "C" int hvae_w1_rowgrad(const hvae_csr_batch* x, const float* da, int64_t
                                       rg->seg_off, rg->fill, rg->contrib_row, rg->contrib_val,
                                       rg->cap);
   HVAE_LAUNCH_CHECK("k_rg_scatter");
-  const unsigned sgrid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(rg->cap, 2048));
-  k_rg_rows<<<sgrid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->fill, rg->contrib_row,
-                                   rg->contrib_val, da, H, rg->rows);
-  HVAE_LAUNCH_CHECK("k_rg_rows");
+  k_rg_sort<<<rg_grid(rg), 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->fill, rg->contrib_row, rg->contrib_val);
+  HVAE_LAUNCH_CHECK("k_rg_sort");
   return HVAE_OK;
+}
+
+extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowgrad* rg, void* stream) {
+  HVAE_REQUIRE(da, "hvae_w1_rowgrad_apply: null da");
+  if (int rc = rg_check(rg)) return rc;
+  if (int rc = check_hidden(H)) return rc;
+  k_rg_apply<<<rg_grid(rg), 256, 0, as_stream(stream)>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
+                                                           rg->contrib_val, da, H, rg->rows);
+  HVAE_LAUNCH_CHECK("k_rg_apply");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_w1_rowgrad(const hvae_csr_batch* x, const float* da, int64_t H,
+                               const hvae_rowgrad* rg, void* ws, size_t ws_bytes, void* stream) {
+  HVAE_REQUIRE(x && x->row_ptr && da && rg, "hvae_w1_rowgrad: null arg");
+  if (int rc = check_hidden(H)) return rc;
+  if (int rc = hvae_w1_rowgrad_plan(x, rg, ws, ws_bytes, stream)) return rc;
+  if (x->nb == 0) return HVAE_OK;
+  return hvae_w1_rowgrad_apply(da, H, rg, stream);
 }
 
 extern "C" int hvae_rowgrad_to_dense(const hvae_rowgrad* rg, int64_t H, float* dense, int64_t ld,

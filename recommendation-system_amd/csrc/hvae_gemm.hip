@@ -6,8 +6,10 @@
 // reference's nn.Linear layers). Tile 64x64x16 per 4-wave block, 32x32 per
 // wave (2x2 MFMA tiles); operands staged through LDS k-major so both
 // fragments are conflict-free ds_read_b32; split-K through a caller
-// workspace with a deterministic reduction for the tall-skinny weight
-// gradients (K = batch).
+// workspace for the tall-skinny weight gradients (K = batch): every split
+// block writes its partial tile, and the last block to arrive at a tile
+// (device-scope ticket) sums the partials in split order 0..S-1 and applies
+// the epilogue -- deterministic, and no second launch.
 #include <algorithm>
 
 #include "hvae_common.h"
@@ -25,6 +27,7 @@ constexpr int GSR = GBK + 2;   // stride of row-major images
 constexpr int GSK = 64 + 16;   // stride of k-major images
 constexpr int GIMG = (64 * GSR > GBK * GSK) ? 64 * GSR : GBK * GSK;
 constexpr int GLD4 = (64 * GBK / 4) / 256;  // float4 staged per thread per operand
+
 
 struct EpiArgs {
   int kind;
@@ -87,8 +90,8 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
                                                   float alpha, const float* __restrict__ A, int64_t lda,
                                                   const float* __restrict__ B, int64_t ldb, float beta,
                                                   float* __restrict__ C, int64_t ldc,
-                                                  float* __restrict__ slab, EpiArgs ep, bool vec_a,
-                                                  bool vec_b) {
+                                                  float* __restrict__ slab, unsigned* __restrict__ tickets,
+                                                  EpiArgs ep, bool vec_a, bool vec_b) {
   __shared__ __attribute__((aligned(16))) float sA[GIMG];
   __shared__ __attribute__((aligned(16))) float sB[GIMG];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -191,6 +194,23 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
     else ep.opa_rowsum[m0 + t] = alpha * rowsum;
   }
   const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP) ? load_step(ep.step_dev) : 0;
+  if (!slab) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
+          const int64_t col = n0 + wn + j * 16 + (lane & 15);
+          if (row >= M || col >= N) continue;
+          float c = alpha * acc[i][j][r];
+          if (beta != 0.f) c += beta * C[row * ldc + col];
+          C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
+        }
+    return;
+  }
+  // ---- split-K: publish the partial tile, the last arrival reduces
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -199,34 +219,25 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
       for (int r = 0; r < 4; ++r) {
         const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
         const int64_t col = n0 + wn + j * 16 + (lane & 15);
-        if (row >= M || col >= N) continue;
-        if (slab) {
-          slab[((int64_t)blockIdx.z * M + row) * N + col] = acc[i][j][r];
-        } else {
-          float c = alpha * acc[i][j][r];
-          if (beta != 0.f) c += beta * C[row * ldc + col];
-          C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
-        }
+        if (row < M && col < N) slab[((int64_t)blockIdx.z * M + row) * N + col] = acc[i][j][r];
       }
-}
-
-__global__ void k_gemm_splitk_reduce(int64_t M, int64_t N, int splits, float alpha,
-                                     const float* __restrict__ slab, float beta, float* __restrict__ C,
-                                     int64_t ldc, EpiArgs ep) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ep.opa_rowsum && i < M) {
-    float r = 0.f;
-    for (int z = 0; z < splits; ++z) r += slab[(int64_t)splits * M * N + (int64_t)z * M + i];
-    ep.opa_rowsum[i] = alpha * r;
+  const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
+  if (!last_block_arrives(&tickets[tile], gridDim.z)) return;
+  const int S = gridDim.z;
+  for (int e = t; e < GBM * GBN; e += 256) {
+    const int64_t row = m0 + e / GBN, col = n0 + e % GBN;
+    if (row >= M || col >= N) continue;
+    float sum = 0.f;
+    for (int z = 0; z < S; ++z) sum += __builtin_nontemporal_load(&slab[((int64_t)z * M + row) * N + col]);
+    float c = alpha * sum;
+    if (beta != 0.f) c += beta * C[row * ldc + col];
+    C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
   }
-  if (i >= M * N) return;
-  const int64_t row = i / N, col = i % N;
-  float s = 0.f;
-  for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * M * N + i];
-  float c = alpha * s;
-  if (beta != 0.f) c += beta * C[row * ldc + col];
-  const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP) ? load_step(ep.step_dev) : 0;
-  C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
+  if (ep.opa_rowsum && blockIdx.x == 0 && t < GBM && m0 + t < M) {
+    float r = 0.f;
+    for (int z = 0; z < S; ++z) r += __builtin_nontemporal_load(&slab[(int64_t)S * M * N + (int64_t)z * M + m0 + t]);
+    ep.opa_rowsum[m0 + t] = alpha * r;
+  }
 }
 
 // ---------------------------------------------------------------- colsum ---
@@ -319,21 +330,22 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
   const bool vec_b = (((uintptr_t)B) % 16 == 0) && (ldb % 4 == 0);
   dim3 grid((unsigned)cdiv(N, GBN), (unsigned)cdiv(M, GBM), (unsigned)std::max(splits, 1));
   float* slab = splits > 1 ? (float*)ws : nullptr;
+  unsigned* tickets = nullptr;
+  if (slab) {
+    HVAE_REQUIRE((uint64_t)grid.x * grid.y <= (uint64_t)kTicketSlice, "hvae_gemm_f32: too many split tiles");
+    tickets = ticket_slice();
+    if (!tickets) return HVAE_ERR_HIP;
+  }
   if (K == 0) kps = 0;
 #define HVAE_GEMM_CALL(TA_, TB_)                                                                  \
   k_gemm_f32<TA_, TB_><<<grid, 256, 0, st>>>(M, N, K, kps, alpha, A, lda, B, ldb, beta, C, ldc,   \
-                                             slab, ep, vec_a, vec_b)
+                                             slab, tickets, ep, vec_a, vec_b)
   if (!trans_a && !trans_b) HVAE_GEMM_CALL(false, false);
   else if (!trans_a && trans_b) HVAE_GEMM_CALL(false, true);
   else if (trans_a && !trans_b) HVAE_GEMM_CALL(true, false);
   else HVAE_GEMM_CALL(true, true);
 #undef HVAE_GEMM_CALL
   HVAE_LAUNCH_CHECK("k_gemm_f32");
-  if (slab) {
-    k_gemm_splitk_reduce<<<(unsigned)cdiv(std::max(M * N, M), 256), 256, 0, st>>>(M, N, splits, alpha, slab,
-                                                                                  beta, C, ldc, ep);
-    HVAE_LAUNCH_CHECK("k_gemm_splitk_reduce");
-  }
   return HVAE_OK;
 }
 

@@ -15,40 +15,53 @@ constexpr int kNormBlocks = 512;
 
 // Sum of squares over a dense flat gradient + the valid rows of a row-sparse
 // one, fixed grid, per-block partials in fp64 (deterministic).
-__global__ void __launch_bounds__(256) k_sqnorm_part(const float* __restrict__ g, int64_t n,
-                                                     const float* __restrict__ rows,
-                                                     const int32_t* __restrict__ n_unique, int64_t H,
-                                                     double* __restrict__ part) {
+// Global squared norm in fp64 over [dense grads | row-sparse W1 rows]; the last
+// block to finish reduces the per-block partials in block order, forms torch's
+// clip coefficient and (optionally) advances the step counters:
+//   step_snap = step; step += 1; boff += advance
+// so that the Adam launches that follow read the pre-increment step from
+// step_snap and no separate counter launch is needed.
+struct ClipArgs {
+  const float* g; int64_t n;
+  const float* rows; const int32_t* n_unique; int64_t H;
+  double* part; unsigned* ticket;
+  float max_norm; float* norm_out; float* coef_out;
+  int64_t* step; int64_t* step_snap; int64_t* boff; int64_t advance;
+};
+
+__global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
   __shared__ double red[4];
-  const int64_t nr = rows ? (int64_t)(*n_unique) * H : 0;
-  const int64_t tot = n + nr;
+  const int64_t nr = a.rows ? (int64_t)(*a.n_unique) * a.H : 0;
+  const int64_t tot = a.n + nr;
   double s = 0.0;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
-    const float v = (i < n) ? g[i] : rows[i - n];
+    const float v = (i < a.n) ? a.g[i] : a.rows[i - a.n];
     s += (double)v * (double)v;
   }
   s = wave_sum_d(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
-}
-
-__global__ void __launch_bounds__(256) k_sqnorm_final(const double* __restrict__ part, int nparts,
-                                                      float max_norm, float* __restrict__ norm_out,
-                                                      float* __restrict__ coef_out) {
-  __shared__ double red[4];
-  double s = 0.0;
-  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
-  s = wave_sum_d(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  if (threadIdx.x == 0) a.part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (!last_block_arrives(a.ticket, gridDim.x)) return;
+  double t = 0.0;
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) t += __builtin_nontemporal_load(&a.part[i]);
+  t = wave_sum_d(t);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
   __syncthreads();
   if (threadIdx.x == 0) {
     const float norm = (float)sqrt(((red[0] + red[1]) + red[2]) + red[3]);
     // torch: clip_coef = max_norm / (total_norm + 1e-6); clamp(max=1.0)
-    const float coef = fminf(max_norm / (norm + 1e-6f), 1.0f);
-    if (norm_out) *norm_out = norm;
-    *coef_out = coef;
+    const float coef = fminf(a.max_norm / (norm + 1e-6f), 1.0f);
+    if (a.norm_out) *a.norm_out = norm;
+    *a.coef_out = coef;
+    if (a.step) {
+      const int64_t st = *a.step;
+      if (a.step_snap) *a.step_snap = st;
+      *a.step = st + 1;
+    }
+    if (a.boff) *a.boff += a.advance;
   }
 }
 
@@ -150,20 +163,40 @@ extern "C" size_t hvae_clip_grad_norm_workspace(int64_t, int64_t, int64_t) {
   return kNormBlocks * sizeof(double);
 }
 
-extern "C" int hvae_clip_grad_norm(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg,
-                                   int64_t H, float max_norm, float* norm_out, float* coef_out,
-                                   void* ws, size_t ws_bytes, void* stream) {
+static int clip_launch(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg, int64_t H, float max_norm,
+                       float* norm_out, float* coef_out, int64_t* step, int64_t* step_snap, int64_t* boff,
+                       int64_t advance, void* ws, size_t ws_bytes, void* stream) {
   HVAE_REQUIRE(coef_out && n_dense >= 0 && (n_dense == 0 || g_dense), "hvae_clip_grad_norm: bad args");
   HVAE_REQUIRE(!rg || (rg->rows && rg->n_unique && H > 0), "hvae_clip_grad_norm: bad rowgrad");
   if (!ws || ws_bytes < kNormBlocks * sizeof(double))
     HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_clip_grad_norm: workspace too small");
-  hipStream_t st = as_stream(stream);
-  k_sqnorm_part<<<kNormBlocks, 256, 0, st>>>(g_dense, n_dense, rg ? rg->rows : nullptr,
-                                             rg ? rg->n_unique : nullptr, H, (double*)ws);
-  HVAE_LAUNCH_CHECK("k_sqnorm_part");
-  k_sqnorm_final<<<1, 256, 0, st>>>((const double*)ws, kNormBlocks, max_norm, norm_out, coef_out);
-  HVAE_LAUNCH_CHECK("k_sqnorm_final");
+  ClipArgs a{};
+  a.g = g_dense; a.n = n_dense;
+  a.rows = rg ? rg->rows : nullptr; a.n_unique = rg ? rg->n_unique : nullptr; a.H = H;
+  a.part = (double*)ws;
+  if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
+  a.max_norm = max_norm; a.norm_out = norm_out; a.coef_out = coef_out;
+  a.step = step; a.step_snap = step_snap; a.boff = boff; a.advance = advance;
+  k_clip_norm<<<kNormBlocks, 256, 0, as_stream(stream)>>>(a);
+  HVAE_LAUNCH_CHECK("k_clip_norm");
   return HVAE_OK;
+}
+
+extern "C" int hvae_clip_grad_norm(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg,
+                                   int64_t H, float max_norm, float* norm_out, float* coef_out,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  return clip_launch(g_dense, n_dense, rg, H, max_norm, norm_out, coef_out, nullptr, nullptr, nullptr, 0, ws,
+                     ws_bytes, stream);
+}
+
+extern "C" int hvae_clip_grad_norm_step(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg,
+                                        int64_t H, float max_norm, float* norm_out, float* coef_out,
+                                        int64_t* step_dev, int64_t* step_snap, int64_t* boff, int64_t advance,
+                                        void* ws, size_t ws_bytes, void* stream) {
+  HVAE_REQUIRE(step_dev && step_snap, "hvae_clip_grad_norm_step: null step counters");
+  HVAE_REQUIRE(advance == 0 || boff, "hvae_clip_grad_norm_step: advance without boff");
+  return clip_launch(g_dense, n_dense, rg, H, max_norm, norm_out, coef_out, step_dev, step_snap, boff, advance,
+                     ws, ws_bytes, stream);
 }
 
 extern "C" int hvae_adam_dense(const hvae_adam* cfg, float* p, float* m, float* v, const float* g,

@@ -78,6 +78,8 @@ SIGNATURES = {
     "hvae_ln_gelu_drop_bwd_workspace": (sz, [i64, i64]),
     "hvae_w1_rowgrad": (cint, [P(CsrBatch), vp, i64, P(RowGrad), vp, sz, vp]),
     "hvae_w1_rowgrad_workspace": (sz, [i64]),
+    "hvae_w1_rowgrad_plan": (cint, [P(CsrBatch), P(RowGrad), vp, sz, vp]),
+    "hvae_w1_rowgrad_apply": (cint, [vp, i64, P(RowGrad), vp]),
     "hvae_rowgrad_to_dense": (cint, [P(RowGrad), i64, vp, i64, vp]),
     "hvae_gemm_f32": (cint, [cint, cint, i64, i64, i64, f32, vp, i64, vp, i64, f32, vp, i64, P(Epilogue), vp,
                              sz, vp]),
@@ -91,10 +93,12 @@ SIGNATURES = {
     "hvae_decoder_supported": (cint, [cint, i64]),
     "hvae_row_norm_max": (cint, [cint, vp, i64, i64, vp, vp]),
     "hvae_decoder_bwd": (cint, [P(CsrBatch), vp, i64, vp, i64, vp, vp, f32, vp, vp, vp]),
+    "hvae_decoder_train": (cint, [cint, vp, i64, vp, vp, vp, P(CsrBatch), i64, f32, vp, vp, vp, vp, vp, sz, vp]),
     "hvae_nll_rows_fwd": (cint, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),
     "hvae_nll_rows_bwd": (cint, [vp, i64, vp, i64, vp, i64, i64, f32, vp, i64, vp]),
     "hvae_loss_finalize": (cint, [vp, vp, i64, f32, vp, vp, vp]),
     "hvae_clip_grad_norm": (cint, [vp, i64, P(RowGrad), i64, f32, vp, vp, vp, sz, vp]),
+    "hvae_clip_grad_norm_step": (cint, [vp, i64, P(RowGrad), i64, f32, vp, vp, vp, vp, vp, i64, vp, sz, vp]),
     "hvae_clip_grad_norm_workspace": (sz, [i64, i64, i64]),
     "hvae_adam_dense": (cint, [P(Adam), vp, vp, vp, vp, i64, vp]),
     "hvae_adam_rows": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp]),

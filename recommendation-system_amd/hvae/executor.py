@@ -164,7 +164,6 @@ class _StepBuffers:
         self.q = f(B, d) if lay.has_proj else None
         self.u = f(B, d) if lay.has_proj else self.z
         self.lse = f(B)
-        self.O = f(B, d)
         self.recon_rows = f(B)
         self.dU = f(B, d)
         self.dp1 = f(B, d) if lay.has_proj else None
@@ -192,6 +191,7 @@ class _StepBuffers:
         for (m_, n_, k_) in gemms:
             need.append(L_.hvae_gemm_f32_workspace(m_, n_, k_))
         self.ws = torch.empty(max(int(max(need)), 256), dtype=torch.uint8, device=dev)
+        self.ws2 = torch.empty_like(self.ws)  # side-stream GEMMs (split-K slabs must not alias the main stream's)
         self.graph = None
 
 
@@ -220,6 +220,8 @@ class FusedTrainer:
         self.g_small = torch.zeros(lay.n_small, device=device)
         self._adopt_parameters()
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=device)
+        self.step_snap = torch.zeros(1, dtype=torch.int64, device=device)  # step before this update (Adam's t - 1)
+        self.side = torch.cuda.Stream(device)
         self.boff = torch.zeros(1, dtype=torch.int64, device=device)
         self.norm = torch.zeros(1, device=device)
         self.coef = torch.ones(1, device=device)
@@ -344,24 +346,48 @@ class FusedTrainer:
         elif advance:
             self._advance(advance)
 
+    def _fork(self, src, dst):
+        """dst waits for everything enqueued on src so far (a graph edge under capture)."""
+        ev = torch.cuda.Event()
+        ev.record(src)
+        dst.wait_event(ev)
+
     def _launch_fwd_bwd(self, bf: _StepBuffers, csr: CsrBatch, train: bool, beta: float, p_drop: float,
                         ext: dict | None = None):
+        """Forward + loss (+ backward when train) of one batch.
+
+        Two streams: the main stream runs the dependent chain (forward, decoder,
+        data-gradient GEMMs, LayerNorm backward, W1 row gather); the side stream
+        runs what only feeds the optimizer -- the W1 row-gradient plan (needs the
+        batch only, so it overlaps the forward), the loss reduction and the
+        weight-gradient GEMMs -- and is joined back before the update.
+        """
         L_, lay = lib(), self.layout
-        st = torch.cuda.current_stream(self.device).cuda_stream
+        main = torch.cuda.current_stream(self.device)
+        side = self.side
+        st, st2 = main.cuda_stream, side.cuda_stream
         B, H, Lt, d = bf.B, lay.hidden, lay.L, lay.d
         ws, wsn = ptr(bf.ws), bf.ws.numel()
+        ws2 = ptr(bf.ws2)
         seed, step = self.seed, ptr(self.step_dev)
         tr = int(train)
         ext = ext or {}
         encm = ext.get("enc_masks", [None] * len(H))
         csr_ref = C.byref(csr)
 
-        def gemm(ta, tb, M, N, K, A, lda, Bm, ldb, Cm, ldc, epi=None, beta_=0.0, rowsum=None):
+        def gemm(ta, tb, M, N, K, A, lda, Bm, ldb, Cm, ldc, epi=None, beta_=0.0, rowsum=None, side_=False):
             if rowsum is not None:  # bias gradient = sum_k op(A)[m, k], fused into the weight-gradient GEMM
                 epi = Epilogue(_lib.EPI_NONE, None, None, None, 0.0, None, 0, None, 0, 0, ptr(rowsum))
             check(L_.hvae_gemm_f32(ta, tb, M, N, K, 1.0, A, lda, Bm, ldb, beta_, Cm, ldc,
-                                   C.byref(epi) if epi is not None else None, ws, wsn, st), "gemm")
+                                   C.byref(epi) if epi is not None else None, ws2 if side_ else ws, wsn,
+                                   st2 if side_ else st), "gemm")
 
+        if train:  # the row-gradient plan depends on the batch only: overlap it with the forward
+            self._fork(main, side)
+            check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st2),
+                  "w1_rowgrad_plan")
+            ev_plan = torch.cuda.Event()
+            ev_plan.record(side)
         # ------------------------------------------------------ forward ---
         check(L_.hvae_encoder_fwd(csr_ref, ptr(self.w1t), ptr(self.P["encoder.0.bias"]),
                                   ptr(self.P["encoder.1.weight"]), ptr(self.P["encoder.1.bias"]), H[0], p_drop,
@@ -391,32 +417,36 @@ class FusedTrainer:
             epi2 = Epilogue(_lib.EPI_BIAS, ptr(bb), None, None, 0.0, None, 0, None, 0, 0, None)
             gemm(0, 1, B, d, d, ptr(bf.q), d, ptr(Wb), d, ptr(bf.u), d, epi2)
         self._probe_begin("decoder_fwd")
-        check(L_.hvae_decoder_fwd(self.dec_dtype, ptr(bf.u), d, ptr(self.E_dec), ptr(self.enorm), B, lay.n_items, d,
-                                  ptr(bf.lse), ptr(bf.O) if train else None, ws, wsn, st), "decoder_fwd")
+        check(L_.hvae_decoder_train(self.dec_dtype, ptr(bf.u), d, ptr(self.E_dec), ptr(self.enorm), ptr(self.E32),
+                                    csr_ref, d, 1.0 / B, ptr(bf.lse), None, ptr(bf.recon_rows),
+                                    ptr(bf.dU) if train else None, ws, wsn, st), "decoder_train")
         self._probe_end("decoder_fwd")
-        check(L_.hvae_decoder_bwd(csr_ref, ptr(bf.u), d, ptr(self.E32), d, ptr(bf.lse), ptr(bf.O) if train else None,
-                                  1.0 / B, ptr(bf.recon_rows), ptr(bf.dU) if train else None, st), "decoder_bwd")
         accum = self.accum_train if train else self.accum_val
-        check(L_.hvae_loss_finalize(ptr(bf.recon_rows), ptr(bf.kl_rows), B, beta, ptr(bf.loss3), ptr(accum), st),
-              "loss_finalize")
         if not train:
+            check(L_.hvae_loss_finalize(ptr(bf.recon_rows), ptr(bf.kl_rows), B, beta, ptr(bf.loss3), ptr(accum), st),
+                  "loss_finalize")
             return
+        self._fork(main, side)
+        check(L_.hvae_loss_finalize(ptr(bf.recon_rows), ptr(bf.kl_rows), B, beta, ptr(bf.loss3), ptr(accum), st2),
+              "loss_finalize")
         # ----------------------------------------------------- backward ---
         G = self.G
         if lay.has_proj:
             gemm(1, 0, d, d, B, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d,
-                 rowsum=G["projection_layer.3.bias"])
+                 rowsum=G["projection_layer.3.bias"], side_=True)
             epi3 = Epilogue(_lib.EPI_GELU_DROP_BWD, None, None, ptr(bf.p1), p_drop, ptr(ext.get("proj_mask")), seed,
                             step, _lib.TAG_PROJ_DROP, tr, None)
             gemm(0, 0, B, d, d, ptr(bf.dU), d, ptr(Wb), d, ptr(bf.dp1), d, epi3)
+            self._fork(main, side)
             gemm(1, 0, d, Lt, B, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt,
-                 rowsum=G["projection_layer.0.bias"])
+                 rowsum=G["projection_layer.0.bias"], side_=True)
             gemm(0, 0, B, Lt, d, ptr(bf.dp1), d, ptr(Wa), Lt, ptr(bf.dz), Lt)
         dmu, dlv = bf.dheads, bf.dheads[:, Lt:]
         check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B, tr,
                                      ptr(dmu), ptr(dlv), 2 * Lt, st), "reparam_kl_bwd")
+        self._fork(main, side)
         gemm(1, 0, 2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl,
-             rowsum=self.gb_heads)
+             rowsum=self.gb_heads, side_=True)
         gemm(0, 0, B, Hl, 2 * Lt, ptr(bf.dheads), 2 * Lt, ptr(self.W_heads), Hl, ptr(bf.dh[-1]), Hl)
         for k in range(len(H) - 1, -1, -1):
             i = 4 * k
@@ -427,29 +457,38 @@ class FusedTrainer:
                                            ptr(G[f"encoder.{i}.bias"]), ws, wsn, st), "ln_gelu_drop_bwd")
             if k > 0:
                 W = self.P[f"encoder.{i}.weight"]
+                self._fork(main, side)
                 gemm(1, 0, H[k], H[k - 1], B, ptr(bf.da[k]), H[k], ptr(bf.h[k - 1]), H[k - 1],
-                     ptr(G[f"encoder.{i}.weight"]), H[k - 1])
+                     ptr(G[f"encoder.{i}.weight"]), H[k - 1], side_=True)
                 gemm(0, 0, B, H[k - 1], H[k], ptr(bf.da[k]), H[k], ptr(W), H[k - 1], ptr(bf.dh[k - 1]), H[k - 1])
-        check(L_.hvae_w1_rowgrad(csr_ref, ptr(bf.da[0]), H[0], bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st),
-              "w1_rowgrad")
+        main.wait_event(ev_plan)
+        check(L_.hvae_w1_rowgrad_apply(ptr(bf.da[0]), H[0], bf.rg.ref, st), "w1_rowgrad_apply")
+        self._fork(side, main)  # join: every gradient is complete on the main stream
 
     def _launch_update(self, rg, bf: _StepBuffers, advance: int = 0):
-        """clip_grad_norm_(5.0) + Adam over the flat state, then step += 1."""
+        """clip_grad_norm_(5.0) + Adam over the flat state; the clip launch also advances step (and boff).
+
+        The dense Adam of the small parameters runs on the side stream beside the
+        W1 Adam and is joined back at the end.
+        """
         L_, lay = lib(), self.layout
-        st = torch.cuda.current_stream(self.device).cuda_stream
+        main = torch.cuda.current_stream(self.device)
+        st, st2 = main.cuda_stream, self.side.cuda_stream
         H = lay.hidden
         ws, wsn = ptr(bf.ws), bf.ws.numel()
-        step = ptr(self.step_dev)
-        check(L_.hvae_clip_grad_norm(ptr(self.g_small), lay.n_small, rg.ref, H[0], self.max_norm,
-                                     ptr(self.norm), ptr(self.coef), ws, wsn, st), "clip_grad_norm")
-        cfg = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, self.coef)
+        check(L_.hvae_clip_grad_norm_step(ptr(self.g_small), lay.n_small, rg.ref, H[0], self.max_norm,
+                                          ptr(self.norm), ptr(self.coef), ptr(self.step_dev), ptr(self.step_snap),
+                                          ptr(self.boff) if advance else None, advance, ws, wsn, st),
+              "clip_grad_norm_step")
+        cfg = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_snap, self.coef)
+        self._fork(main, self.side)
+        check(L_.hvae_adam_dense(C.byref(cfg), ptr(self.small), ptr(self.m_small), ptr(self.v_small),
+                                 ptr(self.g_small), lay.n_small, st2), "adam_dense")
         self._probe_begin("adam_rows")
         check(L_.hvae_adam_rows(C.byref(cfg), ptr(self.w1t), ptr(self.m_w1t), ptr(self.v_w1t), rg.ref,
                                 lay.n_items, H[0], st), "adam_rows")
         self._probe_end("adam_rows")
-        check(L_.hvae_adam_dense(C.byref(cfg), ptr(self.small), ptr(self.m_small), ptr(self.v_small),
-                                 ptr(self.g_small), lay.n_small, st), "adam_dense")
-        check(L_.hvae_counters_add(step, 1, ptr(self.boff) if advance else None, advance, st), "counters_add")
+        self._fork(self.side, main)
 
     # ----------------------------------------------- live kernel timing ---
     probe: dict | None = None  # {"kernel": name, "events": [(start, end), ...]} (eager steps only)

@@ -283,6 +283,23 @@ def decoder_bwd(x: Csr, U, E32, lse, O, grad_scale: float, want_du: bool = True)
     return recon_rows, dU
 
 
+def decoder_train(x: Csr, U, E, enorm, E32, grad_scale: float, want_du: bool = True, want_o: bool = False):
+    """Fused sweep + finalize: (lse, O or None, recon_rows, dU or None)."""
+    require_hip(U, E, E32)
+    assert U.stride(1) == 1
+    nb, D = U.shape
+    dtype = _lib.HVAE_BF16 if E.dtype == torch.bfloat16 else _lib.HVAE_F32
+    lse = torch.empty(nb, device=U.device)
+    O = torch.empty(nb, D, device=U.device) if want_o else None
+    recon_rows = torch.empty(nb, device=U.device)
+    dU = torch.empty(nb, D, device=U.device) if want_du else None
+    ws = workspace(U.device, lib().hvae_decoder_workspace(dtype, nb, E.shape[0], D))
+    check(lib().hvae_decoder_train(dtype, ptr(U), U.stride(0), ptr(E), ptr(enorm), ptr(E32), x.ref, D,
+                                   float(grad_scale), ptr(lse), ptr(O), ptr(recon_rows), ptr(dU), ptr(ws), ws.numel(),
+                                   stream_of(U)), "hvae_decoder_train")
+    return lse, O, recon_rows, dU
+
+
 def nll_rows_fwd(S, X):
     require_hip(S, X)
     nb, N = S.shape

@@ -225,6 +225,14 @@ def test_decoder_large_norm_fixup(ops, hip_device):
     assert torch.isfinite(lse).all() and torch.isfinite(O).all()
     rel = ((lse.double().cpu() - torch.logsumexp(S, 1)).abs() / torch.logsumexp(S, 1).abs().clamp(min=1))
     assert rel.max() < 2e-3
+    # the fused train form recomputes flagged users inside its finalize: same lse, O-derived dU
+    X = synth_csr(8, N, lam=5.0, seed=2)
+    xd = ops.csr_from_scipy(X, hip_device)
+    Ed = E.to(hip_device)
+    lse_t, O_t, _, dU_t = ops.decoder_train(xd, U.to(hip_device), Ek, ops.row_norm_max(Ek), Ed, 0.125, want_o=True)
+    assert torch.equal(lse_t, lse) and torch.equal(O_t, O)
+    _, _, _, dU_n = ops.decoder_train(xd, U.to(hip_device), Ek, ops.row_norm_max(Ek), Ed, 0.125)
+    assert torch.equal(dU_n, dU_t)
 
 
 def test_decoder_bwd_sparse(ops, hip_device):
@@ -243,6 +251,35 @@ def test_decoder_bwd_sparse(ops, hip_device):
     rr.mean().backward()
     assert _maxrel(recon_rows, rr) < 1e-5
     assert _maxrel(dU, u_.grad) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("nb,N,D", [(40, 700, 384), (64, 12101, 384), (5, 3000, 128), (256, 2000, 64)])
+def test_decoder_train_fused(ops, hip_device, dtype, nb, N, D):
+    """Sweep + merge + sparse terms in one finalize launch == decoder_fwd + decoder_bwd == torch autograd."""
+    X = synth_csr(nb, N, lam=5.0, seed=nb + N)
+    x = torch.as_tensor(X.toarray(), dtype=torch.float32)
+    E = torch.as_tensor(synth_embeddings(N, D, seed=3))
+    g = torch.Generator().manual_seed(5)
+    U = torch.randn(nb, D, generator=g) * 2
+    xd = ops.csr_from_scipy(X, hip_device)
+    Ed, Ud = E.to(hip_device), U.to(hip_device)
+    Ek = ops.cast_bf16(Ed) if dtype == "bf16" else Ed
+    enorm = ops.row_norm_max(Ek)
+    lse, O, rr, dU = ops.decoder_train(xd, Ud, Ek, enorm, Ed, 1.0 / nb, want_o=True)
+    lse_b, O_b = ops.decoder_fwd(Ud, Ek, enorm)
+    rr_b, dU_b = ops.decoder_bwd(xd, Ud, Ed, lse_b, O_b, 1.0 / nb)
+    assert torch.equal(lse, lse_b) and torch.equal(rr, rr_b) and torch.equal(dU, dU_b) and torch.equal(O, O_b)
+    _, _, rr2, dU2 = ops.decoder_train(xd, Ud, Ek, enorm, Ed, 1.0 / nb)  # O kept internal
+    assert torch.equal(rr2, rr) and torch.equal(dU2, dU)
+    _, _, rr3, none = ops.decoder_train(xd, Ud, Ek, enorm, Ed, 1.0 / nb, want_du=False)
+    assert none is None and torch.equal(rr3, rr)
+    u_ = U.clone().requires_grad_(True)
+    rr_t = -(x * torch.log_softmax(u_ @ E.t(), 1)).sum(1)
+    rr_t.mean().backward()
+    tol = (1e-5, 1e-4) if dtype == "f32" else (3e-3, 2e-2)
+    assert _maxrel(rr, rr_t) < tol[0]
+    assert _maxrel(dU, u_.grad) < tol[1]
 
 
 def test_nll_rows(ops, hip_device):
@@ -292,6 +329,61 @@ def test_clip_and_adam(ops, hip_device):
         R.adam_update(p_w, w1g * c, rmw, rvw, t)
     assert _maxrel(ps_d, p_s) < 1e-6 and _maxrel(pw_d, p_w) < 1e-6
     assert _maxrel(mw, rmw) < 1e-6 and _maxrel(vw, rvw) < 1e-5
+
+
+def test_clip_step_counters(ops, hip_device):
+    """hvae_clip_grad_norm_step == hvae_clip_grad_norm + (snap = step; step += 1; boff += advance)."""
+    from hvae import _lib
+    from hvae._lib import lib, ptr, stream_of
+    g = torch.Generator().manual_seed(6)
+    small = torch.randn(70001, generator=g).to(hip_device)
+    norm_a, coef_a = ops.clip_grad_norm(small, None, 1.0)
+    norm, coef = torch.empty(1, device=hip_device), torch.empty(1, device=hip_device)
+    step = torch.full((1,), 41, dtype=torch.int64, device=hip_device)
+    snap = torch.zeros(1, dtype=torch.int64, device=hip_device)
+    boff = torch.full((1,), 128, dtype=torch.int64, device=hip_device)
+    ws = torch.empty(lib().hvae_clip_grad_norm_workspace(small.numel(), 0, 0), dtype=torch.uint8, device=hip_device)
+    for _ in range(3):
+        _lib.check(lib().hvae_clip_grad_norm_step(ptr(small), small.numel(), None, 0, 1.0, ptr(norm), ptr(coef),
+                                                  ptr(step), ptr(snap), ptr(boff), 64, ptr(ws), ws.numel(),
+                                                  stream_of(small)), "clip_step")
+    assert torch.equal(norm, norm_a) and torch.equal(coef, coef_a)
+    assert (int(step.item()), int(snap.item()), int(boff.item())) == (44, 43, 128 + 3 * 64)
+
+
+@pytest.mark.parametrize("nb,N,lam,hot", [(40, 300, 5.0, 0), (300, 2000, 8.0, 100), (5000, 500, 2.0, 4500)])
+def test_rowgrad_plan_apply_segments(ops, hip_device, nb, N, lam, hot):
+    """Segments of every sort path (wave <= 64, block <= 4096, selection beyond): plan + apply == dense
+    reference, bitwise == the one-call form, and bitwise reproducible."""
+    import scipy.sparse as sp
+    from hvae._lib import lib, ptr, stream_of
+    from hvae import _lib
+    X = synth_csr(nb, N, lam=lam, seed=nb)
+    if hot:  # item 0 in the first `hot` rows -> one long segment
+        X = X.tolil()
+        X[:hot, 0] = 1.0
+        X = sp.csr_matrix(X)
+    H = 128
+    g = torch.Generator().manual_seed(1)
+    da = torch.randn(nb, H, generator=g)
+    xd = ops.csr_from_scipy(X, hip_device)
+    dad = da.to(hip_device)
+    rg = ops.RowGradBuffers(N, H, int(X.nnz), hip_device)
+    ops.w1_rowgrad(xd, dad, rg)
+    nu = int(rg.n_unique.item())
+    one = rg.rows[:nu].clone()
+    dense = torch.zeros(N, H, device=hip_device)
+    ops.rowgrad_to_dense(rg, dense)
+    x = torch.as_tensor(X.toarray(), dtype=torch.float64)
+    assert _maxrel(dense, x.t() @ da.double()) < 1e-5
+    st = stream_of(dad)
+    _lib.check(lib().hvae_w1_rowgrad_plan(xd.ref, rg.ref, ptr(rg.ws), rg.ws.numel(), st), "plan")
+    _lib.check(lib().hvae_w1_rowgrad_apply(ptr(dad), H, rg.ref, st), "apply")
+    assert torch.equal(rg.rows[:nu], one)
+    assert int(rg.cnt.abs().sum()) == 0 and int(rg.fill.abs().sum()) == 0
+    if hot:  # the long segment (its own sort path) against a float64 sum
+        s0 = int((rg.item_of[:nu] == 0).nonzero()[0, 0])
+        assert _maxrel(rg.rows[s0], x[:, 0] @ da.double()) < 1e-5
 
 
 # ------------------------------------------------------------------ eval ---
