@@ -168,39 +168,48 @@ def main():
     ms = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
-    # ---- live per-kernel timing: HIP events around the kernel's launches (eager steps, same stream)
+    # ---- live per-kernel timing: libhvae brackets each launch of the armed kernel with a hipEvent pair
+    # recorded on the stream the kernel runs on (eager steps of the same workload, after the timed region)
+    import ctypes as C
+    from hvae._lib import check, lib
     N, H, D = w["items"], w["hidden"][0], w["d"]
-    kernels = {}
     fused.use_graphs = False
-    for name in ("adam_rows", "decoder_fwd"):
-        fused.probe = {"kernel": name, "events": []}
+
+    def probe(name):
+        check(lib().hvae_probe_arm(name.encode(), 64 * args.probe_steps), "probe_arm")
         run(args.probe_steps)
         torch.cuda.synchronize()
-        ts = [a.elapsed_time(b) * 1e-3 for a, b in fused.probe["events"]]
-        fused.probe = None
-        kernels[name] = float(np.mean(ts))
+        avg, n = C.c_double(), C.c_int()
+        check(lib().hvae_probe_collect(C.byref(avg), C.byref(n)), "probe_collect")
+        check(lib().hvae_probe_arm(None, 0), "probe_disarm")
+        return avg.value * 1e-6, n.value // args.probe_steps
+
+    kernels = {name: probe(name) for name in ("adam_rows", "decoder_sweep", "decoder_finalize", "encoder_fwd",
+                                             "gemm", "ln_bwd")}
     fused.use_graphs = True
-    adam_bytes = 24.0 * N * H + 4.0 * N                      # read+write p, m, v; slot lookup
-    dec_flops = 4.0 * B * N * D                               # S = U E^T and O = P E
+    adam_bytes = 24.0 * N * H + 4.0 * N                      # read+write p, m, v (fp32) + slot lookup per item
+    dec_flops = 4.0 * B * N * D                               # S = U E^T and O = P E over all items
     dec_peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
     roof = {
-        "adam_rows": {"bound": "hbm", "achieved": adam_bytes / kernels["adam_rows"] / 1e9, "peak": PEAK_HBM_GBS,
-                      "unit": "GB/s", "alg_per_launch": adam_bytes, "avg_launch_us": kernels["adam_rows"] * 1e6},
-        "decoder_fwd": {"bound": "mfma", "achieved": dec_flops / kernels["decoder_fwd"] / 1e12, "peak": dec_peak,
-                        "unit": "TFLOP/s", "alg_per_launch": dec_flops, "avg_launch_us": kernels["decoder_fwd"] * 1e6},
+        "adam_rows": {"bound": "hbm", "achieved": adam_bytes / kernels["adam_rows"][0] / 1e9, "peak": PEAK_HBM_GBS,
+                      "unit": "GB/s", "alg_per_launch": adam_bytes, "avg_launch_us": kernels["adam_rows"][0] * 1e6},
+        "decoder_sweep": {"bound": "mfma", "achieved": dec_flops / kernels["decoder_sweep"][0] / 1e12,
+                          "peak": dec_peak, "unit": "TFLOP/s", "alg_per_launch": dec_flops,
+                          "avg_launch_us": kernels["decoder_sweep"][0] * 1e6},
     }
-    dom = max(kernels, key=kernels.get)
+    dom = max(roof, key=lambda k: kernels[k][0])
     r = roof[dom]
     traffic = None
     pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
     if pmc.exists():
         try:
             traffic = json.loads(pmc.read_text()).get(dom, {}).get("hbm_bytes_per_launch")
-        except Exception:  # noqa: BLE001
+        except (ValueError, OSError):
             traffic = None
     roofline = {"bound": r["bound"], "achieved": round(r["achieved"], 2), "peak": r["peak"], "unit": r["unit"],
                 "frac": round(r["achieved"] / r["peak"], 4), "traffic": traffic, "kernel": dom,
                 "avg_launch_us": round(r["avg_launch_us"], 2)}
+    launch_us = {k: {"avg_us": round(v[0] * 1e6, 2), "launches_per_step": v[1]} for k, v in kernels.items()}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -226,6 +235,7 @@ def main():
             "roofline": roofline,
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in roof.items()},
+            "launch_us": launch_us,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -43,6 +43,14 @@ enum { HVAE_F32 = 0, HVAE_BF16 = 1 };
 int hvae_version(void);
 /* Copies the calling thread's last error text (NUL-terminated) into buf. */
 int hvae_last_error(char* buf, size_t len);
+/* Live kernel timing for benchmarks: arm one kernel by name ("decoder_sweep",
+ * "decoder_finalize", "adam_rows", "adam_dense", "encoder_fwd", "gemm",
+ * "ln_bwd", "rowgrad_apply", "clip"); its next max_launches launches
+ * (outside stream capture) are bracketed by a hipEvent pair recorded on the
+ * launch stream. hvae_probe_collect synchronizes those events and returns the
+ * mean launch duration. hvae_probe_arm(NULL, 0) disarms. */
+int hvae_probe_arm(const char* kernel, int max_launches);
+int hvae_probe_collect(double* avg_us, int* launches);
 
 /* ------------------------------------------------------------ data view -- */
 /* A batch of user rows of a CSR interaction matrix (users x items).

@@ -4,6 +4,8 @@
 #include <string.h>
 
 #include <atomic>
+#include <mutex>
+#include <vector>
 
 #include "hvae_common.h"
 
@@ -33,6 +35,31 @@ void set_error(const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
   va_end(ap);
+}
+
+// ---- live kernel timing
+struct Probe {
+  char name[64] = "";
+  std::vector<hipEvent_t> ev;  // [2 * cap]
+  int n = 0, cap = 0;
+  bool open = false;
+};
+static Probe g_probe;
+static std::mutex g_probe_mu;
+
+void probe_mark(const char* name, hipStream_t st, bool begin) {
+  if (g_probe.cap == 0) return;  // fast path: nothing armed
+  std::lock_guard<std::mutex> lk(g_probe_mu);
+  if (g_probe.cap == 0 || strcmp(name, g_probe.name) != 0) return;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  if (begin) {
+    if (g_probe.n >= g_probe.cap) return;
+    if (hipEventRecord(g_probe.ev[2 * g_probe.n], st) == hipSuccess) g_probe.open = true;
+  } else if (g_probe.open) {
+    if (hipEventRecord(g_probe.ev[2 * g_probe.n + 1], st) == hipSuccess) ++g_probe.n;
+    g_probe.open = false;
+  }
 }
 
 __global__ void k_counter_add(int64_t* c, int64_t d, int64_t* c2, int64_t d2) {
@@ -66,6 +93,37 @@ extern "C" int hvae_last_error(char* buf, size_t len) {
   if (!buf || len == 0) return HVAE_ERR_ARG;
   strncpy(buf, g_last_error, len - 1);
   buf[len - 1] = '\0';
+  return HVAE_OK;
+}
+
+extern "C" int hvae_probe_arm(const char* kernel, int max_launches) {
+  std::lock_guard<std::mutex> lk(g_probe_mu);
+  for (hipEvent_t e : g_probe.ev) (void)hipEventDestroy(e);
+  g_probe.ev.clear();
+  g_probe.n = g_probe.cap = 0;
+  g_probe.open = false;
+  g_probe.name[0] = '\0';
+  if (!kernel || max_launches <= 0) return HVAE_OK;
+  HVAE_REQUIRE(strlen(kernel) < sizeof(g_probe.name), "hvae_probe_arm: name too long");
+  g_probe.ev.resize(2 * (size_t)max_launches);
+  for (auto& e : g_probe.ev) HVAE_HIP(hipEventCreate(&e));
+  strcpy(g_probe.name, kernel);
+  g_probe.cap = max_launches;
+  return HVAE_OK;
+}
+
+extern "C" int hvae_probe_collect(double* avg_us, int* launches) {
+  HVAE_REQUIRE(avg_us && launches, "hvae_probe_collect: null out");
+  std::lock_guard<std::mutex> lk(g_probe_mu);
+  double tot = 0.0;
+  for (int i = 0; i < g_probe.n; ++i) {
+    HVAE_HIP(hipEventSynchronize(g_probe.ev[2 * i + 1]));
+    float ms = 0.f;
+    HVAE_HIP(hipEventElapsedTime(&ms, g_probe.ev[2 * i], g_probe.ev[2 * i + 1]));
+    tot += ms;
+  }
+  *launches = g_probe.n;
+  *avg_us = g_probe.n ? tot * 1e3 / g_probe.n : 0.0;
   return HVAE_OK;
 }
 

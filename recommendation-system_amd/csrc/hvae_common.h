@@ -59,23 +59,55 @@ static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream
 constexpr int kTicketPool = 1 << 16, kTicketSlice = 256;
 unsigned* ticket_slice();  // nullptr (error set) on failure
 
-// Called by every thread of a block after it wrote its partials: true in the
-// one block that arrives last at ticket *t (and then everything the other
-// blocks wrote before arriving is visible to it).
+// Partials exchanged between the blocks of one launch go through agent-coherent
+// (sc1) stores and loads: they bypass the per-XCD L2s that plain accesses may
+// hit stale, without the whole-L2 writeback / invalidate an agent-scope
+// __threadfence() costs on gfx950 (that cost per block is what made a fenced
+// version slower than a second launch).
+__device__ __forceinline__ void st_shared_f(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_shared_f(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_shared_d(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_shared_d(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Called by every thread of a block after it wrote its partials with
+// st_shared_*: true in the one block that arrives last at ticket *t; that block
+// then reads every block's partials with ld_shared_*. Each thread waits for its
+// own stores to complete (s_waitcnt 0) before the barrier, so all of the
+// block's partials have reached the coherence point before thread 0 takes a
+// ticket.
 __device__ __forceinline__ bool last_block_arrives(unsigned* t, unsigned n_blocks) {
   __shared__ unsigned s_last;
-  __threadfence();  // release (L2 writeback: blocks of other XCDs read it)
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned old = atomicAdd(t, 1u);
+    const unsigned old = __hip_atomic_fetch_add(t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = (old == n_blocks - 1);
-    if (s_last) *t = 0u;  // nobody else touches it again in this launch
+    if (s_last) __hip_atomic_store(t, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  const bool last = s_last;
-  if (last) __threadfence();  // acquire
-  return last;
+  return s_last;
 }
+
+// Live kernel timing (hvae_probe_arm / hvae_probe_collect): a launcher brackets
+// the launch of a named kernel with ProbeScope; when that name is armed (and
+// the stream is not capturing) a hipEvent pair is recorded around it on its
+// own stream.
+void probe_mark(const char* name, hipStream_t st, bool begin);
+struct ProbeScope {
+  const char* name;
+  hipStream_t st;
+  ProbeScope(const char* n, hipStream_t s) : name(n), st(s) { probe_mark(name, st, true); }
+  ~ProbeScope() { probe_mark(name, st, false); }
+};
+
 static inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // --------------------------------------------------------------- device ----

@@ -482,13 +482,31 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     L = block_sum<256>(L, red);  // its barriers also publish wsh and any_flag
     lse_b = M + logf(L);
     const float inv = 1.0f / L;
+    if (a.pO) {
+      // sum_s w_s O_s in split order; loads batched 8 splits x 4 columns deep so that
+      // they are in flight together (a one-at-a-time chain is HBM-latency bound)
+      const int nk = (int)min<int64_t>(4, (D - tid + 255) / 256);
+      const int64_t sstride = a.nb * D;
+      const float* base = a.pO + b * D + tid;
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      int s0 = 0;
+      for (; s0 + 8 <= a.splits; s0 += 8) {
+        float v[8][4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t d = tid + 256 * k;
-      if (d >= D || !a.pO) continue;
-      float acc = 0.f;
-      for (int s = 0; s < a.splits; ++s) acc += wsh[s] * a.pO[((int64_t)s * a.nb + b) * D + d];
-      o[k] = acc * inv;
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) v[j][k] = k < nk ? base[(int64_t)(s0 + j) * sstride + 256 * k] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc[k] += wsh[s0 + j] * v[j][k];
+      }
+      for (; s0 < a.splits; ++s0)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k < nk) acc[k] += wsh[s0] * base[(int64_t)s0 * sstride + 256 * k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) o[k] = acc[k] * inv;
     }
   } else {
     if (a.flag && a.flag[b]) any_flag = 1;
@@ -517,6 +535,7 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   const int64_t beg = a.row_ptr[r], end = a.row_ptr[r + 1];
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float n = 0.f;
+#pragma unroll 4
   for (int64_t e = beg; e < end; ++e) {
     const int64_t j = a.col_idx[e];
     const float x = a.vals[e];
@@ -769,8 +788,12 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
     o.l = base + (size_t)p.splits * nb;
     o.O = base + (size_t)2 * p.splits * nb;
   }
-  int rc = want_o ? dispatch<true>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st)
+  int rc;
+  {
+    ProbeScope probe("decoder_sweep", st);
+    rc = want_o ? dispatch<true>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st)
                   : dispatch<false>(dtype, U, ldu, E, e_maxnorm, nb, N, D, p, o, st);
+  }
   if (rc) return rc;
   if (p.splits == 1 && !bf && !x) return HVAE_OK;  // fp32 single split: the sweep wrote lse / O already
   FinArgs a{};
@@ -789,6 +812,7 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   a.O_out = O ? O : (p.splits == 1 ? o_scratch : nullptr);
   a.recon_rows = recon_rows;
   a.dU = dU;
+  ProbeScope probe("decoder_finalize", st);
   k_dec_finalize<<<(unsigned)nb, 256, 0, st>>>(a);
   HVAE_LAUNCH_CHECK("k_dec_finalize");
   return HVAE_OK;

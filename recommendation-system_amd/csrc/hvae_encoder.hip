@@ -238,13 +238,24 @@ __global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
   __syncthreads();
   for (int64_t i = threadIdx.x; i < 3 * H; i += blockDim.x) {
     const float v = ((lds_part[i] + lds_part[3 * H + i]) + lds_part[6 * H + i]) + lds_part[9 * H + i];
-    part[(int64_t)blockIdx.x * 3 * H + i] = v;
+    if (ticket) st_shared_f(&part[(int64_t)blockIdx.x * 3 * H + i], v);
+    else part[(int64_t)blockIdx.x * 3 * H + i] = v;
   }
   // short grids: the last block to finish sums the partials (same order as k_ln_part_reduce)
   if (!ticket || !last_block_arrives(ticket, gridDim.x)) return;
+  // coherent loads batched 8 partials deep (a serial chain would pay the full latency per partial)
+  const int np = gridDim.x;
   for (int64_t i = threadIdx.x; i < 3 * H; i += blockDim.x) {
     float s = 0.f;
-    for (int64_t p = 0; p < (int64_t)gridDim.x; ++p) s += __builtin_nontemporal_load(&part[p * 3 * H + i]);
+    int p = 0;
+    for (; p + 8 <= np; p += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = ld_shared_f(&part[(int64_t)(p + j) * 3 * H + i]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; p < np; ++p) s += ld_shared_f(&part[(int64_t)p * 3 * H + i]);
     if (i < H) d_ln_w[i] = s;
     else if (i < 2 * H) d_ln_b[i - H] = s;
     else if (d_bias) d_bias[i - 2 * H] = s;
@@ -701,6 +712,7 @@ extern "C" int hvae_encoder_fwd(const hvae_csr_batch* x, const float* w1t, const
   HVAE_REQUIRE(x->col_idx && x->vals, "hvae_encoder_fwd: null CSR arrays");
   const float scale = (p_drop < 1.f) ? 1.0f / (1.0f - p_drop) : 0.f;
   const unsigned grid = (unsigned)cdiv(x->nb, 4);
+  ProbeScope probe("encoder_fwd", as_stream(stream));
   HVAE_NV_DISPATCH(H, (k_encoder_sparse_fwd<NV><<<grid, 256, 0, as_stream(stream)>>>(
                           x->row_ptr, x->col_idx, x->vals, x->rows, x->rows_offset, x->nb, w1t, b1, ln_w, ln_b, H,
                           p_drop, scale, drop_mult, seed, step_dev, train, h_out, xhat_out,
@@ -755,6 +767,7 @@ extern "C" int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const f
   unsigned* ticket = nullptr;  // fused final reduction when the partial count is small
   if (nparts <= 64 && !(ticket = ticket_slice())) return HVAE_ERR_HIP;
   HVAE_REQUIRE(lds <= 64 * 1024, "hvae_ln_gelu_drop_bwd: H too large (<= 1364)");
+  ProbeScope probe("ln_bwd", as_stream(stream));
   HVAE_NV_DISPATCH(H, (k_ln_gelu_drop_bwd<NV><<<(unsigned)nparts, 256, lds, as_stream(stream)>>>(
                           dh, xhat, rstd, ln_w, ln_b, nb, H, p_drop, scale, drop_mult, seed,
                           step_dev, kTagEncDrop + layer, train, rpw, da, (float*)ws, ticket, d_ln_w, d_ln_b,
@@ -848,6 +861,7 @@ extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowg
   HVAE_REQUIRE(da, "hvae_w1_rowgrad_apply: null da");
   if (int rc = rg_check(rg)) return rc;
   if (int rc = check_hidden(H)) return rc;
+  ProbeScope probe("rowgrad_apply", as_stream(stream));
   k_rg_apply<<<rg_grid(rg), 256, 0, as_stream(stream)>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
                                                            rg->contrib_val, da, H, rg->rows);
   HVAE_LAUNCH_CHECK("k_rg_apply");

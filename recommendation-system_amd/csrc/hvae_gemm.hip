@@ -3,9 +3,9 @@
 // v_mfma_f32_16x16x4_f32: one f32 A and one f32 B per lane, 4 accumulators,
 // numerically a k-ordered fmaf chain (no reduced-precision fast path exists
 // on gfx950, and none is wanted: these GEMMs carry the fp32 parity of the
-// reference's nn.Linear layers). Tile 64x64x16 per 4-wave block, 32x32 per
-// wave (2x2 MFMA tiles); operands staged through LDS k-major so both
-// fragments are conflict-free ds_read_b32; split-K through a caller
+// reference's nn.Linear layers). Tile 64x64 or 32x32 per 4-wave block
+// (2x2 or 1x1 MFMA tiles per wave); operands staged through LDS in memory
+// order; K per block up to 384 loaded in one go; split-K through a caller
 // workspace for the tall-skinny weight gradients (K = batch): every split
 // block writes its partial tile, and the last block to arrive at a tile
 // (device-scope ticket) sums the partials in split order 0..S-1 and applies
@@ -18,16 +18,23 @@ namespace hvae {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int GBM = 64, GBN = 64, GBK = 32;
+constexpr int GBK = 32;
+// Block tiles BM x BN (64x64 or 32x32), 4 waves as 2x2, each wave (BM/2) x (BN/2) in
+// 16x16 MFMA tiles. The 32x32 tile puts 4x more CUs on the batch-sized GEMMs of the
+// step (M = 64 users): on the exact-f32 MFMA (256 flop/clk/CU) a 64x64x384 tile alone
+// is ~5 us of one CU, so the output must be spread wide.
 // LDS images keep each operand in its memory order (no transposing stores):
-//   row-major A[m][k] / B^T[n][k]  -> [64 rows][GBK + 2] (float2 stores; fragment reads
+//   row-major A[m][k] / B^T[n][k]  -> [BM rows][GBK + 2] (float2 stores; fragment reads
 //                                     hit banks 2*row + k: conflict-free for ds_read_b32)
-//   k-major A^T[k][m] / B[k][n]    -> [GBK rows][64 + 16] (float4 stores; rows 16 banks apart)
-constexpr int GSR = GBK + 2;   // stride of row-major images
-constexpr int GSK = 64 + 16;   // stride of k-major images
-constexpr int GIMG = (64 * GSR > GBK * GSK) ? 64 * GSR : GBK * GSK;
-constexpr int GLD4 = (64 * GBK / 4) / 256;  // float4 staged per thread per operand
-
+//   k-major A^T[k][m] / B[k][n]    -> [GBK rows][BM + 16] (float4 stores)
+constexpr int GSR = GBK + 2;  // stride of row-major images
+template <int BM>
+struct GTile {
+  static constexpr int SK = BM + 16;                                  // stride of k-major images
+  static constexpr int IMG = (BM * GSR > GBK * SK) ? BM * GSR : GBK * SK;
+  static constexpr int LD4 = (BM * GBK / 4 + 255) / 256;             // float4 staged per thread
+};
+constexpr int kRegStages = 12;  // k-tiles a block keeps in flight at once (K per block <= 384)
 
 struct EpiArgs {
   int kind;
@@ -85,46 +92,53 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ p, int64_t idx
   return r;
 }
 
-template <bool TA, bool TB>
+template <bool TA, bool TB, int BM, int BN>
 __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t K, int64_t k_per_split,
                                                   float alpha, const float* __restrict__ A, int64_t lda,
                                                   const float* __restrict__ B, int64_t ldb, float beta,
                                                   float* __restrict__ C, int64_t ldc,
                                                   float* __restrict__ slab, unsigned* __restrict__ tickets,
                                                   EpiArgs ep, bool vec_a, bool vec_b) {
-  __shared__ __attribute__((aligned(16))) float sA[GIMG];
-  __shared__ __attribute__((aligned(16))) float sB[GIMG];
+  using TAo = GTile<BM>;
+  using TBo = GTile<BN>;
+  constexpr int IM = BM / 32, JN = BN / 32;  // 16x16 MFMA tiles per wave
+  __shared__ __attribute__((aligned(16))) float sA[2][TAo::IMG];
+  __shared__ __attribute__((aligned(16))) float sB[2][TBo::IMG];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t m0 = (int64_t)blockIdx.y * GBM, n0 = (int64_t)blockIdx.x * GBN;
+  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
   const int64_t kb = (int64_t)blockIdx.z * k_per_split;
   const int64_t ke = min(K, kb + k_per_split);
-  const int wm = (w >> 1) * 32, wn = (w & 1) * 32;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
 
-  f32x4 acc[2][2];
+  f32x4 acc[IM][JN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < IM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float4 ra[GLD4], rb[GLD4];
   const bool do_rowsum = ep.opa_rowsum != nullptr && blockIdx.x == 0;
-  float rowsum = 0.f;  // thread t < 64: sum over this block's k range of op(A)[m0 + t][k]
+  float rowsum = 0.f;  // thread t < BM: sum over this block's k range of op(A)[m0 + t][k]
   // Operand element (r = m or n, k): row-major sources stage f -> (r = f / (GBK/4), k = 4 (f % (GBK/4)));
-  // k-major sources stage f -> (k = f / 16, r = 4 (f % 16)).
-  constexpr int KQ = GBK / 4;
-  auto gload = [&](int64_t k0) {
+  // k-major sources stage f -> (k = f / (R/4), r = 4 (f % (R/4))).
+  constexpr int KQ = GBK / 4, MQ = BM / 4, NQ = BN / 4;
+  constexpr int LA = TAo::LD4, LB = TBo::LD4;
+  auto gload = [&](int64_t k0, float4 (&ra)[LA], float4 (&rb)[LB]) {
 #pragma unroll
-    for (int i = 0; i < GLD4; ++i) {
+    for (int i = 0; i < LA; ++i) {
       const int f = t + 256 * i;
       if (!TA) {
         const int64_t m = m0 + f / KQ, k = k0 + (f % KQ) * 4;
         ra[i] = (m < M) ? load4(A + m * lda + k, k, ke, vec_a) : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
-        const int64_t k = k0 + (f >> 4), m = m0 + (f & 15) * 4;
+        const int64_t k = k0 + f / MQ, m = m0 + (f % MQ) * 4;
         ra[i] = (k < ke) ? load4(A + k * lda + m, m, M, vec_a) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int f = t + 256 * i;
       if (!TB) {
-        const int64_t k = k0 + (f >> 4), n = n0 + (f & 15) * 4;
+        const int64_t k = k0 + f / NQ, n = n0 + (f % NQ) * 4;
         rb[i] = (k < ke) ? load4(B + k * ldb + n, n, N, vec_b) : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         const int64_t n = n0 + f / KQ, k = k0 + (f % KQ) * 4;
@@ -132,73 +146,103 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
       }
     }
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int buf, const float4 (&ra)[LA], const float4 (&rb)[LB]) {
+    float* a_ = sA[buf];
+    float* b_ = sB[buf];
 #pragma unroll
-    for (int i = 0; i < GLD4; ++i) {
+    for (int i = 0; i < LA; ++i) {
       const int f = t + 256 * i;
       if (!TA) {
-        float* d = &sA[(f / KQ) * GSR + (f % KQ) * 4];
+        float* d = &a_[(f / KQ) * GSR + (f % KQ) * 4];
         *reinterpret_cast<float2*>(d) = make_float2(ra[i].x, ra[i].y);
         *reinterpret_cast<float2*>(d + 2) = make_float2(ra[i].z, ra[i].w);
       } else {
-        *reinterpret_cast<float4*>(&sA[(f >> 4) * GSK + (f & 15) * 4]) = ra[i];
+        *reinterpret_cast<float4*>(&a_[(f / MQ) * TAo::SK + (f % MQ) * 4]) = ra[i];
       }
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+      const int f = t + 256 * i;
       if (!TB) {
-        *reinterpret_cast<float4*>(&sB[(f >> 4) * GSK + (f & 15) * 4]) = rb[i];
+        *reinterpret_cast<float4*>(&b_[(f / NQ) * TBo::SK + (f % NQ) * 4]) = rb[i];
       } else {
-        float* d = &sB[(f / KQ) * GSR + (f % KQ) * 4];
+        float* d = &b_[(f / KQ) * GSR + (f % KQ) * 4];
         *reinterpret_cast<float2*>(d) = make_float2(rb[i].x, rb[i].y);
         *reinterpret_cast<float2*>(d + 2) = make_float2(rb[i].z, rb[i].w);
       }
     }
   };
-  // op(A)[m][k] / op(B)[k][n] as staged
-  auto a_at = [&](int m, int k) -> float { return TA ? sA[k * GSK + m] : sA[m * GSR + k]; };
-  auto b_at = [&](int k, int n) -> float { return TB ? sB[n * GSR + k] : sB[k * GSK + n]; };
+  // one staged k-tile: MFMA chain in k order (+ the fused row sums)
+  auto compute = [&](int buf) {
+    const float* a_ = sA[buf];
+    const float* b_ = sB[buf];
+    auto a_at = [&](int m, int k) -> float { return TA ? a_[k * TAo::SK + m] : a_[m * GSR + k]; };
+    auto b_at = [&](int k, int n) -> float { return TB ? b_[n * GSR + k] : b_[k * TBo::SK + n]; };
+    if (do_rowsum && t < BM) {
+#pragma unroll
+      for (int k = 0; k < GBK; ++k) rowsum += a_at(t, k);
+    }
+#pragma unroll
+    for (int kk = 0; kk < GBK / 4; ++kk) {
+      const int kr = 4 * kk + (lane >> 4);
+      float af[IM], bfr[JN];
+#pragma unroll
+      for (int i = 0; i < IM; ++i) af[i] = a_at(wm + i * 16 + (lane & 15), kr);
+#pragma unroll
+      for (int j = 0; j < JN; ++j) bfr[j] = b_at(kr, wn + j * 16 + (lane & 15));
+#pragma unroll
+      for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
 
-  if (kb < ke) {
-    gload(kb);
-    lstore();
+  const int64_t nst = (ke > kb) ? (ke - kb + GBK - 1) / GBK : 0;
+  if (nst > 0 && nst <= kRegStages) {
+    // short k range (the batch-sized GEMMs of the path): every global load of the block is issued
+    // up front -- one memory latency instead of one per k-tile -- then the tiles stream through
+    // double-buffered LDS with one barrier each
+    float4 ra[kRegStages][LA], rb[kRegStages][LB];
+#pragma unroll
+    for (int st = 0; st < kRegStages; ++st)
+      if (st < nst) gload(kb + (int64_t)st * GBK, ra[st], rb[st]);
+#pragma unroll
+    for (int st = 0; st < kRegStages; ++st) {
+      if (st < nst) {
+        lstore(st & 1, ra[st], rb[st]);
+        __syncthreads();
+        compute(st & 1);
+      }
+    }
+  } else if (nst > 0) {
+    float4 ra[LA], rb[LB];
+    gload(kb, ra, rb);
+    lstore(0, ra, rb);
     __syncthreads();
+    int buf = 0;
     for (int64_t k0 = kb; k0 < ke; k0 += GBK) {
       const bool more = k0 + GBK < ke;
-      if (more) gload(k0 + GBK);
-      if (do_rowsum && t < GBM) {
-#pragma unroll
-        for (int k = 0; k < GBK; ++k) rowsum += a_at(t, k);
-      }
-#pragma unroll
-      for (int kk = 0; kk < GBK / 4; ++kk) {
-        const int kr = 4 * kk + (lane >> 4);
-        float af[2], bfr[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = a_at(wm + i * 16 + (lane & 15), kr);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bfr[j] = b_at(kr, wn + j * 16 + (lane & 15));
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
-      __syncthreads();
+      if (more) gload(k0 + GBK, ra, rb);
+      compute(buf);
       if (more) {
-        lstore();
+        lstore(buf ^ 1, ra, rb);
         __syncthreads();
+        buf ^= 1;
       }
     }
   }
 
-  if (do_rowsum && t < GBM && m0 + t < M) {
-    if (slab) slab[(int64_t)gridDim.z * M * N + (int64_t)blockIdx.z * M + m0 + t] = rowsum;
+  if (do_rowsum && t < BM && m0 + t < M) {
+    if (slab) st_shared_f(&slab[(int64_t)gridDim.z * M * N + (int64_t)blockIdx.z * M + m0 + t], rowsum);
     else ep.opa_rowsum[m0 + t] = alpha * rowsum;
   }
   const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP) ? load_step(ep.step_dev) : 0;
   if (!slab) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < IM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < JN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
@@ -212,30 +256,46 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
   }
   // ---- split-K: publish the partial tile, the last arrival reduces
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < IM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < JN; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
         const int64_t col = n0 + wn + j * 16 + (lane & 15);
-        if (row < M && col < N) slab[((int64_t)blockIdx.z * M + row) * N + col] = acc[i][j][r];
+        if (row < M && col < N) st_shared_f(&slab[((int64_t)blockIdx.z * M + row) * N + col], acc[i][j][r]);
       }
   const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
   if (!last_block_arrives(&tickets[tile], gridDim.z)) return;
+  // the tile's elements per thread: one coherent load each per split, all in flight together
+  constexpr int Q = BM * BN / 256;
   const int S = gridDim.z;
-  for (int e = t; e < GBM * GBN; e += 256) {
-    const int64_t row = m0 + e / GBN, col = n0 + e % GBN;
+  float sum[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) sum[q] = 0.f;
+  for (int z = 0; z < S; ++z) {
+    float v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int e = t + 256 * q;
+      const int64_t row = m0 + e / BN, col = n0 + e % BN;
+      v[q] = (row < M && col < N) ? ld_shared_f(&slab[((int64_t)z * M + row) * N + col]) : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) sum[q] += v[q];
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int e = t + 256 * q;
+    const int64_t row = m0 + e / BN, col = n0 + e % BN;
     if (row >= M || col >= N) continue;
-    float sum = 0.f;
-    for (int z = 0; z < S; ++z) sum += __builtin_nontemporal_load(&slab[((int64_t)z * M + row) * N + col]);
-    float c = alpha * sum;
+    float c = alpha * sum[q];
     if (beta != 0.f) c += beta * C[row * ldc + col];
     C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
   }
-  if (ep.opa_rowsum && blockIdx.x == 0 && t < GBM && m0 + t < M) {
+  if (ep.opa_rowsum && blockIdx.x == 0 && t < BM && m0 + t < M) {
     float r = 0.f;
-    for (int z = 0; z < S; ++z) r += __builtin_nontemporal_load(&slab[(int64_t)S * M * N + (int64_t)z * M + m0 + t]);
+    for (int z = 0; z < S; ++z) r += ld_shared_f(&slab[(int64_t)S * M * N + (int64_t)z * M + m0 + t]);
     ep.opa_rowsum[m0 + t] = alpha * r;
   }
 }
@@ -265,10 +325,15 @@ __global__ void k_colsum_final(const float* __restrict__ part, int64_t P, int64_
   out[n] = (beta != 0.f ? beta * out[n] : 0.f) + s;
 }
 
+// Tile choice: 64x64 when that already gives >= 64 blocks, else 32x32.
+static int gemm_tile(int64_t M, int64_t N) { return cdiv(M, 64) * cdiv(N, 64) >= 64 ? 64 : 32; }
+
 static int gemm_splits(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = cdiv(M, GBM) * cdiv(N, GBN);
-  if (tiles >= 128 || K < 256) return 1;
-  int64_t s = std::min<int64_t>(cdiv(256, tiles), K / 128);
+  const int bt = gemm_tile(M, N);
+  const int64_t tiles = cdiv(M, bt) * cdiv(N, bt);
+  const int64_t kreg = (int64_t)GBK * kRegStages;
+  if (tiles >= 128 || K <= kreg) return 1;  // short K: all loads in flight at once, no split needed
+  int64_t s = std::max<int64_t>(cdiv(K, kreg), std::min<int64_t>(cdiv(256, tiles), K / 128));
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 32));
 }
 
@@ -289,7 +354,7 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
                              size_t ws_bytes, void* stream) {
   HVAE_REQUIRE(M >= 0 && N >= 0 && K >= 0 && C, "hvae_gemm_f32: bad shape / null C");
   HVAE_REQUIRE(ldc >= N, "hvae_gemm_f32: ldc < N");
-  HVAE_REQUIRE(M < (1ll << 31) / GBM * GBM && N < (1ll << 31), "hvae_gemm_f32: too large");
+  HVAE_REQUIRE(M < (1ll << 31) / 64 * 64 && N < (1ll << 31), "hvae_gemm_f32: too large");
   if (M == 0 || N == 0) return HVAE_OK;
   HVAE_REQUIRE(K == 0 || (A && B), "hvae_gemm_f32: null A/B");
   HVAE_REQUIRE(trans_a ? lda >= M : lda >= K, "hvae_gemm_f32: bad lda");
@@ -328,7 +393,8 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
   }
   const bool vec_a = (((uintptr_t)A) % 16 == 0) && (lda % 4 == 0);
   const bool vec_b = (((uintptr_t)B) % 16 == 0) && (ldb % 4 == 0);
-  dim3 grid((unsigned)cdiv(N, GBN), (unsigned)cdiv(M, GBM), (unsigned)std::max(splits, 1));
+  const int bt = gemm_tile(M, N);
+  dim3 grid((unsigned)cdiv(N, bt), (unsigned)cdiv(M, bt), (unsigned)std::max(splits, 1));
   float* slab = splits > 1 ? (float*)ws : nullptr;
   unsigned* tickets = nullptr;
   if (slab) {
@@ -337,9 +403,12 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
     if (!tickets) return HVAE_ERR_HIP;
   }
   if (K == 0) kps = 0;
-#define HVAE_GEMM_CALL(TA_, TB_)                                                                  \
-  k_gemm_f32<TA_, TB_><<<grid, 256, 0, st>>>(M, N, K, kps, alpha, A, lda, B, ldb, beta, C, ldc,   \
-                                             slab, tickets, ep, vec_a, vec_b)
+  ProbeScope probe("gemm", st);
+#define HVAE_GEMM_CALL(TA_, TB_)                                                                        \
+  (bt == 64 ? (k_gemm_f32<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(M, N, K, kps, alpha, A, lda, B, ldb, beta, \
+                                                                 C, ldc, slab, tickets, ep, vec_a, vec_b))  \
+            : (k_gemm_f32<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(M, N, K, kps, alpha, A, lda, B, ldb, beta, \
+                                                                 C, ldc, slab, tickets, ep, vec_a, vec_b)))
   if (!trans_a && !trans_b) HVAE_GEMM_CALL(false, false);
   else if (!trans_a && trans_b) HVAE_GEMM_CALL(false, true);
   else if (trans_a && !trans_b) HVAE_GEMM_CALL(true, false);

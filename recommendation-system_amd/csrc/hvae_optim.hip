@@ -42,10 +42,10 @@ __global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
   s = wave_sum_d(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) a.part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+  if (threadIdx.x == 0) st_shared_d(&a.part[blockIdx.x], ((red[0] + red[1]) + red[2]) + red[3]);
   if (!last_block_arrives(a.ticket, gridDim.x)) return;
   double t = 0.0;
-  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) t += __builtin_nontemporal_load(&a.part[i]);
+  for (int i = threadIdx.x; i < (int)gridDim.x; i += 256) t += ld_shared_d(&a.part[i]);
   t = wave_sum_d(t);
   __syncthreads();
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
@@ -177,6 +177,7 @@ static int clip_launch(const float* g_dense, int64_t n_dense, const hvae_rowgrad
   if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   a.max_norm = max_norm; a.norm_out = norm_out; a.coef_out = coef_out;
   a.step = step; a.step_snap = step_snap; a.boff = boff; a.advance = advance;
+  ProbeScope probe("clip", as_stream(stream));
   k_clip_norm<<<kNormBlocks, 256, 0, as_stream(stream)>>>(a);
   HVAE_LAUNCH_CHECK("k_clip_norm");
   return HVAE_OK;
@@ -204,6 +205,7 @@ extern "C" int hvae_adam_dense(const hvae_adam* cfg, float* p, float* m, float* 
   HVAE_REQUIRE(cfg && (n == 0 || (p && m && v && g)), "hvae_adam_dense: bad args");
   if (n == 0) return HVAE_OK;
   const int64_t blocks = std::min<int64_t>(cdiv(n, 256), 4096);
+  ProbeScope probe("adam_dense", as_stream(stream));
   k_adam_dense<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(to_args(cfg), p, m, v, g, n);
   HVAE_LAUNCH_CHECK("k_adam_dense");
   return HVAE_OK;
@@ -218,6 +220,7 @@ extern "C" int hvae_adam_rows(const hvae_adam* cfg, float* p, float* m, float* v
                "hvae_adam_rows: H %% 4 and 16-B alignment required");
   if (N == 0) return HVAE_OK;
   const int64_t blocks = std::min<int64_t>(cdiv(N * H / 4, 256), 8192);
+  ProbeScope probe("adam_rows", as_stream(stream));
   k_adam_rows<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(to_args(cfg), p, m, v, rg->rows, rg->slot_of,
                                                              rg->item_of, rg->n_unique, N, H);
   HVAE_LAUNCH_CHECK("k_adam_rows");

@@ -69,6 +69,8 @@ P = C.POINTER
 SIGNATURES = {
     "hvae_version": (cint, []),
     "hvae_last_error": (cint, [C.c_char_p, sz]),
+    "hvae_probe_arm": (cint, [C.c_char_p, cint]),
+    "hvae_probe_collect": (cint, [C.POINTER(C.c_double), C.POINTER(cint)]),
     "hvae_dense_to_csr": (cint, [vp, i64, i64, vp, vp, vp, i64, vp, sz, vp]),
     "hvae_dense_to_csr_workspace": (sz, [i64, i64]),
     "hvae_encoder_fwd": (cint, [P(CsrBatch), vp, vp, vp, vp, i64, f32, vp, u64, vp, cint, vp, vp, vp, vp]),

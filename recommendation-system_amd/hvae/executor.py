@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -191,7 +192,8 @@ class _StepBuffers:
         for (m_, n_, k_) in gemms:
             need.append(L_.hvae_gemm_f32_workspace(m_, n_, k_))
         self.ws = torch.empty(max(int(max(need)), 256), dtype=torch.uint8, device=dev)
-        self.ws2 = torch.empty_like(self.ws)  # side-stream GEMMs (split-K slabs must not alias the main stream's)
+        # side-stream GEMMs: their split-K slabs must not alias the main stream's
+        self.ws2 = torch.empty_like(self.ws) if ex.two_streams else None
         self.graph = None
 
 
@@ -221,7 +223,11 @@ class FusedTrainer:
         self._adopt_parameters()
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=device)
         self.step_snap = torch.zeros(1, dtype=torch.int64, device=device)  # step before this update (Adam's t - 1)
-        self.side = torch.cuda.Stream(device)
+        # A second stream for the optimizer-only work measured slower on MI355X: every cross-stream
+        # edge of the captured graph costs 5-10 us, more than the short kernels it overlaps. Off by
+        # default; the dependency structure stays in place for the larger configurations.
+        self.two_streams = bool(int(os.environ.get("HVAE_TWO_STREAMS", "0")))
+        self.side = torch.cuda.Stream(device) if self.two_streams else None
         self.boff = torch.zeros(1, dtype=torch.int64, device=device)
         self.norm = torch.zeros(1, device=device)
         self.coef = torch.ones(1, device=device)
@@ -348,6 +354,8 @@ class FusedTrainer:
 
     def _fork(self, src, dst):
         """dst waits for everything enqueued on src so far (a graph edge under capture)."""
+        if src is dst:
+            return
         ev = torch.cuda.Event()
         ev.record(src)
         dst.wait_event(ev)
@@ -364,11 +372,11 @@ class FusedTrainer:
         """
         L_, lay = lib(), self.layout
         main = torch.cuda.current_stream(self.device)
-        side = self.side
+        side = self.side if self.side is not None else main
         st, st2 = main.cuda_stream, side.cuda_stream
         B, H, Lt, d = bf.B, lay.hidden, lay.L, lay.d
         ws, wsn = ptr(bf.ws), bf.ws.numel()
-        ws2 = ptr(bf.ws2)
+        ws2 = ptr(bf.ws2) if side is not main else ws
         seed, step = self.seed, ptr(self.step_dev)
         tr = int(train)
         ext = ext or {}
@@ -386,8 +394,10 @@ class FusedTrainer:
             self._fork(main, side)
             check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st2),
                   "w1_rowgrad_plan")
-            ev_plan = torch.cuda.Event()
-            ev_plan.record(side)
+            ev_plan = None
+            if side is not main:
+                ev_plan = torch.cuda.Event()
+                ev_plan.record(side)
         # ------------------------------------------------------ forward ---
         check(L_.hvae_encoder_fwd(csr_ref, ptr(self.w1t), ptr(self.P["encoder.0.bias"]),
                                   ptr(self.P["encoder.1.weight"]), ptr(self.P["encoder.1.bias"]), H[0], p_drop,
@@ -416,11 +426,9 @@ class FusedTrainer:
             gemm(0, 1, B, d, Lt, ptr(bf.z), Lt, ptr(Wa), Lt, ptr(bf.q), d, epi1)
             epi2 = Epilogue(_lib.EPI_BIAS, ptr(bb), None, None, 0.0, None, 0, None, 0, 0, None)
             gemm(0, 1, B, d, d, ptr(bf.q), d, ptr(Wb), d, ptr(bf.u), d, epi2)
-        self._probe_begin("decoder_fwd")
         check(L_.hvae_decoder_train(self.dec_dtype, ptr(bf.u), d, ptr(self.E_dec), ptr(self.enorm), ptr(self.E32),
                                     csr_ref, d, 1.0 / B, ptr(bf.lse), None, ptr(bf.recon_rows),
                                     ptr(bf.dU) if train else None, ws, wsn, st), "decoder_train")
-        self._probe_end("decoder_fwd")
         accum = self.accum_train if train else self.accum_val
         if not train:
             check(L_.hvae_loss_finalize(ptr(bf.recon_rows), ptr(bf.kl_rows), B, beta, ptr(bf.loss3), ptr(accum), st),
@@ -461,7 +469,8 @@ class FusedTrainer:
                 gemm(1, 0, H[k], H[k - 1], B, ptr(bf.da[k]), H[k], ptr(bf.h[k - 1]), H[k - 1],
                      ptr(G[f"encoder.{i}.weight"]), H[k - 1], side_=True)
                 gemm(0, 0, B, H[k - 1], H[k], ptr(bf.da[k]), H[k], ptr(W), H[k - 1], ptr(bf.dh[k - 1]), H[k - 1])
-        main.wait_event(ev_plan)
+        if ev_plan is not None:
+            main.wait_event(ev_plan)
         check(L_.hvae_w1_rowgrad_apply(ptr(bf.da[0]), H[0], bf.rg.ref, st), "w1_rowgrad_apply")
         self._fork(side, main)  # join: every gradient is complete on the main stream
 
@@ -473,7 +482,8 @@ class FusedTrainer:
         """
         L_, lay = lib(), self.layout
         main = torch.cuda.current_stream(self.device)
-        st, st2 = main.cuda_stream, self.side.cuda_stream
+        side = self.side if self.side is not None else main
+        st, st2 = main.cuda_stream, side.cuda_stream
         H = lay.hidden
         ws, wsn = ptr(bf.ws), bf.ws.numel()
         check(L_.hvae_clip_grad_norm_step(ptr(self.g_small), lay.n_small, rg.ref, H[0], self.max_norm,
@@ -481,29 +491,12 @@ class FusedTrainer:
                                           ptr(self.boff) if advance else None, advance, ws, wsn, st),
               "clip_grad_norm_step")
         cfg = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_snap, self.coef)
-        self._fork(main, self.side)
+        self._fork(main, side)
         check(L_.hvae_adam_dense(C.byref(cfg), ptr(self.small), ptr(self.m_small), ptr(self.v_small),
                                  ptr(self.g_small), lay.n_small, st2), "adam_dense")
-        self._probe_begin("adam_rows")
         check(L_.hvae_adam_rows(C.byref(cfg), ptr(self.w1t), ptr(self.m_w1t), ptr(self.v_w1t), rg.ref,
                                 lay.n_items, H[0], st), "adam_rows")
-        self._probe_end("adam_rows")
-        self._fork(self.side, main)
-
-    # ----------------------------------------------- live kernel timing ---
-    probe: dict | None = None  # {"kernel": name, "events": [(start, end), ...]} (eager steps only)
-
-    def _probe_begin(self, name):
-        if self.probe is not None and self.probe["kernel"] == name:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record(torch.cuda.current_stream(self.device))
-            self.probe["_open"] = ev
-
-    def _probe_end(self, name):
-        if self.probe is not None and self.probe["kernel"] == name:
-            ev = torch.cuda.Event(enable_timing=True)
-            ev.record(torch.cuda.current_stream(self.device))
-            self.probe["events"].append((self.probe.pop("_open"), ev))
+        self._fork(side, main)
 
     def _advance(self, B: int):
         check(lib().hvae_counter_add(ptr(self.boff), B, torch.cuda.current_stream(self.device).cuda_stream),

@@ -1,0 +1,79 @@
+"""Per-shape timing of libhvae's fp32 GEMM on the shapes of one All_Beauty train step.
+
+    python scripts/bench_gemm.py [--reps 200]
+
+Each shape is launched eagerly `reps` times; the library's probe brackets every
+launch with a hipEvent pair on its stream. torch.mm (hipBLASLt/rocBLAS) on the
+same shapes is timed beside it for scale.
+"""
+import argparse
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "recommendation-system_amd")]
+
+import torch  # noqa: E402
+
+from hvae import _lib, ops  # noqa: E402
+from hvae._lib import check, lib  # noqa: E402
+
+B, H, L, D = 64, 512, 128, 384
+# (name, M, N, K, trans_a, trans_b) -- nn.Linear forward is NT, data grads NN, weight grads TN
+SHAPES = [
+    ("fwd_heads", B, 2 * L, H, False, True),
+    ("fwd_proj_a", B, D, L, False, True),
+    ("fwd_proj_b", B, D, D, False, True),
+    ("bwd_dWb", D, D, B, True, False),
+    ("bwd_dp1", B, D, D, False, False),
+    ("bwd_dWa", D, L, B, True, False),
+    ("bwd_dz", B, L, D, False, False),
+    ("bwd_dWh", 2 * L, H, B, True, False),
+    ("bwd_dh", B, H, 2 * L, False, False),
+]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=200)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cpu").manual_seed(0)
+    out = {}
+    for name, M, N, K, ta, tb in SHAPES:
+        a = torch.randn(K, M, generator=g).to(dev).t() if ta else torch.randn(M, K, generator=g).to(dev)
+        b = torch.randn(N, K, generator=g).to(dev).t() if tb else torch.randn(K, N, generator=g).to(dev)
+        rs = torch.empty(M, device=dev)
+        epi = ops.epilogue(_lib.EPI_NONE, opa_rowsum=rs) if ta else None
+        c = torch.empty(M, N, device=dev)
+        for _ in range(10):
+            ops.gemm(a, b, out=c, epi=epi)
+        torch.cuda.synchronize()
+        check(lib().hvae_probe_arm(b"gemm", args.reps), "arm")
+        for _ in range(args.reps):
+            ops.gemm(a, b, out=c, epi=epi)
+        torch.cuda.synchronize()
+        avg, n = C.c_double(), C.c_int()
+        check(lib().hvae_probe_collect(C.byref(avg), C.byref(n)), "collect")
+        check(lib().hvae_probe_arm(None, 0), "disarm")
+        ref = a.double() @ b.double()
+        err = float((c.double() - ref).abs().max() / ref.abs().max())
+        # torch.mm for scale
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(10):
+            torch.mm(a, b, out=c)
+        torch.cuda.synchronize()
+        s.record()
+        for _ in range(args.reps):
+            torch.mm(a, b, out=c)
+        e.record()
+        torch.cuda.synchronize()
+        out[name] = {"M": M, "N": N, "K": K, "hvae_us": round(avg.value, 2), "torch_mm_us": round(
+            s.elapsed_time(e) * 1e3 / args.reps, 2), "rel_err": err}
+        print(json.dumps({name: out[name]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
