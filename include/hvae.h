@@ -131,7 +131,13 @@ typedef struct hvae_rowgrad {
   int32_t* n_unique;    /* [1] device                                           */
   int64_t cap;          /* >= nnz of any batch                                  */
   int64_t n_items;      /* N                                                    */
+  int32_t* contrib_slot;/* [cap] slot of each (sorted) contribution             */
+  float* part;          /* [part_floats] scratch of the chunked row gather      */
+  int64_t part_floats;  /* >= hvae_rowgrad_part_floats(cap, H)                  */
 } hvae_rowgrad;
+/* Scratch the row gather needs for hidden width H (chunk partials, and the
+ * staging copy of the long-segment sort). */
+int64_t hvae_rowgrad_part_floats(int64_t cap, int64_t H);
 int hvae_w1_rowgrad(const hvae_csr_batch* x, const float* da, int64_t H, const hvae_rowgrad* rg,
                     void* ws, size_t ws_bytes, void* stream);
 size_t hvae_w1_rowgrad_workspace(int64_t n_items);
@@ -159,7 +165,10 @@ enum {
   HVAE_EPI_BIAS = 1,           /* + bias[n]                                        */
   HVAE_EPI_BIAS_GELU_DROP = 2, /* pre = acc + bias -> pre_out; C = Drop(GELU(pre)) */
   HVAE_EPI_GELU_DROP_BWD = 3,  /* C = acc * dropmult * GELU'(pre_in)               */
-  HVAE_EPI_DROP_BWD = 4        /* C = acc * dropmult                               */
+  HVAE_EPI_DROP_BWD = 4,       /* C = acc * dropmult                               */
+  HVAE_EPI_REPARAM_BWD = 5     /* acc = dz; pre_in = heads [M, ldc] (mu | logvar at */
+                               /* col n | N + n); writes C[:, n] = dmu and          */
+                               /* C[:, N + n] = dlogvar (hvae_reparam_kl_bwd's math) */
 };
 typedef struct hvae_epilogue {
   int kind;
@@ -175,6 +184,8 @@ typedef struct hvae_epilogue {
   float* opa_rowsum;      /* [M] or NULL: sum_k op(A)[m, k] (x alpha), computed from */
                           /* the A tiles the GEMM already stages: the bias gradient */
                           /* of a Linear alongside its weight gradient dY^T X       */
+  const float* aux;       /* REPARAM_BWD: eps [M, N]                                */
+  float aux_scale;        /* REPARAM_BWD: KL gradient scale beta / B               */
 } hvae_epilogue;
 int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
                   const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
@@ -222,10 +233,13 @@ int hvae_row_norm_max(int dtype, const void* E, int64_t N, int64_t D, float* out
 /* The train-step form: the streaming sweep above plus, in the same finalize
  * launch (one block per user, after the split merge), the sparse half of the
  * loss and of d(u) against the fp32 E32 (see hvae_decoder_bwd). nb = x->nb,
- * N = x->n_items. O may be NULL (kept internal); dU NULL => loss only. */
+ * N = x->n_items. O may be NULL (kept internal); dU NULL => loss only.
+ * If loss3 != NULL the last finalize block also does hvae_loss_finalize
+ * (recon_rows, kl_rows, beta -> loss3, accum3) with the same arithmetic. */
 int hvae_decoder_train(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                        const float* E32, const hvae_csr_batch* x, int64_t D, float grad_scale, float* lse,
-                       float* O, float* recon_rows, float* dU, void* ws, size_t ws_bytes, void* stream);
+                       float* O, float* recon_rows, float* dU, const float* kl_rows, float beta, float* loss3,
+                       double* accum3, void* ws, size_t ws_bytes, void* stream);
 /* Sparse half of the loss and of d(u), in fp32 against the fp32 E:
  *   recon_rows[b] = n_b * lse[b] - sum_{j in row b} x_bj (u_b . E_j),  n_b = sum_j x_bj
  *   dU[b,:]       = grad_scale * (n_b * O[b,:] - sum_{j in row b} x_bj E_j)
@@ -282,6 +296,11 @@ int hvae_adam_dense(const hvae_adam* cfg, float* p, float* m, float* v, const fl
  * untouched rows get g = 0 (their moments still decay, as in torch). */
 int hvae_adam_rows(const hvae_adam* cfg, float* p, float* m, float* v, const hvae_rowgrad* rg,
                    int64_t N, int64_t H, void* stream);
+/* Both Adam updates of one train step in one launch over the flat parameter
+ * buffer: p[0 : N*H] (item-major W1t, row-sparse gradient rg) and
+ * p[dense_off : dense_off + n_dense] (dense gradient g_dense). */
+int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v, const hvae_rowgrad* rg, int64_t N,
+                   int64_t H, const float* g_dense, int64_t dense_off, int64_t n_dense, void* stream);
 /* *counter += delta (device-side step/batch counters for graph replay). */
 int hvae_counter_add(int64_t* counter, int64_t delta, void* stream);
 /* *a += da and, if b != NULL, *b += db, in one launch (end of a train step). */

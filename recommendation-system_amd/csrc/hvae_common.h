@@ -232,4 +232,33 @@ __device__ __host__ __forceinline__ float bf2f(bf16_t h) {
   return f;
 }
 
+// Batch means of the loss rows in fp64, the step's (total, recon, kl) and the
+// epoch accumulators -- vae_loss_function's reductions (src/ml/model.py:283-292).
+// One 256-thread block; shared by k_loss_finalize and the decoder finalize's last
+// block (which reads recon rows other blocks just wrote, hence `coherent`).
+__device__ __forceinline__ void loss_block_reduce(const float* recon_rows, bool coherent, const float* kl_rows,
+                                                  int64_t nb, float beta, float* out3, double* accum3) {
+  __shared__ double lred[2][4];
+  double r = 0.0, k = 0.0;
+  for (int64_t i = threadIdx.x; i < nb; i += 256) {
+    r += (double)(coherent ? ld_shared_f(&recon_rows[i]) : recon_rows[i]);
+    k += (double)kl_rows[i];
+  }
+  r = wave_sum_d(r);
+  k = wave_sum_d(k);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) { lred[0][w] = r; lred[1][w] = k; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double rs = ((lred[0][0] + lred[0][1]) + lred[0][2]) + lred[0][3];
+    const double ks = ((lred[1][0] + lred[1][1]) + lred[1][2]) + lred[1][3];
+    const float recon = (float)(rs / (double)nb), kl = (float)(ks / (double)nb);
+    const float total = recon + beta * kl;
+    out3[0] = total; out3[1] = recon; out3[2] = kl;
+    if (accum3) {
+      accum3[0] += (double)total; accum3[1] += (double)recon; accum3[2] += (double)kl;
+    }
+  }
+}
+
 }  // namespace hvae

@@ -79,6 +79,17 @@ __device__ __forceinline__ int bf_off(int row, int chunk) {
 
 template <int D>
 constexpr int bf_tile_bytes() { return ((D + 127) / 128) * 8192; }
+// LDS ring depth: as many E tiles in flight as fit in ~100 KB (the sweep at small
+// batches has few tiles per block, so HBM latency, not MFMA, sets its pace)
+template <int D>
+constexpr int bf_stages() { return bf_tile_bytes<D>() <= 24 * 1024 ? 4 : 3; }
+
+// s_waitcnt vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
+template <int n>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(n >= 0 && n < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14));
+}
 
 template <int D, bool WITH_O>
 __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, int64_t ldu,
@@ -151,13 +162,23 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
     }
   };
 
+  // NS-deep ring: tiles t+1 .. t+NS-1 are in flight while tile t is consumed. One
+  // barrier per tile: after it, tile t has landed for every wave (each waited for its
+  // own LDS-DMA pieces with vmcnt) and every wave is done with tile t-1, whose slot
+  // then takes tile t+NS-1.
+  // Past the end of the range the ring re-reads the last tile into the free slot, so
+  // that exactly NS-2 younger tiles are always in flight and the wait is one constant.
+  constexpr int NS = bf_stages<D>();
   if (t_beg < t_end) {
-    issue_tile(t_beg, lds);
-    __syncthreads();  // vmcnt(0) + barrier: tile t_beg has landed
+#pragma unroll
+    for (int i = 0; i < NS - 1; ++i) issue_tile(min(t_beg + i, t_end - 1), lds + i * TB);
   }
   int cur = 0;
   for (int64_t t = t_beg; t < t_end; ++t) {
-    if (t + 1 < t_end) issue_tile(t + 1, lds + (cur ^ 1) * TB);
+    wait_vmcnt<(NS - 2) * PIECES_PER_WAVE>();
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    issue_tile(min(t + NS - 1, t_end - 1), lds + (cur == 0 ? NS - 1 : cur - 1) * TB);
     const unsigned char* buf = lds + cur * TB;
     if (wave_active) {
       // ---- GEMM1: S^T[32 items][32 users] = E_tile U^T, A reads one group ahead
@@ -233,8 +254,7 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
         }
       }
     }
-    __syncthreads();  // next tile landed (vmcnt(0)), this tile's reads done
-    cur ^= 1;
+    cur = cur == NS - 1 ? 0 : cur + 1;
   }
 
   if (!wave_active) return;
@@ -446,6 +466,7 @@ struct FinArgs {
   const int32_t* rows; const int64_t* rows_offset;    // CSR batch (nullable row_ptr => no sparse terms)
   float scale;
   float* lse_out; float* O_out; float* recon_rows; float* dU;
+  const float* kl_rows; float beta; float* loss3; double* accum3; unsigned* ticket;  // fused loss (optional)
 };
 
 __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
@@ -553,7 +574,10 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     if (d < D) dot += a.U[b * a.ldu + d] * acc[k];
   }
   dot = block_sum<256>(dot, red);
-  if (a.recon_rows && tid == 0) a.recon_rows[b] = n * lse_b - dot;
+  if (a.recon_rows && tid == 0) {
+    if (a.loss3) st_shared_f(&a.recon_rows[b], n * lse_b - dot);
+    else a.recon_rows[b] = n * lse_b - dot;
+  }
   if (a.dU) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -561,6 +585,8 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
       if (d < D) a.dU[b * D + d] = a.scale * (n * o[k] - acc[k]);
     }
   }
+  if (a.loss3 && last_block_arrives(a.ticket, gridDim.x))
+    loss_block_reduce(a.recon_rows, true, a.kl_rows, a.nb, a.beta, a.loss3, a.accum3);
 }
 
 // Exact recompute of one user flagged by k_dec_bf16 (its max score sits more
@@ -665,7 +691,7 @@ static size_t dec_ws_bytes(int splits, int64_t nb, int64_t D) {
 template <int D, bool WO>
 static int launch_bf16(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                        const DecPlan& p, DecOut o, hipStream_t st) {
-  constexpr int lds = 2 * bf_tile_bytes<D>();
+  constexpr int lds = bf_stages<D>() * bf_tile_bytes<D>();
   static bool attr_set = false;
   if (!attr_set) {
     HVAE_HIP(hipFuncSetAttribute((const void*)k_dec_bf16<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -746,8 +772,8 @@ extern "C" size_t hvae_decoder_workspace(int dtype, int64_t nb, int64_t N, int64
 // flash sweep + finalize; csr / recon_rows / dU optional
 static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                        const float* E32, const hvae_csr_batch* x, int64_t nb, int64_t N, int64_t D, float scale,
-                       float* lse, float* O, float* recon_rows, float* dU, void* ws, size_t ws_bytes,
-                       hipStream_t st) {
+                       float* lse, float* O, float* recon_rows, float* dU, const float* kl_rows, float beta,
+                       float* loss3, double* accum3, void* ws, size_t ws_bytes, hipStream_t st) {
   HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32, "hvae decoder: bad dtype");
   HVAE_REQUIRE(U && E && lse && N > 0 && D > 0 && ldu >= D, "hvae decoder: bad args");
   HVAE_REQUIRE(dtype != HVAE_BF16 || e_maxnorm, "hvae decoder: bf16 needs e_maxnorm");
@@ -796,6 +822,7 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   }
   if (rc) return rc;
   if (p.splits == 1 && !bf && !x) return HVAE_OK;  // fp32 single split: the sweep wrote lse / O already
+  HVAE_REQUIRE(!loss3 || x, "hvae decoder: fused loss needs the batch");
   FinArgs a{};
   a.splits = p.splits;
   if (p.splits > 1) { a.pm = o.m; a.pl = o.l; a.pO = want_o ? o.O : nullptr; }
@@ -812,6 +839,11 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   a.O_out = O ? O : (p.splits == 1 ? o_scratch : nullptr);
   a.recon_rows = recon_rows;
   a.dU = dU;
+  if (loss3) {
+    HVAE_REQUIRE(x && recon_rows && kl_rows, "hvae_decoder_train: fused loss needs recon_rows and kl_rows");
+    a.kl_rows = kl_rows; a.beta = beta; a.loss3 = loss3; a.accum3 = accum3;
+    if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
+  }
   ProbeScope probe("decoder_finalize", st);
   k_dec_finalize<<<(unsigned)nb, 256, 0, st>>>(a);
   HVAE_LAUNCH_CHECK("k_dec_finalize");
@@ -821,17 +853,18 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
 extern "C" int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                                 int64_t nb, int64_t N, int64_t D, float* lse, float* O, void* ws,
                                 size_t ws_bytes, void* stream) {
-  return decoder_run(dtype, U, ldu, E, e_maxnorm, nullptr, nullptr, nb, N, D, 0.f, lse, O, nullptr, nullptr, ws,
-                     ws_bytes, as_stream(stream));
+  return decoder_run(dtype, U, ldu, E, e_maxnorm, nullptr, nullptr, nb, N, D, 0.f, lse, O, nullptr, nullptr,
+                     nullptr, 0.f, nullptr, nullptr, ws, ws_bytes, as_stream(stream));
 }
 
 extern "C" int hvae_decoder_train(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                                   const float* E32, const hvae_csr_batch* x, int64_t D, float grad_scale,
-                                  float* lse, float* O, float* recon_rows, float* dU, void* ws, size_t ws_bytes,
+                                  float* lse, float* O, float* recon_rows, float* dU, const float* kl_rows,
+                                  float beta, float* loss3, double* accum3, void* ws, size_t ws_bytes,
                                   void* stream) {
   HVAE_REQUIRE(x && recon_rows, "hvae_decoder_train: needs the CSR batch and recon_rows");
   return decoder_run(dtype, U, ldu, E, e_maxnorm, E32, x, x->nb, x->n_items, D, grad_scale, lse, O, recon_rows, dU,
-                     ws, ws_bytes, as_stream(stream));
+                     kl_rows, beta, loss3, accum3, ws, ws_bytes, as_stream(stream));
 }
 
 extern "C" int hvae_decoder_bwd(const hvae_csr_batch* x, const float* U, int64_t ldu, const float* E32,

@@ -262,17 +262,34 @@ __global__ void __launch_bounds__(256) k_ln_gelu_drop_bwd(
   }
 }
 
-// Sum the per-block partials [nparts][3][H] -> (d_ln_w, d_ln_b, d_bias), fixed order.
-__global__ void k_ln_part_reduce(const float* __restrict__ part, int64_t nparts, int64_t H,
-                                 float* __restrict__ d_ln_w, float* __restrict__ d_ln_b,
-                                 float* __restrict__ d_bias) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 3 * H) return;
+// Sum the per-block partials [nparts][3][H] -> (d_ln_w, d_ln_b, d_bias), fixed order:
+// 64 columns per block, 4 groups of partials (p = g mod 4) per column, loads batched
+// 8 deep, the groups combined in order through LDS.
+__global__ void __launch_bounds__(256) k_ln_part_reduce(const float* __restrict__ part, int64_t nparts, int64_t H,
+                                                        float* __restrict__ d_ln_w, float* __restrict__ d_ln_b,
+                                                        float* __restrict__ d_bias) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int64_t p = 0; p < nparts; ++p) s += part[p * 3 * H + i];
-  if (i < H) d_ln_w[i] = s;
-  else if (i < 2 * H) d_ln_b[i - H] = s;
-  else if (d_bias) d_bias[i - 2 * H] = s;
+  if (i < 3 * H) {
+    int64_t p = g;
+    for (; p + 28 < nparts; p += 32) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = part[(p + 4 * j) * 3 * H + i];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; p < nparts; p += 4) s += part[p * 3 * H + i];
+  }
+  red[g][cl] = s;
+  __syncthreads();
+  if (g != 0 || i >= 3 * H) return;
+  const float t = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+  if (i < H) d_ln_w[i] = t;
+  else if (i < 2 * H) d_ln_b[i - H] = t;
+  else if (d_bias) d_bias[i - 2 * H] = t;
 }
 
 // --------------------------------------------------------------------------
@@ -552,22 +569,32 @@ __global__ void __launch_bounds__(256) k_rg_scatter(const int64_t* __restrict__ 
 }
 
 // Sort every item segment's contributions by batch row (keys are unique within
-// a segment: a CSR row holds an item at most once), in place, and re-zero the
-// fill counters. Segments of <= 64: one wave, bitonic network in registers;
-// 64 < len <= kSegSortCap: one block, bitonic in LDS. Longer segments stay
-// unsorted; k_rg_apply sums those in key order by selection instead.
+// a segment: a CSR row holds an item at most once), in place; record each
+// contribution's slot; re-zero the fill counters.
+//   len <= 64          one wave, bitonic network in registers
+//   len > 64, nb <= kRankRows   one block: rank = popcount of a batch-row bitmap
+//                      below the key (O(len + nb/32)), via a staging copy in `stage`
+//   otherwise          one block, bitonic in LDS (len <= kSegSortCap) or an
+//                      in-place selection sort (never met at the path's batch sizes)
 constexpr int kSegSortCap = 4096;
+constexpr int kRankRows = 32768;
 __global__ void __launch_bounds__(256) k_rg_sort(const int32_t* __restrict__ n_unique,
                                                  const int32_t* __restrict__ seg_off, int32_t* __restrict__ fill,
-                                                 int32_t* __restrict__ contrib_row, float* __restrict__ contrib_val) {
+                                                 int32_t* __restrict__ contrib_row, float* __restrict__ contrib_val,
+                                                 int32_t* __restrict__ contrib_slot, int2* __restrict__ stage,
+                                                 int64_t nb) {
   __shared__ int key[kSegSortCap];
   __shared__ float kval[kSegSortCap];
+  __shared__ unsigned bm[kRankRows / 32];
+  __shared__ int pre[kRankRows / 32];
+  __shared__ int red[8];
   const int nu = *n_unique;
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
   for (int s = gw; s < nu; s += nw) {
     const int beg = seg_off[s], len = seg_off[s + 1] - beg;
     if (lane == 0) fill[s] = 0;
+    for (int i = lane; i < len; i += 64) contrib_slot[beg + i] = s;
     if (len <= 1 || len > 64) continue;
     int k_ = lane < len ? contrib_row[beg + lane] : 0x7fffffff;
     float v_ = lane < len ? contrib_val[beg + lane] : 0.f;
@@ -582,90 +609,191 @@ __global__ void __launch_bounds__(256) k_rg_sort(const int32_t* __restrict__ n_u
       }
     if (lane < len) { contrib_row[beg + lane] = k_; contrib_val[beg + lane] = v_; }
   }
+  const int words = (int)((nb + 31) / 32);
   for (int s = blockIdx.x; s < nu; s += gridDim.x) {
     const int beg = seg_off[s], len = seg_off[s + 1] - beg;
-    if (len <= 64 || len > kSegSortCap) continue;  // block-uniform
-    int p2 = 128;
-    while (p2 < len) p2 <<= 1;
+    if (len <= 64) continue;  // block-uniform
     __syncthreads();
-    for (int i = threadIdx.x; i < p2; i += 256) {
-      key[i] = (i < len) ? contrib_row[beg + i] : 0x7fffffff;
-      kval[i] = (i < len) ? contrib_val[beg + i] : 0.f;
-    }
-    __syncthreads();
-    for (int k = 2; k <= p2; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = threadIdx.x; i < p2; i += 256) {
-          const int ixj = i ^ j;
-          if (ixj > i) {
-            const bool up = (i & k) == 0;
-            const int a = key[i], c = key[ixj];
-            if ((a > c) == up) {
-              key[i] = c; key[ixj] = a;
-              const float t = kval[i]; kval[i] = kval[ixj]; kval[ixj] = t;
+    if (nb <= kRankRows) {
+      for (int w = threadIdx.x; w < words; w += 256) bm[w] = 0u;
+      __syncthreads();
+      for (int i = threadIdx.x; i < len; i += 256) {
+        const int b = contrib_row[beg + i];
+        stage[beg + i] = make_int2(b, __float_as_int(contrib_val[beg + i]));
+        atomicOr(&bm[b >> 5], 1u << (b & 31));
+      }
+      __syncthreads();
+      // exclusive prefix of the word popcounts (each thread owns a run of consecutive words)
+      const int per = (words + 255) / 256;
+      const int w0 = threadIdx.x * per;
+      int c = 0;
+      for (int w = w0; w < min(words, w0 + per); ++w) c += __popc(bm[w]);
+      int incl = c;  // inclusive scan over the block
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      if (lane == 63) red[threadIdx.x >> 6] = incl;
+      __syncthreads();
+      int wbase = 0;
+      for (int q = 0; q < (threadIdx.x >> 6); ++q) wbase += red[q];
+      int run = wbase + incl - c;
+      for (int w = w0; w < min(words, w0 + per); ++w) { pre[w] = run; run += __popc(bm[w]); }
+      __syncthreads();
+      for (int i = threadIdx.x; i < len; i += 256) {
+        const int2 e = stage[beg + i];
+        const int b = e.x;
+        const int rank = pre[b >> 5] + __popc(bm[b >> 5] & ((1u << (b & 31)) - 1u));
+        contrib_row[beg + rank] = b;
+        contrib_val[beg + rank] = __int_as_float(e.y);
+      }
+    } else if (len <= kSegSortCap) {
+      int p2 = 128;
+      while (p2 < len) p2 <<= 1;
+      for (int i = threadIdx.x; i < p2; i += 256) {
+        key[i] = (i < len) ? contrib_row[beg + i] : 0x7fffffff;
+        kval[i] = (i < len) ? contrib_val[beg + i] : 0.f;
+      }
+      __syncthreads();
+      for (int k = 2; k <= p2; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+          for (int i = threadIdx.x; i < p2; i += 256) {
+            const int ixj = i ^ j;
+            if (ixj > i) {
+              const bool up = (i & k) == 0;
+              const int a = key[i], c = key[ixj];
+              if ((a > c) == up) {
+                key[i] = c; key[ixj] = a;
+                const float t = kval[i]; kval[i] = kval[ixj]; kval[ixj] = t;
+              }
             }
           }
+          __syncthreads();
+        }
+      }
+      for (int i = threadIdx.x; i < len; i += 256) { contrib_row[beg + i] = key[i]; contrib_val[beg + i] = kval[i]; }
+    } else {
+      for (int i = 0; i < len - 1; ++i) {  // selection sort, one block
+        int best = 0x7fffffff, at = -1;
+        for (int j = i + threadIdx.x; j < len; j += 256) {
+          const int k = contrib_row[beg + j];
+          if (k < best) { best = k; at = j; }
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+          const int ob = __shfl_xor(best, o), oa = __shfl_xor(at, o);
+          if (ob < best) { best = ob; at = oa; }
+        }
+        __syncthreads();
+        if (lane == 0) { key[threadIdx.x >> 6] = best; key[4 + (threadIdx.x >> 6)] = at; }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+          int bb = key[0], ba = key[4];
+          for (int q = 1; q < 4; ++q)
+            if (key[q] < bb) { bb = key[q]; ba = key[4 + q]; }
+          const float tv = contrib_val[beg + ba];
+          contrib_row[beg + ba] = contrib_row[beg + i];
+          contrib_val[beg + ba] = contrib_val[beg + i];
+          contrib_row[beg + i] = bb;
+          contrib_val[beg + i] = tv;
         }
         __syncthreads();
       }
     }
-    for (int i = threadIdx.x; i < len; i += 256) { contrib_row[beg + i] = key[i]; contrib_val[beg + i] = kval[i]; }
   }
 }
 
-// One wave per item segment: rows[s, :] = sum over the segment (ascending batch
-// row) of x * da[b, :]. Each lane owns 4 consecutive columns per 256-column pass.
+// Row gather rows[s, :] = sum over segment s (ascending batch row) of x * da[b, :],
+// over the sorted contribution list in chunks of CH (8..64, sized so that the
+// chunks give ~2K waves): one wave per chunk, lane i
+// holds contribution i of the chunk, NV float4 columns per lane. A run of one
+// segment that is the whole segment is written to its row; a run cut by a chunk
+// edge goes to the chunk's head (run starts the chunk) or tail partial, and
+// k_rg_span adds those up in chunk order. Loads are batched 8 contributions deep.
+template <int NV>
 __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_unique,
                                                   const int32_t* __restrict__ seg_off,
                                                   const int32_t* __restrict__ contrib_row,
                                                   const float* __restrict__ contrib_val,
-                                                  const float* __restrict__ da, int64_t H,
-                                                  float* __restrict__ out_rows) {
+                                                  const int32_t* __restrict__ contrib_slot,
+                                                  const float* __restrict__ da, int64_t H, int CH,
+                                                  float* __restrict__ out_rows, float* __restrict__ part) {
+  const int nu = *n_unique;
+  const int total = seg_off[nu];
+  const int nchunks = (total + CH - 1) / CH;
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (int c = gw; c < nchunks; c += nw) {
+    const int c0 = c * CH, n = min(CH, total - c0);
+    const int mb = lane < n ? contrib_row[c0 + lane] : 0;
+    const float mx = lane < n ? contrib_val[c0 + lane] : 0.f;
+    const int ms = lane < n ? contrib_slot[c0 + lane] : -1;
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int run_lo = 0;
+    for (int i0 = 0; i0 < n; i0 += 8) {
+      float4 d[8][NV];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int b = __shfl(mb, i0 + j);
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          const int64_t col = 4 * (int64_t)(lane + 64 * k);
+          d[j][k] = (i0 + j < n && col < H) ? *reinterpret_cast<const float4*>(da + (int64_t)b * H + col)
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int i = i0 + j;
+        if (i >= n) break;
+        const float x = __shfl(mx, i);
+        const int si = __shfl(ms, i);
+        const int snext = __shfl(ms, min(i + 1, 63));
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          acc[k].x += x * d[j][k].x; acc[k].y += x * d[j][k].y;
+          acc[k].z += x * d[j][k].z; acc[k].w += x * d[j][k].w;
+        }
+        if (i == n - 1 || snext != si) {  // end of a run (wave-uniform)
+          const int lo = c0 + run_lo, hi = c0 + i + 1;
+          float* dst;
+          if (lo == seg_off[si] && hi == seg_off[si + 1]) dst = out_rows + (int64_t)si * H;
+          else if (run_lo == 0) dst = part + (int64_t)(2 * c) * H;
+          else dst = part + (int64_t)(2 * c + 1) * H;
+#pragma unroll
+          for (int k = 0; k < NV; ++k) {
+            const int64_t col = 4 * (int64_t)(lane + 64 * k);
+            if (col < H) *reinterpret_cast<float4*>(dst + col) = acc[k];
+            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          run_lo = i + 1;
+        }
+      }
+    }
+  }
+}
+
+// Segments cut by chunk edges: first chunk's partial (head if the segment starts the
+// chunk, else tail) + the head partials of the following chunks, in chunk order.
+__global__ void __launch_bounds__(256) k_rg_span(const int32_t* __restrict__ n_unique,
+                                                 const int32_t* __restrict__ seg_off, int64_t H, int CH,
+                                                 const float* __restrict__ part, float* __restrict__ out_rows) {
   const int nu = *n_unique;
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
   for (int s = gw; s < nu; s += nw) {
-    const int beg = seg_off[s], len = seg_off[s + 1] - beg;
-    for (int64_t c0 = 0; c0 < H; c0 += 256) {
-      const int64_t c = c0 + 4 * lane;
-      const bool on = c < H;
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (len <= kSegSortCap) {
-        for (int i0 = 0; i0 < len; i0 += 64) {
-          const int n = min(64, len - i0);
-          const int mb = lane < n ? contrib_row[beg + i0 + lane] : 0;
-          const float mx = lane < n ? contrib_val[beg + i0 + lane] : 0.f;
-          for (int i = 0; i < n; ++i) {
-            const int b = __shfl(mb, i);
-            const float x = __shfl(mx, i);
-            if (on) {
-              const float4 d = *reinterpret_cast<const float4*>(da + (int64_t)b * H + c);
-              acc.x += x * d.x; acc.y += x * d.y; acc.z += x * d.z; acc.w += x * d.w;
-            }
-          }
-        }
-      } else {  // unsorted long segment: visit contributions in ascending key order
-        int prev = -1;
-        for (int it = 0; it < len; ++it) {
-          int best = 0x7fffffff;
-          float bx = 0.f;
-          for (int i = lane; i < len; i += 64) {
-            const int k = contrib_row[beg + i];
-            if (k > prev && k < best) { best = k; bx = contrib_val[beg + i]; }
-          }
-          for (int o = 32; o > 0; o >>= 1) {
-            const int ok = __shfl_xor(best, o);
-            const float ox = __shfl_xor(bx, o);
-            if (ok < best) { best = ok; bx = ox; }
-          }
-          prev = best;
-          if (on) {
-            const float4 d = *reinterpret_cast<const float4*>(da + (int64_t)best * H + c);
-            acc.x += bx * d.x; acc.y += bx * d.y; acc.z += bx * d.z; acc.w += bx * d.w;
-          }
-        }
+    const int beg = seg_off[s], end = seg_off[s + 1];
+    const int ca = beg / CH, cb = (end - 1) / CH;
+    if (ca == cb) continue;
+    const float* first = part + (int64_t)(2 * ca + (beg % CH == 0 ? 0 : 1)) * H;
+    for (int64_t col = 4 * lane; col < H; col += 256) {
+      float4 acc = *reinterpret_cast<const float4*>(first + col);
+      for (int c = ca + 1; c <= cb; ++c) {
+        const float4 p = *reinterpret_cast<const float4*>(part + (int64_t)(2 * c) * H + col);
+        acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
       }
-      if (on) *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + c) = acc;
+      *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + col) = acc;
     }
   }
 }
@@ -774,7 +902,7 @@ extern "C" int hvae_ln_gelu_drop_bwd(const float* dh, const float* xhat, const f
                           d_bias)));
   HVAE_LAUNCH_CHECK("k_ln_gelu_drop_bwd");
   if (!ticket) {
-    k_ln_part_reduce<<<(unsigned)cdiv(3 * H, 256), 256, 0, as_stream(stream)>>>((const float*)ws, nparts,
+    k_ln_part_reduce<<<(unsigned)cdiv(3 * H, 64), 256, 0, as_stream(stream)>>>((const float*)ws, nparts,
                                                                                  H, d_ln_w, d_ln_b, d_bias);
     HVAE_LAUNCH_CHECK("k_ln_part_reduce");
   }
@@ -852,19 +980,39 @@ extern "C" int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad*
                                       rg->seg_off, rg->fill, rg->contrib_row, rg->contrib_val,
                                       rg->cap);
   HVAE_LAUNCH_CHECK("k_rg_scatter");
-  k_rg_sort<<<rg_grid(rg), 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->fill, rg->contrib_row, rg->contrib_val);
+  HVAE_REQUIRE(rg->part && rg->part_floats >= 2 * rg->cap, "hvae_w1_rowgrad_plan: part scratch too small");
+  k_rg_sort<<<rg_grid(rg), 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->fill, rg->contrib_row, rg->contrib_val,
+                                         rg->contrib_slot, (int2*)rg->part, x->nb);
   HVAE_LAUNCH_CHECK("k_rg_sort");
   return HVAE_OK;
+}
+
+static int rg_chunk(int64_t cap) {
+  int ch = 8;
+  while (ch < 64 && cap / ch > 2048) ch *= 2;
+  return ch;
+}
+
+extern "C" int64_t hvae_rowgrad_part_floats(int64_t cap, int64_t H) {
+  return std::max<int64_t>(2 * (cap / rg_chunk(cap) + 1) * H, 2 * cap);
 }
 
 extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowgrad* rg, void* stream) {
   HVAE_REQUIRE(da, "hvae_w1_rowgrad_apply: null da");
   if (int rc = rg_check(rg)) return rc;
   if (int rc = check_hidden(H)) return rc;
-  ProbeScope probe("rowgrad_apply", as_stream(stream));
-  k_rg_apply<<<rg_grid(rg), 256, 0, as_stream(stream)>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
-                                                           rg->contrib_val, da, H, rg->rows);
+  HVAE_REQUIRE(rg->contrib_slot && rg->part && rg->part_floats >= hvae_rowgrad_part_floats(rg->cap, H),
+               "hvae_w1_rowgrad_apply: part scratch too small for H");
+  hipStream_t st = as_stream(stream);
+  const int ch = rg_chunk(rg->cap);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(rg->cap, ch), 4), 4096));
+  ProbeScope probe("rowgrad_apply", st);
+  HVAE_NV_DISPATCH(H, (k_rg_apply<NV><<<grid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
+                                                            rg->contrib_val, rg->contrib_slot, da, H, ch, rg->rows,
+                                                            rg->part)));
   HVAE_LAUNCH_CHECK("k_rg_apply");
+  k_rg_span<<<rg_grid(rg), 256, 0, st>>>(rg->n_unique, rg->seg_off, H, ch, rg->part, rg->rows);
+  HVAE_LAUNCH_CHECK("k_rg_span");
   return HVAE_OK;
 }
 

@@ -48,11 +48,19 @@ struct EpiArgs {
   uint32_t tag;
   int train;
   float* opa_rowsum;  // [M]: sum_k op(A)[m, k] (bias gradient alongside dY^T X)
+  const float* aux;   // REPARAM_BWD: eps [M, N]
+  float aux_scale;    // REPARAM_BWD: beta / B
 };
 
 __device__ __forceinline__ float epi_apply(const EpiArgs& ep, int64_t step, int64_t row, int64_t col,
-                                           int64_t N, int64_t ldc, float c) {
+                                           int64_t N, int64_t ldc, float c, float* __restrict__ C) {
   switch (ep.kind) {
+    case HVAE_EPI_REPARAM_BWD: {  // c = dz; same arithmetic as k_reparam_kl_bwd
+      const float m = ep.pre_in[row * ldc + col], v = ep.pre_in[row * ldc + N + col];
+      const float gz = ep.train ? c * ep.aux[row * N + col] * 0.5f * expf(0.5f * v) : 0.f;
+      C[row * ldc + N + col] = gz + ep.aux_scale * 0.5f * (expf(v) - 1.f);
+      return c + ep.aux_scale * m;
+    }
     case HVAE_EPI_BIAS:
       return c + ep.bias[col];
     case HVAE_EPI_BIAS_GELU_DROP: {
@@ -237,7 +245,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
     if (slab) st_shared_f(&slab[(int64_t)gridDim.z * M * N + (int64_t)blockIdx.z * M + m0 + t], rowsum);
     else ep.opa_rowsum[m0 + t] = alpha * rowsum;
   }
-  const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP) ? load_step(ep.step_dev) : 0;
+  const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP && ep.kind <= HVAE_EPI_DROP_BWD) ? load_step(ep.step_dev) : 0;
   if (!slab) {
 #pragma unroll
     for (int i = 0; i < IM; ++i)
@@ -250,7 +258,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
           if (row >= M || col >= N) continue;
           float c = alpha * acc[i][j][r];
           if (beta != 0.f) c += beta * C[row * ldc + col];
-          C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
+          C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c, C);
         }
     return;
   }
@@ -291,7 +299,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
     if (row >= M || col >= N) continue;
     float c = alpha * sum[q];
     if (beta != 0.f) c += beta * C[row * ldc + col];
-    C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c);
+    C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c, C);
   }
   if (ep.opa_rowsum && blockIdx.x == 0 && t < BM && m0 + t < M) {
     float r = 0.f;
@@ -325,16 +333,22 @@ __global__ void k_colsum_final(const float* __restrict__ part, int64_t P, int64_
   out[n] = (beta != 0.f ? beta * out[n] : 0.f) + s;
 }
 
-// Tile choice: 64x64 when that already gives >= 64 blocks, else 32x32.
-static int gemm_tile(int64_t M, int64_t N) { return cdiv(M, 64) * cdiv(N, 64) >= 64 ? 64 : 32; }
+// Tile choice: 32x32 for the batch-sized GEMMs (short K, few 64x64 tiles: spread the
+// output over more CUs); 64x64 when that already gives >= 64 tiles or K is long
+// (then split-K into register-staged ranges fills the machine instead).
+static int gemm_tile(int64_t M, int64_t N, int64_t K) {
+  if (K > 4 * (int64_t)GBK * kRegStages) return 64;
+  return cdiv(M, 64) * cdiv(N, 64) >= 64 ? 64 : 32;
+}
 
 static int gemm_splits(int64_t M, int64_t N, int64_t K) {
-  const int bt = gemm_tile(M, N);
+  const int bt = gemm_tile(M, N, K);
   const int64_t tiles = cdiv(M, bt) * cdiv(N, bt);
   const int64_t kreg = (int64_t)GBK * kRegStages;
-  if (tiles >= 128 || K <= kreg) return 1;  // short K: all loads in flight at once, no split needed
+  if (K <= kreg || tiles >= 256) return 1;  // short K: all loads in flight at once, no split needed
   int64_t s = std::max<int64_t>(cdiv(K, kreg), std::min<int64_t>(cdiv(256, tiles), K / 128));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 32));
+  if (tiles * s > (int64_t)kTicketSlice * 4) s = std::max<int64_t>(1, (int64_t)kTicketSlice * 4 / tiles);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
 static int colsum_parts(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 64), 64)); }
@@ -374,7 +388,11 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
     ep.tag = epi->tag;
     ep.train = epi->train;
     ep.opa_rowsum = epi->opa_rowsum;
-    HVAE_REQUIRE(ep.kind >= 0 && ep.kind <= HVAE_EPI_DROP_BWD, "hvae_gemm_f32: bad epilogue");
+    ep.aux = epi->aux;
+    ep.aux_scale = epi->aux_scale;
+    HVAE_REQUIRE(ep.kind >= 0 && ep.kind <= HVAE_EPI_REPARAM_BWD, "hvae_gemm_f32: bad epilogue");
+    HVAE_REQUIRE(ep.kind != HVAE_EPI_REPARAM_BWD || (ep.pre_in && (ep.aux || !ep.train) && ldc >= 2 * N),
+                 "hvae_gemm_f32: REPARAM_BWD needs heads (pre_in), eps (aux) and ldc >= 2N");
     HVAE_REQUIRE(ep.kind != HVAE_EPI_BIAS || ep.bias, "hvae_gemm_f32: BIAS without bias");
     HVAE_REQUIRE(ep.kind != HVAE_EPI_BIAS_GELU_DROP || ep.pre_out, "hvae_gemm_f32: no pre_out");
     HVAE_REQUIRE(ep.kind != HVAE_EPI_GELU_DROP_BWD || ep.pre_in, "hvae_gemm_f32: no pre_in");
@@ -393,7 +411,7 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
   }
   const bool vec_a = (((uintptr_t)A) % 16 == 0) && (lda % 4 == 0);
   const bool vec_b = (((uintptr_t)B) % 16 == 0) && (ldb % 4 == 0);
-  const int bt = gemm_tile(M, N);
+  const int bt = gemm_tile(M, N, K);
   dim3 grid((unsigned)cdiv(N, bt), (unsigned)cdiv(M, bt), (unsigned)std::max(splits, 1));
   float* slab = splits > 1 ? (float*)ws : nullptr;
   unsigned* tickets = nullptr;

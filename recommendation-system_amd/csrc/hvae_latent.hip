@@ -58,27 +58,7 @@ __global__ void __launch_bounds__(256) k_loss_finalize(const float* __restrict__
                                                        const float* __restrict__ kl_rows, int64_t nb,
                                                        float beta, float* __restrict__ out3,
                                                        double* __restrict__ accum3) {
-  __shared__ double red[2][4];
-  double r = 0.0, k = 0.0;
-  for (int64_t i = threadIdx.x; i < nb; i += 256) {
-    r += (double)recon_rows[i];
-    k += (double)kl_rows[i];
-  }
-  r = wave_sum_d(r);
-  k = wave_sum_d(k);
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (lane == 0) { red[0][w] = r; red[1][w] = k; }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const double rs = ((red[0][0] + red[0][1]) + red[0][2]) + red[0][3];
-    const double ks = ((red[1][0] + red[1][1]) + red[1][2]) + red[1][3];
-    const float recon = (float)(rs / (double)nb), kl = (float)(ks / (double)nb);
-    const float total = recon + beta * kl;
-    out3[0] = total; out3[1] = recon; out3[2] = kl;
-    if (accum3) {
-      accum3[0] += (double)total; accum3[1] += (double)recon; accum3[2] += (double)kl;
-    }
-  }
+  loss_block_reduce(recon_rows, false, kl_rows, nb, beta, out3, accum3);
 }
 
 // Row-wise multinomial NLL over materialised scores (block per row).

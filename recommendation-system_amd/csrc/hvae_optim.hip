@@ -147,6 +147,53 @@ __global__ void __launch_bounds__(256) k_adam_rows(AdamArgs a, float* __restrict
   }
 }
 
+// Both updates of the step in one launch: blocks [0, nb_rows) stream W1t (as
+// k_adam_rows), the rest the dense segment (as k_adam_dense).
+__global__ void __launch_bounds__(256) k_adam_flat(AdamArgs a, float* __restrict__ p, float* __restrict__ m,
+                                                   float* __restrict__ v, const float* __restrict__ rows,
+                                                   const int32_t* __restrict__ slot_of,
+                                                   const int32_t* __restrict__ item_of,
+                                                   const int32_t* __restrict__ n_unique, int64_t N, int64_t H,
+                                                   const float* __restrict__ g_dense, int64_t dense_off,
+                                                   int64_t n_dense, int nb_rows) {
+  const AdamK k = adam_consts(a);
+  const float coef = a.coef_dev ? *a.coef_dev : 1.f;
+  if ((int)blockIdx.x < nb_rows) {
+    const int nu = *n_unique;
+    const int64_t H4 = H / 4, n4 = N * H4;
+    const int64_t stride = (int64_t)nb_rows * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+      const int64_t row = i / H4, c = i - row * H4;
+      const int s = slot_of[row];
+      float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (s >= 0 && s < nu && item_of[s] == (int32_t)row) {
+        gv = *reinterpret_cast<const float4*>(rows + (int64_t)s * H + 4 * c);
+        gv.x *= coef; gv.y *= coef; gv.z *= coef; gv.w *= coef;
+      }
+      float4 pp = reinterpret_cast<float4*>(p)[i];
+      float4 mm = reinterpret_cast<float4*>(m)[i];
+      float4 vv = reinterpret_cast<float4*>(v)[i];
+      adam_elem(pp.x, mm.x, vv.x, gv.x, k);
+      adam_elem(pp.y, mm.y, vv.y, gv.y, k);
+      adam_elem(pp.z, mm.z, vv.z, gv.z, k);
+      adam_elem(pp.w, mm.w, vv.w, gv.w, k);
+      reinterpret_cast<float4*>(p)[i] = pp;
+      reinterpret_cast<float4*>(m)[i] = mm;
+      reinterpret_cast<float4*>(v)[i] = vv;
+    }
+  } else {
+    float* pd = p + dense_off;
+    float* md = m + dense_off;
+    float* vd = v + dense_off;
+    const int64_t stride = (int64_t)(gridDim.x - nb_rows) * blockDim.x;
+    for (int64_t i = (int64_t)(blockIdx.x - nb_rows) * blockDim.x + threadIdx.x; i < n_dense; i += stride) {
+      float pp = pd[i], mm = md[i], vv = vd[i];
+      adam_elem(pp, mm, vv, g_dense[i] * coef, k);
+      pd[i] = pp; md[i] = mm; vd[i] = vv;
+    }
+  }
+}
+
 static AdamArgs to_args(const hvae_adam* c) {
   AdamArgs a;
   a.lr = c->lr; a.b1 = c->beta1; a.b2 = c->beta2; a.eps = c->eps; a.wd = c->weight_decay;
@@ -224,5 +271,23 @@ extern "C" int hvae_adam_rows(const hvae_adam* cfg, float* p, float* m, float* v
   k_adam_rows<<<(unsigned)blocks, 256, 0, as_stream(stream)>>>(to_args(cfg), p, m, v, rg->rows, rg->slot_of,
                                                              rg->item_of, rg->n_unique, N, H);
   HVAE_LAUNCH_CHECK("k_adam_rows");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v, const hvae_rowgrad* rg,
+                              int64_t N, int64_t H, const float* g_dense, int64_t dense_off, int64_t n_dense,
+                              void* stream) {
+  HVAE_REQUIRE(cfg && p && m && v && rg && rg->rows && rg->slot_of && rg->item_of && rg->n_unique,
+               "hvae_adam_flat: bad args");
+  HVAE_REQUIRE(H % 4 == 0 && ((uintptr_t)p % 16) == 0 && ((uintptr_t)m % 16) == 0 && ((uintptr_t)v % 16) == 0,
+               "hvae_adam_flat: H %% 4 and 16-B alignment required");
+  HVAE_REQUIRE(n_dense == 0 || (g_dense && dense_off >= N * H), "hvae_adam_flat: dense segment overlaps W1t");
+  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(N * H / 4, 256), 8192));
+  const int64_t b_dense = std::min<int64_t>(cdiv(n_dense, 256), 2048);
+  ProbeScope probe("adam_rows", as_stream(stream));
+  k_adam_flat<<<(unsigned)(b_rows + b_dense), 256, 0, as_stream(stream)>>>(
+      to_args(cfg), p, m, v, rg->rows, rg->slot_of, rg->item_of, rg->n_unique, N, H, g_dense, dense_off, n_dense,
+      (int)b_rows);
+  HVAE_LAUNCH_CHECK("k_adam_flat");
   return HVAE_OK;
 }

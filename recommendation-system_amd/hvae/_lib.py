@@ -19,7 +19,7 @@ HVAE_OK = 0
 HVAE_F32 = 0
 HVAE_BF16 = 1
 
-EPI_NONE, EPI_BIAS, EPI_BIAS_GELU_DROP, EPI_GELU_DROP_BWD, EPI_DROP_BWD = range(5)
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU_DROP, EPI_GELU_DROP_BWD, EPI_DROP_BWD, EPI_REPARAM_BWD = range(6)
 
 # Philox stream tags (csrc/hvae_common.h)
 TAG_ENC_DROP = 0x100
@@ -45,7 +45,7 @@ class RowGrad(C.Structure):
     _fields_ = [
         ("cnt", vp), ("slot_of", vp), ("item_of", vp), ("seg_off", vp), ("fill", vp),
         ("contrib_row", vp), ("contrib_val", vp), ("rows", vp), ("n_unique", vp),
-        ("cap", i64), ("n_items", i64),
+        ("cap", i64), ("n_items", i64), ("contrib_slot", vp), ("part", vp), ("part_floats", i64),
     ]
 
 
@@ -53,7 +53,7 @@ class Epilogue(C.Structure):
     _fields_ = [
         ("kind", cint), ("bias", vp), ("pre_out", vp), ("pre_in", vp), ("p_drop", f32),
         ("drop_mult", vp), ("seed", u64), ("step_dev", vp), ("tag", u32), ("train", cint),
-        ("opa_rowsum", vp),
+        ("opa_rowsum", vp), ("aux", vp), ("aux_scale", f32),
     ]
 
 
@@ -83,6 +83,7 @@ SIGNATURES = {
     "hvae_w1_rowgrad_plan": (cint, [P(CsrBatch), P(RowGrad), vp, sz, vp]),
     "hvae_w1_rowgrad_apply": (cint, [vp, i64, P(RowGrad), vp]),
     "hvae_rowgrad_to_dense": (cint, [P(RowGrad), i64, vp, i64, vp]),
+    "hvae_rowgrad_part_floats": (i64, [i64, i64]),
     "hvae_gemm_f32": (cint, [cint, cint, i64, i64, i64, f32, vp, i64, vp, i64, f32, vp, i64, P(Epilogue), vp,
                              sz, vp]),
     "hvae_gemm_f32_workspace": (sz, [i64, i64, i64]),
@@ -95,7 +96,8 @@ SIGNATURES = {
     "hvae_decoder_supported": (cint, [cint, i64]),
     "hvae_row_norm_max": (cint, [cint, vp, i64, i64, vp, vp]),
     "hvae_decoder_bwd": (cint, [P(CsrBatch), vp, i64, vp, i64, vp, vp, f32, vp, vp, vp]),
-    "hvae_decoder_train": (cint, [cint, vp, i64, vp, vp, vp, P(CsrBatch), i64, f32, vp, vp, vp, vp, vp, sz, vp]),
+    "hvae_decoder_train": (cint, [cint, vp, i64, vp, vp, vp, P(CsrBatch), i64, f32, vp, vp, vp, vp, vp, f32, vp,
+                                  vp, vp, sz, vp]),
     "hvae_nll_rows_fwd": (cint, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),
     "hvae_nll_rows_bwd": (cint, [vp, i64, vp, i64, vp, i64, i64, f32, vp, i64, vp]),
     "hvae_loss_finalize": (cint, [vp, vp, i64, f32, vp, vp, vp]),
@@ -104,6 +106,7 @@ SIGNATURES = {
     "hvae_clip_grad_norm_workspace": (sz, [i64, i64, i64]),
     "hvae_adam_dense": (cint, [P(Adam), vp, vp, vp, vp, i64, vp]),
     "hvae_adam_rows": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp]),
+    "hvae_adam_flat": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp, i64, i64, vp]),
     "hvae_counter_add": (cint, [vp, i64, vp]),
     "hvae_counters_add": (cint, [vp, i64, vp, i64, vp]),
     "hvae_score_candidates": (cint, [vp, i64, vp, vp, i64, vp, i64, i64, vp, vp]),

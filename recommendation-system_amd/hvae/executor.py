@@ -426,17 +426,14 @@ class FusedTrainer:
             gemm(0, 1, B, d, Lt, ptr(bf.z), Lt, ptr(Wa), Lt, ptr(bf.q), d, epi1)
             epi2 = Epilogue(_lib.EPI_BIAS, ptr(bb), None, None, 0.0, None, 0, None, 0, 0, None)
             gemm(0, 1, B, d, d, ptr(bf.q), d, ptr(Wb), d, ptr(bf.u), d, epi2)
+        accum = self.accum_train if train else self.accum_val
+        # decoder sweep + finalize (split merge, sparse loss terms, du) + the batch loss means, one call
         check(L_.hvae_decoder_train(self.dec_dtype, ptr(bf.u), d, ptr(self.E_dec), ptr(self.enorm), ptr(self.E32),
                                     csr_ref, d, 1.0 / B, ptr(bf.lse), None, ptr(bf.recon_rows),
-                                    ptr(bf.dU) if train else None, ws, wsn, st), "decoder_train")
-        accum = self.accum_train if train else self.accum_val
+                                    ptr(bf.dU) if train else None, ptr(bf.kl_rows), beta, ptr(bf.loss3), ptr(accum),
+                                    ws, wsn, st), "decoder_train")
         if not train:
-            check(L_.hvae_loss_finalize(ptr(bf.recon_rows), ptr(bf.kl_rows), B, beta, ptr(bf.loss3), ptr(accum), st),
-                  "loss_finalize")
             return
-        self._fork(main, side)
-        check(L_.hvae_loss_finalize(ptr(bf.recon_rows), ptr(bf.kl_rows), B, beta, ptr(bf.loss3), ptr(accum), st2),
-              "loss_finalize")
         # ----------------------------------------------------- backward ---
         G = self.G
         if lay.has_proj:
@@ -448,10 +445,14 @@ class FusedTrainer:
             self._fork(main, side)
             gemm(1, 0, d, Lt, B, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt,
                  rowsum=G["projection_layer.0.bias"], side_=True)
-            gemm(0, 0, B, Lt, d, ptr(bf.dp1), d, ptr(Wa), Lt, ptr(bf.dz), Lt)
-        dmu, dlv = bf.dheads, bf.dheads[:, Lt:]
-        check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B, tr,
-                                     ptr(dmu), ptr(dlv), 2 * Lt, st), "reparam_kl_bwd")
+            # dz = dp1 Wa with the reparameterisation + KL backward as its epilogue -> dheads = [dmu | dlogvar]
+            epi_r = Epilogue(_lib.EPI_REPARAM_BWD, None, None, ptr(bf.heads), 0.0, None, 0, None, 0, tr, None,
+                             ptr(bf.eps), beta / B)
+            gemm(0, 0, B, Lt, d, ptr(bf.dp1), d, ptr(Wa), Lt, ptr(bf.dheads), 2 * Lt, epi_r)
+        else:
+            dmu, dlv = bf.dheads, bf.dheads[:, Lt:]
+            check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B, tr,
+                                         ptr(dmu), ptr(dlv), 2 * Lt, st), "reparam_kl_bwd")
         self._fork(main, side)
         gemm(1, 0, 2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl,
              rowsum=self.gb_heads, side_=True)
@@ -475,15 +476,13 @@ class FusedTrainer:
         self._fork(side, main)  # join: every gradient is complete on the main stream
 
     def _launch_update(self, rg, bf: _StepBuffers, advance: int = 0):
-        """clip_grad_norm_(5.0) + Adam over the flat state; the clip launch also advances step (and boff).
+        """clip_grad_norm_(5.0) + Adam over the flat state: two launches.
 
-        The dense Adam of the small parameters runs on the side stream beside the
-        W1 Adam and is joined back at the end.
+        The clip launch also advances the step counter (and the batch offset);
+        Adam reads the pre-increment step from step_snap.
         """
         L_, lay = lib(), self.layout
-        main = torch.cuda.current_stream(self.device)
-        side = self.side if self.side is not None else main
-        st, st2 = main.cuda_stream, side.cuda_stream
+        st = torch.cuda.current_stream(self.device).cuda_stream
         H = lay.hidden
         ws, wsn = ptr(bf.ws), bf.ws.numel()
         check(L_.hvae_clip_grad_norm_step(ptr(self.g_small), lay.n_small, rg.ref, H[0], self.max_norm,
@@ -491,12 +490,9 @@ class FusedTrainer:
                                           ptr(self.boff) if advance else None, advance, ws, wsn, st),
               "clip_grad_norm_step")
         cfg = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_snap, self.coef)
-        self._fork(main, side)
-        check(L_.hvae_adam_dense(C.byref(cfg), ptr(self.small), ptr(self.m_small), ptr(self.v_small),
-                                 ptr(self.g_small), lay.n_small, st2), "adam_dense")
-        check(L_.hvae_adam_rows(C.byref(cfg), ptr(self.w1t), ptr(self.m_w1t), ptr(self.v_w1t), rg.ref,
-                                lay.n_items, H[0], st), "adam_rows")
-        self._fork(side, main)
+        # W1t (row-sparse gradient, offset 0 of the flat buffer) and the dense segment in one launch
+        check(L_.hvae_adam_flat(C.byref(cfg), ptr(self.flat), ptr(self.m), ptr(self.v), rg.ref, lay.n_items, H[0],
+                                ptr(self.g_small), lay.small_offset, lay.n_small, st), "adam_flat")
 
     def _advance(self, B: int):
         check(lib().hvae_counter_add(ptr(self.boff), B, torch.cuda.current_stream(self.device).cuda_stream),

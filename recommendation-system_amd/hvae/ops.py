@@ -133,10 +133,12 @@ class RowGradBuffers:
         self.contrib_val = torch.zeros(cap, dtype=torch.float32, device=device)
         self.rows = torch.zeros(cap, H, dtype=torch.float32, device=device)
         self.n_unique = torch.zeros(1, **i32)
+        self.contrib_slot = torch.zeros(cap, **i32)
+        self.part = torch.empty(int(lib().hvae_rowgrad_part_floats(cap, H)), dtype=torch.float32, device=device)
         self.cap, self.n_items, self.H = cap, n_items, H
         self.struct = RowGrad(ptr(self.cnt), ptr(self.slot_of), ptr(self.item_of), ptr(self.seg_off), ptr(self.fill),
                               ptr(self.contrib_row), ptr(self.contrib_val), ptr(self.rows), ptr(self.n_unique), cap,
-                              n_items)
+                              n_items, ptr(self.contrib_slot), ptr(self.part), self.part.numel())
         self.ws = torch.empty(max(int(lib().hvae_w1_rowgrad_workspace(n_items)), 256), dtype=torch.uint8,
                               device=device)
 
@@ -193,9 +195,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, alph
 
 
 def epilogue(kind, bias=None, pre_out=None, pre_in=None, p_drop=0.0, drop_mult=None, seed=0, step=None,
-             tag=0, train=False, opa_rowsum=None) -> Epilogue:
+             tag=0, train=False, opa_rowsum=None, aux=None, aux_scale=0.0) -> Epilogue:
     return Epilogue(kind, ptr(bias), ptr(pre_out), ptr(pre_in), float(p_drop), ptr(drop_mult), int(seed), ptr(step),
-                    int(tag), int(train), ptr(opa_rowsum))
+                    int(tag), int(train), ptr(opa_rowsum), ptr(aux), float(aux_scale))
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor | None = None, beta=0.0):
@@ -283,8 +285,13 @@ def decoder_bwd(x: Csr, U, E32, lse, O, grad_scale: float, want_du: bool = True)
     return recon_rows, dU
 
 
-def decoder_train(x: Csr, U, E, enorm, E32, grad_scale: float, want_du: bool = True, want_o: bool = False):
-    """Fused sweep + finalize: (lse, O or None, recon_rows, dU or None)."""
+def decoder_train(x: Csr, U, E, enorm, E32, grad_scale: float, want_du: bool = True, want_o: bool = False,
+                  kl_rows=None, beta: float = 0.0, loss3=None, accum3=None):
+    """Fused sweep + finalize: (lse, O or None, recon_rows, dU or None).
+
+    With kl_rows and loss3 given, the finalize also writes the batch loss means
+    (total, recon, kl) into loss3 (and adds them to accum3), as hvae_loss_finalize.
+    """
     require_hip(U, E, E32)
     assert U.stride(1) == 1
     nb, D = U.shape
@@ -295,8 +302,9 @@ def decoder_train(x: Csr, U, E, enorm, E32, grad_scale: float, want_du: bool = T
     dU = torch.empty(nb, D, device=U.device) if want_du else None
     ws = workspace(U.device, lib().hvae_decoder_workspace(dtype, nb, E.shape[0], D))
     check(lib().hvae_decoder_train(dtype, ptr(U), U.stride(0), ptr(E), ptr(enorm), ptr(E32), x.ref, D,
-                                   float(grad_scale), ptr(lse), ptr(O), ptr(recon_rows), ptr(dU), ptr(ws), ws.numel(),
-                                   stream_of(U)), "hvae_decoder_train")
+                                   float(grad_scale), ptr(lse), ptr(O), ptr(recon_rows), ptr(dU), ptr(kl_rows),
+                                   float(beta), ptr(loss3), ptr(accum3), ptr(ws), ws.numel(), stream_of(U)),
+          "hvae_decoder_train")
     return lse, O, recon_rows, dU
 
 

@@ -3,6 +3,7 @@
 Each HIP op is compared with a plain fp32 PyTorch-on-CPU statement of the same
 op (the oracle's building blocks). Integer/index work is checked bit-exact.
 """
+import ctypes as C
 import math
 
 import numpy as np
@@ -184,6 +185,15 @@ def test_reparam_kl(ops, hip_device):
     (zr * dz).sum().add(beta * klr.sum() / B).backward()
     dmu, dlv = ops.reparam_kl_bwd(dz.to(hip_device), mu, lv, eps_o, beta / B, True)
     assert _maxrel(dmu, m_.grad) < 1e-5 and _maxrel(dlv, l_.grad) < 1e-5
+    # the same backward as the epilogue of the GEMM that produces dz (dz = G W): [dmu | dlogvar]
+    from hvae import _lib
+    Gm, W = torch.randn(B, 96, generator=g), torch.randn(96, L, generator=g)
+    dz2 = (Gm @ W).to(hip_device)
+    dmu2, dlv2 = ops.reparam_kl_bwd(dz2, mu, lv, eps_o, beta / B, True)
+    dheads = torch.empty(B, 2 * L, device=hip_device)
+    epi = ops.epilogue(_lib.EPI_REPARAM_BWD, pre_in=hd, train=True, aux=eps_o, aux_scale=beta / B)
+    ops.gemm(Gm.to(hip_device), W.to(hip_device), out=dheads, epi=epi)
+    assert _maxrel(dheads[:, :L], dmu2) < 1e-5 and _maxrel(dheads[:, L:], dlv2) < 1e-5
 
 
 # --------------------------------------------------------------- decoder ---
@@ -274,6 +284,15 @@ def test_decoder_train_fused(ops, hip_device, dtype, nb, N, D):
     assert torch.equal(rr2, rr) and torch.equal(dU2, dU)
     _, _, rr3, none = ops.decoder_train(xd, Ud, Ek, enorm, Ed, 1.0 / nb, want_du=False)
     assert none is None and torch.equal(rr3, rr)
+    # the batch loss means fused into the finalize == hvae_loss_finalize on the same rows
+    kl = torch.rand(nb, generator=g).to(hip_device)
+    loss3 = torch.empty(3, device=hip_device)
+    acc3 = torch.zeros(3, dtype=torch.float64, device=hip_device)
+    _, _, rr4, dU4 = ops.decoder_train(xd, Ud, Ek, enorm, Ed, 1.0 / nb, kl_rows=kl, beta=0.2, loss3=loss3,
+                                       accum3=acc3)
+    assert torch.equal(rr4, rr) and torch.equal(dU4, dU)
+    ref3 = ops.loss_finalize(rr, kl, 0.2)
+    assert torch.equal(loss3, ref3) and torch.equal(acc3.float(), ref3)
     u_ = U.clone().requires_grad_(True)
     rr_t = -(x * torch.log_softmax(u_ @ E.t(), 1)).sum(1)
     rr_t.mean().backward()
@@ -331,6 +350,30 @@ def test_clip_and_adam(ops, hip_device):
     assert _maxrel(mw, rmw) < 1e-6 and _maxrel(vw, rvw) < 1e-5
 
 
+def test_adam_flat_equals_split(ops, hip_device):
+    """hvae_adam_flat (one launch over [W1t | pad | dense]) == hvae_adam_rows + hvae_adam_dense, bitwise."""
+    from hvae._lib import lib, ptr, stream_of
+    from hvae import _lib
+    g = torch.Generator().manual_seed(9)
+    N, H, nd, off = 300, 64, 5003, 300 * 64 + 32
+    X = synth_csr(20, N, seed=5)
+    rg = ops.RowGradBuffers(N, H, int(X.nnz), hip_device)
+    ops.w1_rowgrad(ops.csr_from_scipy(X, hip_device), torch.randn(20, H, generator=g).to(hip_device), rg)
+    gd = torch.randn(nd, generator=g).to(hip_device)
+    flat = torch.randn(off + nd, generator=g).to(hip_device)
+    m, v = torch.randn_like(flat) * 0.1, torch.rand_like(flat) * 0.1
+    step = torch.full((1,), 4, dtype=torch.int64, device=hip_device)
+    coef = torch.full((1,), 0.7, device=hip_device)
+    cfg = ops.adam_config(1e-3, (0.9, 0.999), 1e-8, 0.01, step, coef)
+    p1, m1, v1 = flat.clone(), m.clone(), v.clone()
+    ops.adam_rows(cfg, p1[: N * H].view(N, H), m1[: N * H].view(N, H), v1[: N * H].view(N, H), rg)
+    ops.adam_dense(cfg, p1[off:], m1[off:], v1[off:], gd)
+    p2, m2, v2 = flat.clone(), m.clone(), v.clone()
+    _lib.check(lib().hvae_adam_flat(C.byref(cfg), ptr(p2), ptr(m2), ptr(v2), rg.ref, N, H, ptr(gd), off, nd,
+                                    stream_of(p2)), "adam_flat")
+    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+
+
 def test_clip_step_counters(ops, hip_device):
     """hvae_clip_grad_norm_step == hvae_clip_grad_norm + (snap = step; step += 1; boff += advance)."""
     from hvae import _lib
@@ -351,10 +394,12 @@ def test_clip_step_counters(ops, hip_device):
     assert (int(step.item()), int(snap.item()), int(boff.item())) == (44, 43, 128 + 3 * 64)
 
 
-@pytest.mark.parametrize("nb,N,lam,hot", [(40, 300, 5.0, 0), (300, 2000, 8.0, 100), (5000, 500, 2.0, 4500)])
+@pytest.mark.parametrize("nb,N,lam,hot", [(40, 300, 5.0, 0), (300, 2000, 8.0, 100), (5000, 500, 2.0, 4500),
+                                         (40000, 3000, 1.0, 3000), (40000, 3000, 1.0, 6000)])
 def test_rowgrad_plan_apply_segments(ops, hip_device, nb, N, lam, hot):
-    """Segments of every sort path (wave <= 64, block <= 4096, selection beyond): plan + apply == dense
-    reference, bitwise == the one-call form, and bitwise reproducible."""
+    """Segments of every sort path (wave <= 64; bitmap rank for nb <= 32768; beyond that block bitonic
+    <= 4096 and selection): plan + apply == dense reference, bitwise == the one-call form, and bitwise
+    reproducible; contributions end sorted by batch row within each segment."""
     import scipy.sparse as sp
     from hvae._lib import lib, ptr, stream_of
     from hvae import _lib
@@ -381,6 +426,12 @@ def test_rowgrad_plan_apply_segments(ops, hip_device, nb, N, lam, hot):
     _lib.check(lib().hvae_w1_rowgrad_apply(ptr(dad), H, rg.ref, st), "apply")
     assert torch.equal(rg.rows[:nu], one)
     assert int(rg.cnt.abs().sum()) == 0 and int(rg.fill.abs().sum()) == 0
+    seg = rg.seg_off[: nu + 1].cpu().numpy()
+    crow = rg.contrib_row[: seg[-1]].cpu().numpy()
+    cslot = rg.contrib_slot[: seg[-1]].cpu().numpy()
+    for s_ in range(nu):
+        assert np.all(np.diff(crow[seg[s_]:seg[s_ + 1]]) > 0)
+        assert np.all(cslot[seg[s_]:seg[s_ + 1]] == s_)
     if hot:  # the long segment (its own sort path) against a float64 sum
         s0 = int((rg.item_of[:nu] == 0).nonzero()[0, 0])
         assert _maxrel(rg.rows[s0], x[:, 0] @ da.double()) < 1e-5
