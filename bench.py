@@ -120,13 +120,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(torch.cuda.device_count(), 1)
+    local = local % ndev  # more ranks than GPUs (a 1-GPU rehearsal with HVAE_DIST_BACKEND=gloo) share devices
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     group = None
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("HVAE_DIST_BACKEND", "nccl")  # nccl = RCCL over xGMI
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
         group = dist.group.WORLD
 
     from hvae.executor import ConstBeta, FusedTrainer
@@ -162,7 +168,8 @@ def main():
         torch.distributed.barrier()
     elapsed = time.perf_counter() - t0
     if group is not None:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        on_dev = torch.distributed.get_backend(group) == "nccl"
+        t = torch.tensor([elapsed], device=device if on_dev else "cpu", dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3

@@ -222,6 +222,15 @@ int hvae_reparam_kl_bwd(const float* dz, const float* mu, const float* logvar, i
  * U is rounded to bf16, MFMA 32x32x16 bf16 with f32 accumulation, and
  * e_maxnorm (device scalar, hvae_row_norm_max) bounds the scores; HVAE_F32:
  * exact-f32 MFMA (e_maxnorm unused). ws >= hvae_decoder_workspace() bytes. */
+/* The decoder's image of the frozen embeddings, built once per model:
+ *   HVAE_BF16: E rounded to bf16 [N, D], then (at a 256-B aligned offset) the
+ *              same values tile-transposed, [ceil(N/32)][D][32] with items in the
+ *              MFMA k order, so that both products of the sweep read LDS tiles
+ *              with plain 16-B reads;
+ *   HVAE_F32:  E itself [N, D].
+ * Every `E` argument of the decoder functions below is this image. */
+size_t hvae_decoder_image_bytes(int dtype, int64_t N, int64_t D);
+int hvae_decoder_image(int dtype, const float* E32, int64_t N, int64_t D, void* out, void* stream);
 int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                      int64_t nb, int64_t N, int64_t D, float* lse, float* O, void* ws,
                      size_t ws_bytes, void* stream);
@@ -301,6 +310,24 @@ int hvae_adam_rows(const hvae_adam* cfg, float* p, float* m, float* v, const hva
  * p[dense_off : dense_off + n_dense] (dense gradient g_dense). */
 int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v, const hvae_rowgrad* rg, int64_t N,
                    int64_t H, const float* g_dense, int64_t dense_off, int64_t n_dense, void* stream);
+
+/* Exact lazy Adam for the item-major W1t. torch's Adam moves every row every
+ * step, with g = 0 for rows outside the batch; those steps are a fixed map per
+ * step, so they are deferred and replayed -- the same float operations in the
+ * same order, bitwise equal to updating eagerly -- when the row is next needed.
+ *   last_step [N] int32: steps already applied to each row (start at 0)
+ *   tab [tab_len][2] float: per-step (lr / bc1_t, sqrt(bc2_t)), entry t written
+ *                           by step t's hvae_adam_lazy; tab_len > total steps
+ * hvae_adam_lazy: step t = *cfg->step_dev + 1 for the dense segment and for the
+ *   gradient rows of rg (their missed steps replayed first).
+ * hvae_adam_lazy_catchup: bring rows to *cfg->step_dev completed steps: the
+ *   rows listed by `rows` (item_of[0 : *n_unique]; before a batch's forward),
+ *   or all N rows when rows == NULL (before anything else reads W1t, m or v). */
+int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
+                   int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense, int64_t dense_off,
+                   int64_t n_dense, void* stream);
+int hvae_adam_lazy_catchup(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v,
+                           int32_t* last_step, const hvae_rowgrad* rows, int64_t N, int64_t H, void* stream);
 /* *counter += delta (device-side step/batch counters for graph replay). */
 int hvae_counter_add(int64_t* counter, int64_t delta, void* stream);
 /* *a += da and, if b != NULL, *b += db, in one launch (end of a train step). */

@@ -79,10 +79,25 @@ __device__ __forceinline__ int bf_off(int row, int chunk) {
 
 template <int D>
 constexpr int bf_tile_bytes() { return ((D + 127) / 128) * 8192; }
-// LDS ring depth: as many E tiles in flight as fit in ~100 KB (the sweep at small
-// batches has few tiles per block, so HBM latency, not MFMA, sets its pace)
+// The transposed tile image Et: per 32-item tile, [D rows][32 items] bf16 with the
+// items of each 16-group in the k order the P operand of GEMM2 carries (middle
+// two 4-groups swapped), so a GEMM2 A fragment is one 16-B ds_read_b128. (The
+// ds_read_b64_tr_b16 alternative makes the compiler drain every in-flight
+// LDS-DMA before each read, which serialises the tile ring on HBM latency.)
 template <int D>
-constexpr int bf_stages() { return bf_tile_bytes<D>() <= 24 * 1024 ? 4 : 3; }
+constexpr int bf_ttile_bytes() { return D * 64; }
+__host__ __device__ constexpr int et_item_of_pos(int p) {  // tile position -> item within the tile
+  return 16 * (p >> 4) + 4 * ((p >> 3) & 1) + 8 * ((p & 7) >> 2) + (p & 3);
+}
+// LDS ring depth: as many (E, Et) tile pairs in flight as fit in ~150 KB
+template <int D>
+constexpr int bf_stages() {
+  return (150 * 1024) / (bf_tile_bytes<D>() + bf_ttile_bytes<D>()) >= 4
+             ? 4
+             : ((150 * 1024) / (bf_tile_bytes<D>() + bf_ttile_bytes<D>()) >= 3 ? 3 : 2);
+}
+// bf16 decoder image: E as bf16 [N][D], then (256-B aligned) Et [ntiles][D][32]
+static inline int64_t et_offset_bytes(int64_t N, int64_t D) { return (N * D * 2 + 255) / 256 * 256; }
 
 // s_waitcnt vmcnt(n) alone (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14])
 template <int n>
@@ -93,7 +108,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 template <int D, bool WITH_O>
 __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, int64_t ldu,
-                                                  const bf16_t* __restrict__ E,
+                                                  const bf16_t* __restrict__ E, const bf16_t* __restrict__ Et,
                                                   const float* __restrict__ e_maxnorm, int64_t nb,
                                                   int64_t N, int splits, int64_t tiles_per_split,
                                                   DecOut out) {
@@ -103,7 +118,11 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
   constexpr int CH = D / 8;               // 16-B chunks per row
   constexpr int NSEG = (D + 127) / 128;
   constexpr int TB = bf_tile_bytes<D>();  // NSEG * 8 KiB
-  constexpr int PIECES_PER_WAVE = NSEG * 2;  // 1-KiB LDS-DMA pieces per wave per tile
+  constexpr int PIECES_E = NSEG * 2;          // 1-KiB LDS-DMA pieces per wave per E tile
+  constexpr int PIECES_T = D / 64;            // ... per Et tile (D * 64 B over 4 waves)
+  constexpr int PIECES_PER_WAVE = PIECES_E + PIECES_T;
+  constexpr int TBT = bf_ttile_bytes<D>();
+  constexpr int SB = TB + TBT;                // one ring stage: E tile | Et tile
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, col = lane & 31;
@@ -148,8 +167,8 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
   // Tail rows (item >= N) re-read row N-1; their scores are masked to -inf.
   auto issue_tile = [&](int64_t t, unsigned char* buf) {
 #pragma unroll
-    for (int i = 0; i < PIECES_PER_WAVE; ++i) {
-      const int piece = w * PIECES_PER_WAVE + i;
+    for (int i = 0; i < PIECES_E; ++i) {
+      const int piece = w * PIECES_E + i;
       const int o_b = piece * 1024 + lane * 16;  // byte offset in the tile image
       const int seg = o_b >> 13, row = (o_b >> 8) & 31, slot = (o_b >> 4) & 15;
       const int gc = seg * 16 + (slot ^ bf_swz(row));
@@ -158,6 +177,19 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
       const bf16_t* src = E + item * D + (gc < CH ? gc : 0) * 8;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(buf + piece * 1024),
+                                       16, 0, 0);
+    }
+    // Et tile: row d = 64 B = 4 chunks, physical chunk = logical ^ ((d >> 1) & 3) (8 lanes of a
+    // ds_read_b128 phase then cover all 32 banks)
+    const bf16_t* et = Et + t * (int64_t)D * kBfTI;
+#pragma unroll
+    for (int i = 0; i < PIECES_T; ++i) {
+      const int piece = w * PIECES_T + i;
+      const int o_b = piece * 1024 + lane * 16;
+      const int d = o_b >> 6, pc = (o_b >> 4) & 3;
+      const bf16_t* src = et + d * kBfTI + ((pc ^ ((d >> 1) & 3)) * 8);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(buf + TB + piece * 1024),
                                        16, 0, 0);
     }
   };
@@ -171,15 +203,16 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
   constexpr int NS = bf_stages<D>();
   if (t_beg < t_end) {
 #pragma unroll
-    for (int i = 0; i < NS - 1; ++i) issue_tile(min(t_beg + i, t_end - 1), lds + i * TB);
+    for (int i = 0; i < NS - 1; ++i) issue_tile(min(t_beg + i, t_end - 1), lds + i * SB);
   }
   int cur = 0;
   for (int64_t t = t_beg; t < t_end; ++t) {
     wait_vmcnt<(NS - 2) * PIECES_PER_WAVE>();
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    issue_tile(min(t + NS - 1, t_end - 1), lds + (cur == 0 ? NS - 1 : cur - 1) * TB);
-    const unsigned char* buf = lds + cur * TB;
+    issue_tile(min(t + NS - 1, t_end - 1), lds + (cur == 0 ? NS - 1 : cur - 1) * SB);
+    const unsigned char* buf = lds + cur * SB;
+    const unsigned char* bufT = buf + TB;
     if (wave_active) {
       // ---- GEMM1: S^T[32 items][32 users] = E_tile U^T, A reads one group ahead
       f32x16 s;
@@ -229,27 +262,22 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
                                                        pack_bf16x2(pv[8 * s2 + 4], pv[8 * s2 + 5]),
                                                        pack_bf16x2(pv[8 * s2 + 6], pv[8 * s2 + 7])));
       if (WITH_O) {
-        // ---- GEMM2: O^T[D][32 users] += E_tile^T P^T, transposed LDS reads
-        const int g = (lane >> 4) & 1, i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
-        auto rdT = [&](int d, int row) {
-          const int chunk = 4 * d + 2 * g + (pp >> 1);
-          auto* p = (__attribute__((address_space(3))) s16x4*)(void*)(buf + bf_off(row, chunk) + 8 * (pp & 1));
-          return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+        // ---- GEMM2: O^T[D][32 users] += Et_tile P^T: lane (h, m) reads row d = 32 db + m,
+        // logical chunk 2 s2 + h (the 8 items of k-block s2 it supplies), one ds_read_b128
+        const int mrow = lane & 31;
+        auto rdE = [&](int db, int s2) {
+          const int d = 32 * db + mrow;
+          return __builtin_bit_cast(
+              bf16x8, *reinterpret_cast<const uint4*>(bufT + d * 64 + (((2 * s2 + h) ^ ((d >> 1) & 3)) << 4)));
         };
-        s16x4 n00 = rdT(0, 4 * h + q), n01 = rdT(0, 8 + 4 * h + q);
-        s16x4 n10 = rdT(0, 16 + 4 * h + q), n11 = rdT(0, 24 + 4 * h + q);
+        bf16x8 e0 = rdE(0, 0), e1 = rdE(0, 1);
 #pragma unroll
-        for (int d = 0; d < (WITH_O ? DB : 1); ++d) {
-          const s16x4 c00 = n00, c01 = n01, c10 = n10, c11 = n11;
-          if (d + 1 < DB) {
-            n00 = rdT(d + 1, 4 * h + q); n01 = rdT(d + 1, 8 + 4 * h + q);
-            n10 = rdT(d + 1, 16 + 4 * h + q); n11 = rdT(d + 1, 24 + 4 * h + q);
-          }
+        for (int db = 0; db < (WITH_O ? DB : 1); ++db) {
+          const bf16x8 c0 = e0, c1 = e1;
+          if (db + 1 < DB) { e0 = rdE(db + 1, 0); e1 = rdE(db + 1, 1); }
           __builtin_amdgcn_sched_barrier(0);
-          const s16x8 a0 = {c00[0], c00[1], c00[2], c00[3], c01[0], c01[1], c01[2], c01[3]};
-          const s16x8 a1 = {c10[0], c10[1], c10[2], c10[3], c11[0], c11[1], c11[2], c11[3]};
-          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a0), pf[0], o[d], 0, 0, 0);
-          o[d] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a1), pf[1], o[d], 0, 0, 0);
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, pf[0], o[db], 0, 0, 0);
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, pf[1], o[db], 0, 0, 0);
           __builtin_amdgcn_sched_barrier(0);
         }
       }
@@ -632,6 +660,21 @@ __device__ float exact_user(int64_t b, const float* __restrict__ U, int64_t ldu,
   return mx + logf(l);
 }
 
+// bf16 decoder image: E rounded to bf16 [N][D], then the tile-transposed Et (tail items 0)
+__global__ void __launch_bounds__(256) k_build_image(const float* __restrict__ E32, int64_t N, int64_t D,
+                                                     bf16_t* __restrict__ Ebf, bf16_t* __restrict__ Et,
+                                                     int64_t ntiles) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N * D; i += stride) Ebf[i] = f2bf(E32[i]);
+  const int64_t tot = ntiles * D * kBfTI;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
+    const int64_t t = i / (D * kBfTI), r = i % (D * kBfTI);
+    const int64_t d = r / kBfTI, pos = r % kBfTI;
+    const int64_t item = t * kBfTI + et_item_of_pos((int)pos);
+    Et[i] = item < N ? f2bf(E32[item * D + d]) : (bf16_t)0;
+  }
+}
+
 // max_i ||E_i||_2 over an fp32 or bf16 [N, D] matrix (score bound of the bf16 path).
 __global__ void __launch_bounds__(256) k_row_norm_max(int dtype, const void* __restrict__ E, int64_t N, int64_t D,
                                                       unsigned* __restrict__ out_bits) {
@@ -691,13 +734,14 @@ static size_t dec_ws_bytes(int splits, int64_t nb, int64_t D) {
 template <int D, bool WO>
 static int launch_bf16(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                        const DecPlan& p, DecOut o, hipStream_t st) {
-  constexpr int lds = bf_stages<D>() * bf_tile_bytes<D>();
+  constexpr int lds = bf_stages<D>() * (bf_tile_bytes<D>() + bf_ttile_bytes<D>());
   static bool attr_set = false;
   if (!attr_set) {
     HVAE_HIP(hipFuncSetAttribute((const void*)k_dec_bf16<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = true;
   }
-  k_dec_bf16<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N, p.splits,
+  const bf16_t* Et = (const bf16_t*)((const char*)E + et_offset_bytes(N, D));
+  k_dec_bf16<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, (const bf16_t*)E, Et, enorm, nb, N, p.splits,
                                                          p.tiles_per_split, o);
   HVAE_LAUNCH_CHECK("k_dec_bf16");
   return HVAE_OK;
@@ -761,6 +805,28 @@ extern "C" int hvae_row_norm_max(int dtype, const void* E, int64_t N, int64_t D,
   const unsigned grid = (unsigned)std::min<int64_t>(cdiv(N, 4), 1024);
   k_row_norm_max<<<grid, 256, 0, st>>>(dtype, E, N, D, (unsigned*)out);
   HVAE_LAUNCH_CHECK("k_row_norm_max");
+  return HVAE_OK;
+}
+
+extern "C" size_t hvae_decoder_image_bytes(int dtype, int64_t N, int64_t D) {
+  if (dtype == HVAE_F32) return (size_t)N * D * sizeof(float);
+  return (size_t)et_offset_bytes(N, D) + (size_t)cdiv(N, kBfTI) * D * kBfTI * sizeof(bf16_t);
+}
+
+extern "C" int hvae_decoder_image(int dtype, const float* E32, int64_t N, int64_t D, void* out, void* stream) {
+  HVAE_REQUIRE(E32 && out && N > 0 && D > 0, "hvae_decoder_image: bad args");
+  HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32, "hvae_decoder_image: bad dtype");
+  hipStream_t st = as_stream(stream);
+  if (dtype == HVAE_F32) {
+    HVAE_HIP(hipMemcpyAsync(out, E32, (size_t)N * D * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return HVAE_OK;
+  }
+  const int64_t ntiles = cdiv(N, kBfTI);
+  bf16_t* Ebf = (bf16_t*)out;
+  bf16_t* Et = (bf16_t*)((char*)out + et_offset_bytes(N, D));
+  const unsigned grid = (unsigned)std::min<int64_t>(cdiv(ntiles * D * kBfTI, 256), 8192);
+  k_build_image<<<grid, 256, 0, st>>>(E32, N, D, Ebf, Et, ntiles);
+  HVAE_LAUNCH_CHECK("k_build_image");
   return HVAE_OK;
 }
 

@@ -194,6 +194,169 @@ __global__ void __launch_bounds__(256) k_adam_flat(AdamArgs a, float* __restrict
   }
 }
 
+// ---- exact lazy Adam for W1t -------------------------------------------------
+// torch's Adam moves every row each step, gradient or not: with g = 0 a row's
+// (p, m, v) evolve by a fixed per-step map that depends only on the step's bias
+// corrections. Rows outside the batch are therefore left as they are and the
+// missed steps are replayed -- the identical float operations in the identical
+// order, so the result is bitwise the eager one -- when the row is next read:
+// before the forward of a batch that contains it (catch-up of the batch rows),
+// in the update (rows merged from other ranks), and at an epoch end / state
+// read (flush of all rows). last_step[j] = steps already applied to row j;
+// tab[t] = (lr / bc1_t, sqrt(bc2_t)) of step t, written by the step's update.
+__device__ __forceinline__ AdamK adam_consts_tab(const AdamArgs& a, float2 c) {
+  AdamK k;
+  k.lr_over_bc1 = c.x;
+  k.bc2_sqrt = c.y;
+  k.omb1 = (float)(1.0 - a.b1);
+  k.b2 = (float)a.b2;
+  k.omb2 = (float)(1.0 - a.b2);
+  k.eps = (float)a.eps;
+  k.wd = (float)a.wd;
+  return k;
+}
+
+// replay steps (from, to] of row j with g = 0; one wave per row, lane owns float4
+// columns. The per-step constants come 64 steps at a time (one coalesced load,
+// then a lane broadcast per step), so a replay costs compute, not load latency.
+__device__ __forceinline__ void lazy_row_catchup(const AdamArgs& a, const float2* __restrict__ tab, float* p,
+                                                 float* m, float* v, int64_t j, int64_t H, int from, int to,
+                                                 int lane) {
+  if (from >= to) return;
+  const int64_t H4 = H / 4;
+  for (int64_t c = lane; c - lane < H4; c += 64) {  // wave-uniform trip count (shuffles below)
+    const bool on = c < H4;
+    const int64_t i = j * H4 + (on ? c : 0);
+    float4 pp = on ? reinterpret_cast<float4*>(p)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 mm = on ? reinterpret_cast<float4*>(m)[i] : pp;
+    float4 vv = on ? reinterpret_cast<float4*>(v)[i] : pp;
+    for (int t0 = from + 1; t0 <= to; t0 += 64) {
+      const int n = min(64, to - t0 + 1);
+      const float2 mine = lane < n ? tab[t0 + lane] : make_float2(0.f, 1.f);
+      for (int q = 0; q < n; ++q) {
+        const AdamK k = adam_consts_tab(a, make_float2(__shfl(mine.x, q), __shfl(mine.y, q)));
+        adam_elem(pp.x, mm.x, vv.x, 0.f, k);
+        adam_elem(pp.y, mm.y, vv.y, 0.f, k);
+        adam_elem(pp.z, mm.z, vv.z, 0.f, k);
+        adam_elem(pp.w, mm.w, vv.w, 0.f, k);
+      }
+    }
+    if (on) {
+      reinterpret_cast<float4*>(p)[i] = pp;
+      reinterpret_cast<float4*>(m)[i] = mm;
+      reinterpret_cast<float4*>(v)[i] = vv;
+    }
+  }
+}
+
+// one g = 0 step with the constants of the running step (not yet in the table)
+__device__ __forceinline__ void lazy_row_zero_step(const AdamK& k, float* p, float* m, float* v, int64_t j,
+                                                   int64_t H, int lane) {
+  const int64_t H4 = H / 4;
+  for (int64_t c = lane; c < H4; c += 64) {
+    const int64_t i = j * H4 + c;
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_elem(pp.x, mm.x, vv.x, 0.f, k);
+    adam_elem(pp.y, mm.y, vv.y, 0.f, k);
+    adam_elem(pp.z, mm.z, vv.z, 0.f, k);
+    adam_elem(pp.w, mm.w, vv.w, 0.f, k);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+  }
+}
+
+// Bring rows up to the completed step count *step: the batch's rows (item_of /
+// n_unique) or, with item_of == NULL, all N rows.
+__global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* __restrict__ tab, float* p, float* m,
+                                                      float* v, int32_t* __restrict__ last_step,
+                                                      const int32_t* __restrict__ item_of,
+                                                      const int32_t* __restrict__ n_unique, int64_t N, int64_t H) {
+  const int to = (int)load_step(a.step_dev);
+  const int64_t nrows = item_of ? (int64_t)*n_unique : N;
+  const int lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+  for (int64_t r = gw; r < nrows; r += nw) {
+    const int64_t j = item_of ? item_of[r] : r;
+    const int from = last_step[j];
+    lazy_row_catchup(a, tab, p, m, v, j, H, from, to, lane);
+    if (lane == 0 && from < to) last_step[j] = to;
+  }
+}
+
+// The step's update with lazy W1t. Blocks [0, nb_rows) take the gradient rows
+// (wave per slot: replay missed steps, then step t = *step + 1 with the clipped
+// gradient); blocks [nb_rows, nb_rows + nb_sweep) bring one of kLazySweep row
+// ranges (rotating with t) through step t with g = 0 -- skipping rows with a
+// gradient, which the first group owns -- so that no row ever lags more than
+// kLazySweep steps; the rest run the dense segment. Block 0 records tab[t].
+constexpr int kLazySweep = 8;
+__global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restrict__ tab, float* __restrict__ p,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   int32_t* __restrict__ last_step, const float* __restrict__ rows,
+                                                   const int32_t* __restrict__ slot_of,
+                                                   const int32_t* __restrict__ item_of,
+                                                   const int32_t* __restrict__ n_unique, int64_t N, int64_t H,
+                                                   const float* __restrict__ g_dense, int64_t dense_off,
+                                                   int64_t n_dense, int nb_rows, int nb_sweep) {
+  const AdamK k = adam_consts(a);
+  const float coef = a.coef_dev ? *a.coef_dev : 1.f;
+  const int t = (int)load_step(a.step_dev) + 1;
+  const int lane = threadIdx.x & 63;
+  if (blockIdx.x == 0 && threadIdx.x == 0) tab[t] = make_float2(k.lr_over_bc1, k.bc2_sqrt);
+  const int nu = *n_unique;
+  if ((int)blockIdx.x < nb_rows) {
+    const int64_t H4 = H / 4;
+    for (int s = blockIdx.x * 4 + (threadIdx.x >> 6); s < nu; s += nb_rows * 4) {
+      const int64_t j = item_of[s];
+      const int from = last_step[j];
+      lazy_row_catchup(a, tab, p, m, v, j, H, from, t - 1, lane);
+      for (int64_t c = lane; c < H4; c += 64) {
+        const int64_t i = j * H4 + c;
+        float4 gv = *reinterpret_cast<const float4*>(rows + (int64_t)s * H + 4 * c);
+        gv.x *= coef; gv.y *= coef; gv.z *= coef; gv.w *= coef;
+        float4 pp = reinterpret_cast<float4*>(p)[i];
+        float4 mm = reinterpret_cast<float4*>(m)[i];
+        float4 vv = reinterpret_cast<float4*>(v)[i];
+        adam_elem(pp.x, mm.x, vv.x, gv.x, k);
+        adam_elem(pp.y, mm.y, vv.y, gv.y, k);
+        adam_elem(pp.z, mm.z, vv.z, gv.z, k);
+        adam_elem(pp.w, mm.w, vv.w, gv.w, k);
+        reinterpret_cast<float4*>(p)[i] = pp;
+        reinterpret_cast<float4*>(m)[i] = mm;
+        reinterpret_cast<float4*>(v)[i] = vv;
+      }
+      if (lane == 0) last_step[j] = t;
+    }
+  } else if ((int)blockIdx.x < nb_rows + nb_sweep) {
+    const int64_t chunk = (N + kLazySweep - 1) / kLazySweep;
+    const int64_t r0 = (int64_t)((t - 1) % kLazySweep) * chunk, r1 = min(N, r0 + chunk);
+    const int64_t gw = (int64_t)(blockIdx.x - nb_rows) * 4 + (threadIdx.x >> 6), nw = (int64_t)nb_sweep * 4;
+    for (int64_t j = r0 + gw; j < r1; j += nw) {
+      const int sl = slot_of[j];
+      if (sl >= 0 && sl < nu && item_of[sl] == (int32_t)j) continue;  // has a gradient: first group's row
+      const int from = last_step[j];
+      if (from >= t) continue;
+      lazy_row_catchup(a, tab, p, m, v, j, H, from, t - 1, lane);
+      lazy_row_zero_step(k, p, m, v, j, H, lane);
+      if (lane == 0) last_step[j] = t;
+    }
+  } else {
+    float* pd = p + dense_off;
+    float* md = m + dense_off;
+    float* vd = v + dense_off;
+    const int nb_rest = nb_rows + nb_sweep;
+    const int64_t stride = (int64_t)(gridDim.x - nb_rest) * blockDim.x;
+    for (int64_t i = (int64_t)(blockIdx.x - nb_rest) * blockDim.x + threadIdx.x; i < n_dense; i += stride) {
+      float pp = pd[i], mm = md[i], vv = vd[i];
+      adam_elem(pp, mm, vv, g_dense[i] * coef, k);
+      pd[i] = pp; md[i] = mm; vd[i] = vv;
+    }
+  }
+}
+
 static AdamArgs to_args(const hvae_adam* c) {
   AdamArgs a;
   a.lr = c->lr; a.b1 = c->beta1; a.b2 = c->beta2; a.eps = c->eps; a.wd = c->weight_decay;
@@ -289,5 +452,45 @@ extern "C" int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v
       to_args(cfg), p, m, v, rg->rows, rg->slot_of, rg->item_of, rg->n_unique, N, H, g_dense, dense_off, n_dense,
       (int)b_rows);
   HVAE_LAUNCH_CHECK("k_adam_flat");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_adam_lazy_catchup(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v,
+                                      int32_t* last_step, const hvae_rowgrad* rows, int64_t N, int64_t H,
+                                      void* stream) {
+  HVAE_REQUIRE(cfg && cfg->step_dev && tab && p && m && v && last_step && H % 4 == 0,
+               "hvae_adam_lazy_catchup: bad args");
+  HVAE_REQUIRE(!rows || (rows->item_of && rows->n_unique), "hvae_adam_lazy_catchup: bad row list");
+  if (N == 0) return HVAE_OK;
+  const int64_t nrows = rows ? rows->cap : N;
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(nrows, 4), 16384));
+  ProbeScope probe("adam_catchup", as_stream(stream));
+  k_adam_catchup<<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v, last_step,
+                                                      rows ? rows->item_of : nullptr,
+                                                      rows ? rows->n_unique : nullptr, N, H);
+  HVAE_LAUNCH_CHECK("k_adam_catchup");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
+                              int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense,
+                              int64_t dense_off, int64_t n_dense, void* stream) {
+  HVAE_REQUIRE(cfg && cfg->step_dev && tab && p && m && v && last_step && rg && rg->rows && rg->item_of &&
+                   rg->n_unique,
+               "hvae_adam_lazy: bad args");
+  HVAE_REQUIRE(H % 4 == 0 && ((uintptr_t)p % 16) == 0 && ((uintptr_t)m % 16) == 0 && ((uintptr_t)v % 16) == 0,
+               "hvae_adam_lazy: H %% 4 and 16-B alignment required");
+  HVAE_REQUIRE(n_dense == 0 || (g_dense && dense_off >= rg->n_items * H), "hvae_adam_lazy: dense overlaps W1t");
+  HVAE_REQUIRE(tab_len >= 2, "hvae_adam_lazy: step table too short");
+  const int64_t N = rg->n_items;
+  HVAE_REQUIRE(rg->slot_of, "hvae_adam_lazy: rowgrad without slot_of");
+  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, 4), 4096));
+  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, kLazySweep), 4), 4096));
+  const int64_t b_dense = std::min<int64_t>(cdiv(n_dense, 256), 2048);
+  ProbeScope probe("adam_rows", as_stream(stream));
+  k_adam_lazy<<<(unsigned)(b_rows + b_sweep + b_dense), 256, 0, as_stream(stream)>>>(
+      to_args(cfg), (float2*)tab, p, m, v, last_step, rg->rows, rg->slot_of, rg->item_of, rg->n_unique, N, H,
+      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep);
+  HVAE_LAUNCH_CHECK("k_adam_lazy");
   return HVAE_OK;
 }

@@ -91,6 +91,8 @@ SIGNATURES = {
     "hvae_colsum_workspace": (sz, [i64, i64]),
     "hvae_reparam_kl_fwd": (cint, [vp, vp, i64, i64, i64, cint, vp, u64, vp, vp, vp, vp, vp]),
     "hvae_reparam_kl_bwd": (cint, [vp, vp, vp, i64, vp, i64, i64, f32, cint, vp, vp, i64, vp]),
+    "hvae_decoder_image_bytes": (sz, [cint, i64, i64]),
+    "hvae_decoder_image": (cint, [cint, vp, i64, i64, vp, vp]),
     "hvae_decoder_fwd": (cint, [cint, vp, i64, vp, vp, i64, i64, i64, vp, vp, vp, sz, vp]),
     "hvae_decoder_workspace": (sz, [cint, i64, i64, i64]),
     "hvae_decoder_supported": (cint, [cint, i64]),
@@ -107,6 +109,8 @@ SIGNATURES = {
     "hvae_adam_dense": (cint, [P(Adam), vp, vp, vp, vp, i64, vp]),
     "hvae_adam_rows": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp]),
     "hvae_adam_flat": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp, i64, i64, vp]),
+    "hvae_adam_lazy": (cint, [P(Adam), vp, i64, vp, vp, vp, vp, P(RowGrad), i64, vp, i64, i64, vp]),
+    "hvae_adam_lazy_catchup": (cint, [P(Adam), vp, vp, vp, vp, vp, P(RowGrad), i64, i64, vp]),
     "hvae_counter_add": (cint, [vp, i64, vp]),
     "hvae_counters_add": (cint, [vp, i64, vp, i64, vp]),
     "hvae_score_candidates": (cint, [vp, i64, vp, vp, i64, vp, i64, i64, vp, vp]),

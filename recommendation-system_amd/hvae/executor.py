@@ -119,6 +119,9 @@ class DeviceData:
     n_items: int
     row_nnz: np.ndarray       # host copy of nnz per listed user (capacity planning)
     perm: torch.Tensor = field(default=None)  # int32 [n] current epoch order
+    host_indptr: np.ndarray = field(default=None)   # host CSR (data-parallel exchange sizing)
+    host_indices: np.ndarray = field(default=None)
+    users_host: np.ndarray = field(default=None)
 
     @staticmethod
     def from_scipy(mat, users, device) -> "DeviceData":
@@ -135,6 +138,7 @@ class DeviceData:
             n_items=mat.shape[1],
             row_nnz=(rp[users + 1] - rp[users]) if len(users) else np.zeros(0, np.int64),
             perm=users_d.clone(),  # fixed address: captured graphs read the epoch order from here
+            host_indptr=rp, host_indices=mat.indices, users_host=users,
         )
 
     def max_batch_nnz(self, B: int) -> int:
@@ -223,6 +227,12 @@ class FusedTrainer:
         self._adopt_parameters()
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=device)
         self.step_snap = torch.zeros(1, dtype=torch.int64, device=device)  # step before this update (Adam's t - 1)
+        # Exact lazy Adam for W1t (hvae_adam_lazy): rows outside a batch replay their g = 0 steps when next
+        # read -- bitwise equal to torch's every-row update, without streaming all N*H each step.
+        self.lazy_adam = not bool(int(os.environ.get("HVAE_DENSE_ADAM", "0")))
+        self.last_step = torch.zeros(lay.n_items, dtype=torch.int32, device=device)
+        self.tab_len = 1 << 22
+        self.adam_tab = torch.zeros(2 * self.tab_len, dtype=torch.float32, device=device)
         # A second stream for the optimizer-only work measured slower on MI355X: every cross-stream
         # edge of the captured graph costs 5-10 us, more than the short kernels it overlaps. Off by
         # default; the dependency structure stays in place for the larger configurations.
@@ -245,7 +255,7 @@ class FusedTrainer:
             if not ops.decoder_supported(_lib.HVAE_BF16, d):
                 raise NotImplementedError(f"no bf16 streaming decoder for embedding dim {d}")
             self.dec_dtype = _lib.HVAE_BF16
-            self.E_dec = ops.cast_bf16(self.E32)
+            self.E_dec = ops.decoder_image(self.E32)  # bf16 E + its tile-transposed copy
         elif precision == "fp32":
             if not ops.decoder_supported(_lib.HVAE_F32, d):
                 raise NotImplementedError(f"no fp32 streaming decoder for embedding dim {d}")
@@ -346,11 +356,20 @@ class FusedTrainer:
             if self.dp is None:
                 self._launch_update(bf.rg, bf, advance)
             else:
-                self.dp.all_reduce_dense(self.g_small)
-                merged = self.dp.merged_rows(bf.rg.n_unique, bf.rg.item_of, bf.rg.rows)
-                self._launch_update(merged, bf, advance)
+                self._launch_exchange(bf)
+                self._launch_dp_update(bf, advance)
         elif advance:
             self._advance(advance)
+
+    def _launch_exchange(self, bf: _StepBuffers):
+        """Data-parallel collectives of a step (eager, between the two graphs): AVG of the dense gradients,
+        all-gather of the row lists."""
+        self.dp.all_reduce_dense(self.g_small)
+        self.dp.exchange(bf.rg.n_unique, bf.rg.item_of, bf.rg.rows)
+
+    def _launch_dp_update(self, bf: _StepBuffers, advance: int):
+        merged = self.dp.merge()
+        self._launch_update(merged, bf, advance)
 
     def _fork(self, src, dst):
         """dst waits for everything enqueued on src so far (a graph edge under capture)."""
@@ -394,6 +413,11 @@ class FusedTrainer:
             self._fork(main, side)
             check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st2),
                   "w1_rowgrad_plan")
+            if self.lazy_adam:  # the batch's W1t rows replay their deferred steps before the forward reads them
+                cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
+                check(L_.hvae_adam_lazy_catchup(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
+                                                ptr(self.v), ptr(self.last_step), bf.rg.ref, lay.n_items, H[0],
+                                                st2), "adam_lazy_catchup")
             ev_plan = None
             if side is not main:
                 ev_plan = torch.cuda.Event()
@@ -491,8 +515,35 @@ class FusedTrainer:
               "clip_grad_norm_step")
         cfg = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_snap, self.coef)
         # W1t (row-sparse gradient, offset 0 of the flat buffer) and the dense segment in one launch
-        check(L_.hvae_adam_flat(C.byref(cfg), ptr(self.flat), ptr(self.m), ptr(self.v), rg.ref, lay.n_items, H[0],
-                                ptr(self.g_small), lay.small_offset, lay.n_small, st), "adam_flat")
+        if self.lazy_adam:
+            check(L_.hvae_adam_lazy(C.byref(cfg), ptr(self.adam_tab), self.tab_len, ptr(self.flat), ptr(self.m),
+                                    ptr(self.v), ptr(self.last_step), rg.ref, H[0], ptr(self.g_small),
+                                    lay.small_offset, lay.n_small, st), "adam_lazy")
+        else:
+            check(L_.hvae_adam_flat(C.byref(cfg), ptr(self.flat), ptr(self.m), ptr(self.v), rg.ref, lay.n_items,
+                                    H[0], ptr(self.g_small), lay.small_offset, lay.n_small, st), "adam_flat")
+
+    def flush(self):
+        """Bring every W1t row (and its m, v) up to the completed step count (lazy Adam).
+
+        Called at the end of every epoch and eager step, so that whatever reads the
+        parameters or the optimizer state next sees torch's values.
+        """
+        if not self.lazy_adam:
+            return
+        cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
+        check(lib().hvae_adam_lazy_catchup(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
+                                           ptr(self.v), ptr(self.last_step), None, self.layout.n_items,
+                                           self.layout.hidden[0], torch.cuda.current_stream(self.device).cuda_stream),
+              "adam_lazy_flush")
+
+    def mark_all_current(self):
+        """Every row has had every step applied (after an external dense update of W1t)."""
+        self.last_step.copy_(self.step_dev.to(torch.int32).expand_as(self.last_step))
+
+    def _check_steps(self, more: int):
+        if self.lazy_adam and self.host_step + more + 2 >= self.tab_len:
+            raise RuntimeError("lazy Adam step table exhausted; run with HVAE_DENSE_ADAM=1")
 
     def _advance(self, B: int):
         check(lib().hvae_counter_add(ptr(self.boff), B, torch.cuda.current_stream(self.device).cuda_stream),
@@ -505,9 +556,14 @@ class FusedTrainer:
         cap = int(data.row_ptr[-1].item()) if rows is None else data.max_batch_nnz(B)
         bf = self._buffers(B, cap, train)
         csr = self._csr(data, B, rows, None)
+        if train:
+            self._check_steps(1)
+        else:
+            self.flush()
         self._launch(bf, csr, train, beta, p_drop, ext)
         if train:
             self.host_step += 1
+            self.flush()
         return bf.loss3
 
     def run_epoch(self, data: DeviceData, batch_size: int, shuffle: bool, beta_fn, p_drop: float,
@@ -525,10 +581,15 @@ class FusedTrainer:
             order = torch.randperm(n, generator=generator)
             data.perm.copy_(data.users[order.to(self.device)])
         else:
+            order = None
             data.perm.copy_(data.users)
         accum = self.accum_train if train else self.accum_val
         accum.zero_()
         self.boff.zero_()
+        if train:
+            self._check_steps(n // batch_size + 1)
+        else:
+            self.flush()  # the forward reads W1t rows that no catch-up precedes
         n_full, tail = divmod(n, batch_size)
         if drop_last:
             tail = 0
@@ -537,41 +598,65 @@ class FusedTrainer:
         n_batches = n_full + (1 if tail else 0)
         const_beta = getattr(beta_fn, "constant", None)
         B = batch_size
+        dp = self.dp if train else None
+        M = 0
+        if dp is not None:  # fixed exchange size for the epoch: one host all-reduce, no per-step sync
+            from .dist import batch_unique_counts
+            users_h = data.users_host if order is None else data.users_host[order.numpy()]
+            counts = batch_unique_counts(data.host_indptr, data.host_indices,
+                                         users_h[: n_full * B + (tail if tail else 0)], B)
+            M = dp.plan_epoch(counts)
         for bi in range(n_full):
             beta = beta_fn(bi)
-            bf = self._buffers(B, data.max_batch_nnz(B), train)
-            if self.use_graphs and const_beta is not None and self.dp is None:
-                if bf.graph is None or bf.graph_key != (id(data), beta, p_drop):
+            bf = self._buffers(B, max(data.max_batch_nnz(B), M), train)
+            if self.use_graphs and const_beta is not None:
+                key = (id(data), beta, p_drop, M)
+                if bf.graph is None or bf.graph_key != key:
                     if bi == 0 and bf.graph is None:
                         # first use: run eagerly (loads kernels, sets attributes), capture afterwards
                         self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
                         if train:
                             self.host_step += 1
                         continue
-                    self._capture(bf, data, train, beta, p_drop)
+                    self._capture(bf, data, train, beta, p_drop, key)
                 bf.graph.replay()
+                if dp is not None:  # collectives between the two graphs of a data-parallel step
+                    self._launch_exchange(bf)
+                    bf.graph_up.replay()
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
             if train:
                 self.host_step += 1
         if tail:
             beta = beta_fn(n_full)
-            bf = self._buffers(tail, data.max_batch_nnz(tail), train)
+            bf = self._buffers(tail, max(data.max_batch_nnz(tail), M), train)
             self._launch(bf, self._csr(data, tail, data.perm, self.boff), train, beta, p_drop, advance=tail)
             if train:
                 self.host_step += 1
+        self.flush()
         sums = accum.cpu().tolist()  # the one host sync of the epoch
         return {"total_loss": sums[0] / n_batches, "recon_loss": sums[1] / n_batches, "kl_loss": sums[2] / n_batches}
 
-    def _capture(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float):
-        g = torch.cuda.CUDAGraph()
+    def _capture(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float, key):
+        """One graph per step (single GPU); data-parallel: forward/backward, then merge + clip + Adam,
+        with the collectives launched eagerly in between (they stay out of the graphs)."""
         csr = self._csr(data, bf.B, data.perm, self.boff)
         bf.csr_keepalive = csr
         torch.cuda.synchronize(self.device)
-        with torch.cuda.graph(g):
-            self._launch(bf, csr, train, beta, p_drop, advance=bf.B)
+        g = torch.cuda.CUDAGraph()
+        if self.dp is None or not train:
+            with torch.cuda.graph(g):
+                self._launch(bf, csr, train, beta, p_drop, advance=bf.B)
+            bf.graph_up = None
+        else:
+            with torch.cuda.graph(g):
+                self._launch_fwd_bwd(bf, csr, train, beta, p_drop, None)
+            g2 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g2):
+                self._launch_dp_update(bf, bf.B)
+            bf.graph_up = g2
         bf.graph = g
-        bf.graph_key = (id(data), beta, p_drop)
+        bf.graph_key = key
 
     def sync_state_to_model(self):
         """Parameters are views of the flat buffer already; nothing to copy."""

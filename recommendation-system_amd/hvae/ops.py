@@ -239,7 +239,43 @@ def reparam_kl_bwd(dz, mu, logvar, eps, kl_scale: float, train: bool, dmu=None, 
 
 
 # ------------------------------------------------------------------ decoder --
-def row_norm_max(E: torch.Tensor) -> torch.Tensor:
+class DecoderImage:
+    """The frozen embeddings as the bf16 decoder reads them (hvae_decoder_image): bf16 E [N, D] followed by
+    its tile-transposed copy. `bf16` is a view of the first part."""
+
+    def __init__(self, E32: torch.Tensor):
+        require_hip(E32)
+        E32 = E32.contiguous()
+        self.N, self.D = E32.shape
+        self.dtype = _lib.HVAE_BF16
+        nbytes = int(lib().hvae_decoder_image_bytes(self.dtype, self.N, self.D))
+        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=E32.device)
+        check(lib().hvae_decoder_image(self.dtype, ptr(E32), self.N, self.D, ptr(self.buf), stream_of(E32)),
+              "hvae_decoder_image")
+        self.bf16 = self.buf[: self.N * self.D * 2].view(torch.bfloat16).view(self.N, self.D)
+        self.device = E32.device
+
+    def data_ptr(self) -> int:
+        return self.buf.data_ptr()
+
+
+def decoder_image(E32: torch.Tensor) -> DecoderImage:
+    return DecoderImage(E32)
+
+
+def _dec_operand(E):
+    """(dtype code, N, pointer holder) of a decoder E argument: a DecoderImage (bf16) or an fp32 [N, D]."""
+    if isinstance(E, DecoderImage):
+        return _lib.HVAE_BF16, E.N, E
+    if E.dtype == torch.bfloat16:
+        raise TypeError("the bf16 decoder takes a DecoderImage (ops.decoder_image), not a bf16 tensor")
+    return _lib.HVAE_F32, E.shape[0], E
+
+
+def row_norm_max(E) -> torch.Tensor:
+    """max_i ||E_i|| of an fp32 / bf16 [N, D] matrix or of a DecoderImage's bf16 values (device scalar)."""
+    if isinstance(E, DecoderImage):
+        E = E.bf16
     require_hip(E)
     out = torch.empty(1, device=E.device)
     dtype = _lib.HVAE_BF16 if E.dtype == torch.bfloat16 else _lib.HVAE_F32
@@ -260,18 +296,17 @@ def decoder_supported(dtype: int, D: int) -> bool:
     return bool(lib().hvae_decoder_supported(dtype, D))
 
 
-def decoder_fwd(U: torch.Tensor, E: torch.Tensor, enorm: torch.Tensor | None, with_o: bool = True):
-    """(lse [nb], O [nb, D] or None) of the streaming decoder; E fp32 or bf16."""
-    require_hip(U, E)
+def decoder_fwd(U: torch.Tensor, E, enorm: torch.Tensor | None, with_o: bool = True):
+    """(lse [nb], O [nb, D] or None) of the streaming decoder; E a DecoderImage (bf16) or fp32 [N, D]."""
+    dtype, N, Eh = _dec_operand(E)
+    require_hip(U)
     assert U.stride(1) == 1
     nb, D = U.shape
-    N = E.shape[0]
-    dtype = _lib.HVAE_BF16 if E.dtype == torch.bfloat16 else _lib.HVAE_F32
     lse = torch.empty(nb, device=U.device)
     O = torch.empty(nb, D, device=U.device) if with_o else None
     need = lib().hvae_decoder_workspace(dtype, nb, N, D)
     ws = workspace(U.device, need)
-    check(lib().hvae_decoder_fwd(dtype, ptr(U), U.stride(0), ptr(E), ptr(enorm), nb, N, D, ptr(lse), ptr(O),
+    check(lib().hvae_decoder_fwd(dtype, ptr(U), U.stride(0), ptr(Eh), ptr(enorm), nb, N, D, ptr(lse), ptr(O),
                                  ptr(ws), ws.numel(), stream_of(U)), "hvae_decoder_fwd")
     return lse, O
 
@@ -292,16 +327,16 @@ def decoder_train(x: Csr, U, E, enorm, E32, grad_scale: float, want_du: bool = T
     With kl_rows and loss3 given, the finalize also writes the batch loss means
     (total, recon, kl) into loss3 (and adds them to accum3), as hvae_loss_finalize.
     """
-    require_hip(U, E, E32)
+    dtype, N, Eh = _dec_operand(E)
+    require_hip(U, E32)
     assert U.stride(1) == 1
     nb, D = U.shape
-    dtype = _lib.HVAE_BF16 if E.dtype == torch.bfloat16 else _lib.HVAE_F32
     lse = torch.empty(nb, device=U.device)
     O = torch.empty(nb, D, device=U.device) if want_o else None
     recon_rows = torch.empty(nb, device=U.device)
     dU = torch.empty(nb, D, device=U.device) if want_du else None
-    ws = workspace(U.device, lib().hvae_decoder_workspace(dtype, nb, E.shape[0], D))
-    check(lib().hvae_decoder_train(dtype, ptr(U), U.stride(0), ptr(E), ptr(enorm), ptr(E32), x.ref, D,
+    ws = workspace(U.device, lib().hvae_decoder_workspace(dtype, nb, N, D))
+    check(lib().hvae_decoder_train(dtype, ptr(U), U.stride(0), ptr(Eh), ptr(enorm), ptr(E32), x.ref, D,
                                    float(grad_scale), ptr(lse), ptr(O), ptr(recon_rows), ptr(dU), ptr(kl_rows),
                                    float(beta), ptr(loss3), ptr(accum3), ptr(ws), ws.numel(), stream_of(U)),
           "hvae_decoder_train")

@@ -96,6 +96,7 @@ class HipAdam(torch.optim.Optimizer):
             self._moments[p] = (m, v)
 
     def _sync_state(self):
+        self.fused.flush()
         step = float(self.fused.step_dev.item())
         for p, (m, v) in self._moments.items():
             if step > 0:
@@ -110,6 +111,7 @@ class HipAdam(torch.optim.Optimizer):
         loss = closure() if closure is not None else None
         g0 = self.param_groups[0]
         cfg = ops.adam_config(g0["lr"], g0["betas"], g0["eps"], g0["weight_decay"], self.fused.step_dev, None)
+        self.fused.flush()  # W1t rows current before the dense update of every row
         for p, (m, v) in self._moments.items():
             if p.grad is None:
                 continue
@@ -117,6 +119,7 @@ class HipAdam(torch.optim.Optimizer):
             g.copy_(p.grad)
             ops.adam_dense(cfg, p, m, v, g)  # p, m, v, g share one dense memory order
         ops.counter_add(self.fused.step_dev, 1)
+        self.fused.mark_all_current()
         return loss
 
 

@@ -2,12 +2,15 @@
 
 Checks the collective protocol the GPU path uses over RCCL: dense gradients are
 averaged; row-sparse first-layer gradients of different lengths per rank are
-gathered, padded, weighted 1/world and merged in (rank, slot) order, so every
-rank ends with the identical merged gradient = mean of the ranks' dense grads.
+gathered at the epoch's fixed size (max over ranks and batches, one host
+all-reduce per epoch), weighted 1/world (0 past each rank's count) and merged
+in (rank, slot) order, so every rank ends with the identical merged gradient =
+mean of the ranks' dense grads.
 """
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -22,7 +25,7 @@ class _Dense:
         self.dense = torch.zeros(N, H, dtype=torch.float64)
 
 
-def _cpu_merge(ex, items, grows, weights, out):
+def _cpu_merge(ex, items, grows, weights, out, rp):
     out.dense.zero_()
     for b in range(items.numel()):  # fixed (rank, slot) order, as the HIP merge
         out.dense[int(items[b])] += float(weights[b]) * grows[b].double()
@@ -48,6 +51,8 @@ def _worker(rank, world, port, q):
     rows = torch.zeros(cap, H)
     rows[:k] = torch.randn(k, H, generator=g)
     rows[k:] = 1e30  # stale slots beyond n_unique must never contribute
+    ex.plan_epoch(np.array([3, k]))  # per-batch counts of this rank; the epoch size is the max over ranks
+    assert ex.M == 5 + 7 * (world - 1)
     merged = ex.merged_rows(torch.tensor([k], dtype=torch.int32), item_of, rows)
     dense_mine = torch.zeros(N, H, dtype=torch.float64)
     dense_mine[items.long()] = rows[:k].double()

@@ -205,9 +205,9 @@ def test_decoder(ops, hip_device, dtype, nb, N, D):
     g = torch.Generator().manual_seed(nb)
     U = torch.randn(nb, D, generator=g) * 3.0
     Ed = E.to(hip_device)
-    Ek = ops.cast_bf16(Ed) if dtype == "bf16" else Ed
+    Ek = ops.decoder_image(Ed) if dtype == "bf16" else Ed
     if dtype == "bf16":
-        Ur, Er = U.bfloat16().float(), Ek.float().cpu()
+        Ur, Er = U.bfloat16().float(), Ek.bf16.float().cpu()
     else:
         Ur, Er = U, E
     enorm = ops.row_norm_max(Ek)
@@ -229,9 +229,9 @@ def test_decoder_large_norm_fixup(ops, hip_device):
     g = torch.Generator().manual_seed(1)
     U = torch.randn(8, D, generator=g)
     U = U / U.norm(dim=1, keepdim=True) * torch.tensor([1, 10, 50, 100, 200, 400, 800, 1500.0])[:, None]
-    Ek = ops.cast_bf16(E.to(hip_device))
+    Ek = ops.decoder_image(E.to(hip_device))
     lse, O = ops.decoder_fwd(U.to(hip_device), Ek, ops.row_norm_max(Ek))
-    S = U.bfloat16().double() @ Ek.float().cpu().double().t()
+    S = U.bfloat16().double() @ Ek.bf16.float().cpu().double().t()
     assert torch.isfinite(lse).all() and torch.isfinite(O).all()
     rel = ((lse.double().cpu() - torch.logsumexp(S, 1)).abs() / torch.logsumexp(S, 1).abs().clamp(min=1))
     assert rel.max() < 2e-3
@@ -274,7 +274,7 @@ def test_decoder_train_fused(ops, hip_device, dtype, nb, N, D):
     U = torch.randn(nb, D, generator=g) * 2
     xd = ops.csr_from_scipy(X, hip_device)
     Ed, Ud = E.to(hip_device), U.to(hip_device)
-    Ek = ops.cast_bf16(Ed) if dtype == "bf16" else Ed
+    Ek = ops.decoder_image(Ed) if dtype == "bf16" else Ed
     enorm = ops.row_norm_max(Ek)
     lse, O, rr, dU = ops.decoder_train(xd, Ud, Ek, enorm, Ed, 1.0 / nb, want_o=True)
     lse_b, O_b = ops.decoder_fwd(Ud, Ek, enorm)
@@ -461,3 +461,22 @@ def test_candidates_rank_topk(ops, hip_device):
     for r in range(7):
         ref_idx = R.topk_exclude_seen(S[r].numpy(), X[r].indices, 20)
         np.testing.assert_array_equal(idx[r].cpu().numpy(), ref_idx)
+
+
+def test_decoder_image_layout(ops, hip_device):
+    """bf16 image = bf16(E) then the tile-transposed copy with items in the MFMA k order (tail items 0)."""
+    N, D = 77, 64
+    E = torch.as_tensor(synth_embeddings(N, D, seed=2))
+    img = ops.decoder_image(E.to(hip_device))
+    Eb = E.bfloat16()
+    assert torch.equal(img.bf16.cpu(), Eb)
+    off = (N * D * 2 + 255) // 256 * 256
+    nt = (N + 31) // 32
+    Et = img.buf[off: off + nt * D * 32 * 2].view(torch.bfloat16).view(nt, D, 32).cpu()
+    pos_item = [16 * (p >> 4) + 4 * ((p >> 3) & 1) + 8 * ((p & 7) >> 2) + (p & 3) for p in range(32)]
+    assert sorted(pos_item) == list(range(32))
+    for t in range(nt):
+        for p_, it in enumerate(pos_item):
+            item = 32 * t + it
+            want = Eb[item] if item < N else torch.zeros(D, dtype=torch.bfloat16)
+            assert torch.equal(Et[t, :, p_], want)
