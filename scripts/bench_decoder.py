@@ -1,0 +1,58 @@
+"""Standalone timing of the streaming decoder sweep (hvae_decoder_fwd with O) on one shape.
+
+    python scripts/bench_decoder.py [--nb 4096] [--N 100000] [--D 384] [--dtype bf16|fp8|fp32] [--reps 20]
+
+U rows are random with |u| ~ 4 (the scale trained projections reach), E is L2-normalised
+random. The library's probe brackets every sweep launch with a hipEvent pair on its stream;
+TFLOP/s counts the algorithmic 4 * nb * N * D of the sweep (S = U E^T and O = P E).
+"""
+import argparse
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "recommendation-system_amd")]
+
+import torch  # noqa: E402
+
+from hvae import _lib, ops  # noqa: E402
+from hvae._lib import check, lib  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nb", type=int, default=4096)
+    ap.add_argument("--N", type=int, default=100000)
+    ap.add_argument("--D", type=int, default=384)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    E32 = torch.randn(args.N, args.D, device=dev, generator=g)
+    E32 /= E32.norm(dim=1, keepdim=True)
+    U = torch.randn(args.nb, args.D, device=dev, generator=g) * (4.0 / args.D ** 0.5)
+    if args.dtype == "fp32":
+        E, enorm = E32, None
+    else:
+        E = ops.decoder_image(E32)
+        enorm = ops.row_norm_max(E)
+    ops.decoder_fwd(U, E, enorm)  # warm-up (and kernel attributes)
+    torch.cuda.synchronize()
+    check(lib().hvae_probe_arm(b"decoder_sweep", 4 * args.reps), "probe_arm")
+    for _ in range(args.reps):
+        ops.decoder_fwd(U, E, enorm)
+    torch.cuda.synchronize()
+    avg, n = C.c_double(), C.c_int()
+    check(lib().hvae_probe_collect(C.byref(avg), C.byref(n)), "probe_collect")
+    check(lib().hvae_probe_arm(None, 0), "probe_disarm")
+    us = avg.value
+    flops = 4.0 * args.nb * args.N * args.D
+    print(json.dumps({"nb": args.nb, "N": args.N, "D": args.D, "dtype": args.dtype, "launches": n.value,
+                      "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
