@@ -323,6 +323,370 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
   }
 }
 
+// ------------------------------------------------------- bf16, version 2 ---
+// One row-major E image per tile (no transposed copy): GEMM1 reads its rows with
+// ds_read_b128, GEMM2 reads its columns with ds_read_b64_tr_b16 (T10). E tiles
+// arrive by LDS-DMA issued from inline asm (buffer_load_dwordx4 ... lds): the
+// compiler does not see those writes, so it neither drains them before the
+// transposed reads nor recomputes their addresses -- each lane's source offsets
+// are fixed for the kernel, the tile base is a scalar soffset, and rows past N
+// read 0 through the buffer's bounds check.
+//
+// Software pipeline, one barrier per tile: the softmax of tile t (VALU) is
+// interleaved with GEMM1 of tile t+1 (MFMA), then GEMM2 of tile t.
+//
+// DS = 1: 4 waves x 32 users, each over all D (D <= 384: U 96 + O 192 VGPRs).
+// DS = 2: waves (ug, dh) = (w & 1, w >> 1): 2 user groups x 2 halves of D, each
+// wave's GEMM1 sums over its half and the two halves' partial S^T tiles are added
+// through LDS (double-buffered by tile parity); both waves of a user group run the
+// softmax, each accumulates O for its half of D. Serves D = 768 (U 96 + O 192 per
+// wave) and small batches (64 users per block keeps all 4 waves busy).
+constexpr float kLog2e = 1.4426950408889634f;
+#ifndef DEC2_G1_AHEAD
+#define DEC2_G1_AHEAD 1
+#endif
+#ifndef DEC2_G2_AHEAD
+#define DEC2_G2_AHEAD 1
+#endif
+// a split's ltot below e^-60 means its max term lost precision (see k_dec2_bf16)
+constexpr float kMinL = 8.75651e-27f;
+
+template <int D, int DS>
+constexpr int d2_tile_bytes() { return ((D + 127) / 128) * 8192; }
+template <int DS, int NW>
+constexpr int d2_xbytes() { return DS == 2 ? 2 * NW * 4096 : 0; }
+template <int D, int DS, int NW>
+constexpr int d2_stages() {
+  return (160 * 1024 - d2_xbytes<DS, NW>() - 1024) / d2_tile_bytes<D, DS>() >= 6
+             ? 6
+             : (160 * 1024 - d2_xbytes<DS, NW>() - 1024) / d2_tile_bytes<D, DS>();
+}
+template <int D, int DS, int NW>
+constexpr int d2_lds_bytes() {
+  return d2_stages<D, DS, NW>() * d2_tile_bytes<D, DS>() + d2_xbytes<DS, NW>() + 1024;
+}
+
+// LDS image of one 32-item tile (version 2): per 128-column segment (8 KiB) 8-row x 32-column
+// subtiles of 512 B with a 2-bit chunk XOR (cdna_hip_programming.md T10 image (a)). Row reads of the
+// 32x32x16 A operand and the transposed reads both hit every bank once, and the reads of one GEMM
+// differ by lane-constant offsets, so two base registers serve all of them.
+__device__ __forceinline__ int d2_off(int row, int ch) {
+  return ((ch >> 4) << 13) + ((row >> 3) << 11) + (((ch & 15) >> 2) << 9) + ((row & 7) << 6) +
+         (((ch & 3) ^ ((row >> 2) & 3)) << 4);
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+template <int D, int DS, int NW, bool WITH_O>
+__global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__ U, int64_t ldu,
+                                                   const bf16_t* __restrict__ E, const float* __restrict__ e_maxnorm,
+                                                   int64_t nb, int64_t N, int splits, int64_t tiles_per_split,
+                                                   DecOut out) {
+  constexpr int DW = D / DS;            // dims owned by one wave
+  constexpr int KS = DW / 16;           // GEMM1 k-steps
+  constexpr int DB = DW / 32;           // GEMM2 d-blocks
+  constexpr int CH = D / 8;             // 16-B chunks per E row
+  constexpr int NSEG = (D + 127) / 128;
+  constexpr int TB = d2_tile_bytes<D, DS>();
+  constexpr int PW = NSEG * 8 / NW;     // 1-KiB LDS-DMA pieces per wave per tile
+  constexpr int NS = d2_stages<D, DS, NW>();
+  constexpr int UPB = 32 * NW / DS;
+  constexpr int HALF = NW / 2;          // DS = 2: partner wave = w ^ HALF
+  static_assert(NW == 4 || (NW == 8 && DS == 2), "8-wave blocks split D");
+  static_assert(DW % 32 == 0 && KS % 2 == 0, "D / DS must be a multiple of 32");
+  static_assert(NS >= 2, "LDS ring too small");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  float* xbuf = reinterpret_cast<float*>(lds + NS * TB);                        // [2][4 w][4 r4][64 lane][4]
+  float* usq_sh = reinterpret_cast<float*>(lds + NS * TB + d2_xbytes<DS, NW>());  // [NW w][32]
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ug = DS == 1 ? w : (w % HALF), dh = DS == 1 ? 0 : (w / HALF);
+  const int split = blockIdx.x % splits;
+  const int64_t ub = blockIdx.x / splits;
+  const int64_t u0 = ub * UPB + ug * 32;
+  const int64_t user = u0 + col;
+  const bool wave_active = u0 < nb;
+  const int64_t ntiles = (N + kBfTI - 1) / kBfTI;
+  const int64_t t_beg = (int64_t)split * tiles_per_split;
+  const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
+  const int dbase = dh * DW;
+  const float emax = *e_maxnorm;  // before any LDS-DMA is in flight (the compiler's wait would drain them)
+
+  // U fragments (B operand of GEMM1): lane holds U[user][dbase + 16 ks + 8 h + j]
+  uint4 uf[KS];
+  float usq = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (user < nb) {
+      a = *reinterpret_cast<const float4*>(U + user * ldu + dbase + 16 * ks + 8 * h);
+      b = *reinterpret_cast<const float4*>(U + user * ldu + dbase + 16 * ks + 8 * h + 4);
+    }
+    usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+    uf[ks] = make_uint4(pack_bf16x2(a.x, a.y), pack_bf16x2(a.z, a.w), pack_bf16x2(b.x, b.y),
+                        pack_bf16x2(b.z, b.w));
+  }
+  usq += __shfl_xor(usq, 32, 64);
+  if (DS == 2 && h == 0) usq_sh[w * 32 + col] = usq;
+
+  // LDS-DMA source offsets of this lane's pieces (tile-relative) and the buffer
+  // resource over bf16 E [N][D] (bounds = N D 2 bytes: tail rows read 0)
+  int voff[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int o_b = (w * PW + i) * 1024 + lane * 16;  // inverse of d2_off
+    const int seg = o_b >> 13, rem = o_b & 8191;
+    const int row = ((rem >> 11) << 3) + ((rem >> 6) & 7);
+    const int ch = (((rem >> 9) & 3) << 2) + (((rem >> 4) & 3) ^ ((row >> 2) & 3));
+    const int gc = seg * 16 + ch;
+    voff[i] = row * (D * 2) + (gc < CH ? gc : 0) * 16;
+  }
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(E), (short)0, (int)(N * D * 2), 0x00020000);
+  const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
+  auto issue = [&](int64_t t, int slot_i) {
+    const uint32_t soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(kBfTI * D * 2)));
+    const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
+  };
+  auto lds_fence = [] { asm volatile("" ::: "memory"); };
+
+  // GEMM2 operand addressing (T10): group g16 = lane >> 4 reads 4 item rows x 16 d columns;
+  // lane 4q + p of the group addresses row q, columns 4p..4p+3
+  const int g1 = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
+  // lane parts of d2_off for the GEMM1 row reads (by ks parity) and the transposed reads (by j)
+  const int c4 = dbase / 32;  // chunk group of this wave's first column (dbase / 8 / 4)
+  const int laneA0 = ((col >> 3) << 11) + ((col & 7) << 6) + (((0 + h) ^ ((col >> 2) & 3)) << 4);
+  const int laneA1 = ((col >> 3) << 11) + ((col & 7) << 6) + (((2 + h) ^ ((col >> 2) & 3)) << 4);
+  const int laneT0 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((0 + h) & 3)) << 4) + 8 * (pp & 1);
+  const int laneT1 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((2 + h) & 3)) << 4) + 8 * (pp & 1);
+
+  // GEMM1 partial over this wave's dims: S^T[32 items][32 users] = E_tile U^T. A operands are read
+  // two k-groups ahead; fill(g) places other work (the previous tile's softmax) after the g-th MFMA
+  // pair, in the shadow of the MFMA pipe (sched_barrier pins the interleave).
+  auto gemm1 = [&](const unsigned char* buf, auto&& fill) {
+    f32x16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+    // d2_off(col, c0 + 2 ks + h) = laneA[ks & 1] + (wave-uniform chunk-group term) + immediate
+    const unsigned char* b0 = buf + laneA0;
+    const unsigned char* b1 = buf + laneA1;
+    auto rdA = [&](int ks) {
+      const int grp = c4 + (ks >> 1);
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(((ks & 1) ? b1 : b0) + ((grp >> 2) << 13) +
+                                                                         ((grp & 3) << 9)));
+    };
+    constexpr int AH = DEC2_G1_AHEAD;  // k-groups of A operands in flight
+    bf16x8 a[2 * AH];
+#pragma unroll
+    for (int j = 0; j < 2 * AH; ++j)
+      if (j < KS) a[j] = rdA(j);
+#pragma unroll
+    for (int g = 0; g < KS / 2; ++g) {
+      const bf16x8 c0 = a[(2 * g) % (2 * AH)], c1 = a[(2 * g + 1) % (2 * AH)];
+      if (2 * g + 2 * AH < KS) {
+        a[(2 * g) % (2 * AH)] = rdA(2 * g + 2 * AH);
+        a[(2 * g + 1) % (2 * AH)] = rdA(2 * g + 2 * AH + 1);
+      }
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, __builtin_bit_cast(bf16x8, uf[2 * g]), s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, __builtin_bit_cast(bf16x8, uf[2 * g + 1]), s, 0, 0, 0);
+      fill(g);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return s;
+  };
+  // DS = 2: this wave's partial S^T of a tile <-> its partner's, [r4][lane] float4 rows
+  auto xput = [&](int par, const f32x16& s) {
+    float* xb = xbuf + ((par * NW + w) * 4) * 256;
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4)
+      *reinterpret_cast<float4*>(xb + r4 * 256 + lane * 4) = make_float4(s[4 * r4], s[4 * r4 + 1], s[4 * r4 + 2],
+                                                                         s[4 * r4 + 3]);
+  };
+  auto xadd = [&](int par, f32x16& s) {
+    const float* xb = xbuf + ((par * NW + (w ^ HALF)) * 4) * 256;
+#pragma unroll
+    for (int r4 = 0; r4 < 4; ++r4) {
+      const float4 v = *reinterpret_cast<const float4*>(xb + r4 * 256 + lane * 4);
+      s[4 * r4] += v.x; s[4 * r4 + 1] += v.y; s[4 * r4 + 2] += v.z; s[4 * r4 + 3] += v.w;
+    }
+  };
+
+  f32x16 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m = 0.f, mL = 0.f, lsum = 0.f;
+  f32x16 s_cur;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s_cur[r] = 0.f;
+
+  int cur = 0;
+  // GEMM2: O^T[DW][32 users] += E_tile^T P^T; A operands by transposed reads, two d-blocks ahead
+  auto gemm2 = [&](const bf16x8 (&pf)[2]) {
+    if constexpr (WITH_O) {
+      const unsigned char* buf = lds + cur * TB;
+      // d2_off(16 s2 + 8 j + 4 h + q, c0 + 4 db + 2 g1 + pp / 2) + 8 (pp & 1) = laneT[j] + uniform + immediate
+      const unsigned char* t0 = buf + laneT0;
+      const unsigned char* t1 = buf + laneT1;
+      auto rdT = [&](int db, int row) {  // row = 16 s2 + 8 j + (4 h + q): pass 16 s2 + 8 j
+        const int j = (row >> 3) & 1, grp = c4 + db;
+        auto* p = (__attribute__((address_space(3))) s16x4*)(void*)((j ? t1 : t0) + ((row >> 3) << 11) +
+                                                                     ((grp >> 2) << 13) + ((grp & 3) << 9));
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+      };
+      constexpr int BH = DEC2_G2_AHEAD;  // d-blocks of A operands in flight
+      s16x4 n[BH][4];
+#pragma unroll
+      for (int j = 0; j < BH; ++j)
+        if (j < DB) {
+          n[j][0] = rdT(j, 0); n[j][1] = rdT(j, 8);
+          n[j][2] = rdT(j, 16); n[j][3] = rdT(j, 24);
+        }
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        const int jb = db % BH;
+        const s16x4 c00 = n[jb][0], c01 = n[jb][1], c10 = n[jb][2], c11 = n[jb][3];
+        if (db + BH < DB) {
+          n[jb][0] = rdT(db + BH, 0); n[jb][1] = rdT(db + BH, 8);
+          n[jb][2] = rdT(db + BH, 16); n[jb][3] = rdT(db + BH, 24);
+        }
+        const s16x8 a0 = {c00[0], c00[1], c00[2], c00[3], c01[0], c01[1], c01[2], c01[3]};
+        const s16x8 a1 = {c10[0], c10[1], c10[2], c10[3], c11[0], c11[1], c11[2], c11[3]};
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a0), pf[0], o[db], 0, 0, 0);
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a1), pf[1], o[db], 0, 0, 0);
+      }
+    }
+  };
+
+  constexpr int PRE = NS == 2 ? 2 : NS - 1;  // tiles in flight before the loop
+  if (t_beg < t_end) {
+#pragma unroll
+    for (int i = 0; i < PRE; ++i) issue(min(t_beg + i, t_end - 1), i);
+    wait_vmcnt<(PRE - 1) * PW>();
+  }
+  lds_fence();
+  __builtin_amdgcn_s_barrier();
+  lds_fence();
+  float bound = 0.f;
+  if (t_beg < t_end && wave_active) {
+    s_cur = gemm1(lds, [](int) {});
+    if (DS == 2) xput((int)(t_beg & 1), s_cur);
+  }
+  if (DS == 2) usq += usq_sh[(w ^ HALF) * 32 + col];
+  bound = sqrtf(usq) * emax * 1.02f;
+
+  for (int64_t t = t_beg; t < t_end; ++t) {
+    const bool more = t + 1 < t_end;
+    if (NS >= 3) wait_vmcnt<(NS >= 3 ? NS - 3 : 0) * PW>();
+    else wait_vmcnt<0>();
+    lds_fence();
+    __builtin_amdgcn_s_barrier();
+    lds_fence();
+    const int nxt = cur == NS - 1 ? 0 : cur + 1;
+    if (NS >= 3) issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
+    if (wave_active) {
+      if (DS == 2) xadd((int)(t & 1), s_cur);
+      if (t == ntiles - 1 && (N % kBfTI) != 0) {  // rows past N (read as 0) leave the softmax
+        const int64_t ib = t * kBfTI + 4 * h;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (ib + (r & 3) + 8 * (r >> 2) >= N) s_cur[r] = -INFINITY;
+      }
+      if (t == t_beg) {
+        // Fixed per-user offset, set once per split: m >= bound - kOffsetSpan keeps every
+        // p = exp(s - m) <= e^60 (no rescale of O ever); m >= first-tile max keeps the
+        // large terms normal. A split whose sum ends below e^-60 is flagged for exact
+        // recompute (its max term may have lost precision).
+        float mx = s_cur[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, s_cur[r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        m = fmaxf(mx, bound - kOffsetSpan);
+        mL = m * kLog2e;
+      }
+      // softmax of tile t (rows spread over GEMM1(t+1)'s MFMA pairs)
+      float pv[16];
+      uint32_t pk[8];
+      auto smax_rows = [&](int r0, int r1) {
+#pragma unroll
+        for (int r = r0; r < r1; ++r) {
+          pv[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_cur[r], kLog2e, -mL));
+          lsum += pv[r];
+          if (r & 1) pk[r >> 1] = pack_bf16x2(pv[r - 1], pv[r]);
+        }
+      };
+      f32x16 s_nx = s_cur;
+      if (more) {
+        constexpr int NG = KS / 2;
+        if constexpr (DS == 1) {  // all of U and O in registers: no room for the interleave (it spills)
+          smax_rows(0, 16);
+          s_nx = gemm1(lds + nxt * TB, [&](int) {});
+        } else {
+          s_nx = gemm1(lds + nxt * TB, [&](int g) { smax_rows(16 * g / NG, 16 * (g + 1) / NG); });
+        }
+        if (DS == 2) xput((int)((t + 1) & 1), s_nx);
+      } else {
+        smax_rows(0, 16);
+      }
+      bf16x8 pf[2];
+      pf[0] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+      pf[1] = __builtin_bit_cast(bf16x8, make_uint4(pk[4], pk[5], pk[6], pk[7]));
+      gemm2(pf);
+      s_cur = s_nx;
+    }
+    if (NS == 2) {  // the slot of tile t is free once every wave is past GEMM2(t)
+      lds_fence();
+      __builtin_amdgcn_s_barrier();
+      lds_fence();
+      if (t + 2 < t_end) issue(t + 2, cur);
+    }
+    cur = nxt;
+  }
+
+  if (!wave_active) return;
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  if (user >= nb) return;
+  if (h == 0 && dh == 0) {
+    const int f = !(ltot >= kMinL);
+    out.flag[out.direct ? user : (int64_t)split * nb + user] = f;
+  }
+  if (out.direct) {
+    const float inv = 1.0f / ltot;
+    if (h == 0 && dh == 0) out.lse[user] = m + logf(ltot);
+    if (WITH_O) {
+#pragma unroll
+      for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
+          *reinterpret_cast<float4*>(out.O + user * D + dd) =
+              make_float4(o[d][4 * g4] * inv, o[d][4 * g4 + 1] * inv, o[d][4 * g4 + 2] * inv, o[d][4 * g4 + 3] * inv);
+        }
+    }
+  } else {
+    const int64_t pi = (int64_t)split * nb + user;
+    if (h == 0 && dh == 0) { out.m[pi] = m; out.l[pi] = ltot; }
+    if (WITH_O) {
+#pragma unroll
+      for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
+          *reinterpret_cast<float4*>(out.O + pi * D + dd) =
+              make_float4(o[d][4 * g4], o[d][4 * g4 + 1], o[d][4 * g4 + 2], o[d][4 * g4 + 3]);
+        }
+    }
+  }
+}
+
 // ------------------------------------------------------------------- f32 ---
 // Same algorithm on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 sums):
 // 4 waves x 16 users, 16-item tiles, LDS rows padded to D+2 floats
@@ -697,25 +1061,68 @@ struct DecPlan {
   int64_t tiles_per_split;
   int64_t blocks;
   size_t lds;
+  int v2;    // bf16 version-2 sweep (k_dec2_bf16)
+  int ds;    // its D split (1 or 2)
+  int nw;    // its waves per block (4, or 8 with ds = 2)
+  int64_t upb;
 };
 
-static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
-  const int64_t upb = dtype == HVAE_BF16 ? kBfUsersPerBlock : kF32UsersPerBlock;
-  const int64_t ti = dtype == HVAE_BF16 ? kBfTI : kF32TI;
-  const int64_t target = dtype == HVAE_BF16 ? 256 : 512;
-  const int64_t nub = cdiv(nb, upb), tiles = cdiv(N, ti);
-  int64_t s = cdiv(target, nub);
-  s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 2));
-  s = std::min<int64_t>(s, std::max<int64_t>(1, N / std::max<int64_t>(1, 2 * nb)));
-  if (s >= 8) s = s / 8 * 8;
-  s = std::max<int64_t>(1, std::min<int64_t>(s, kMaxSplits));
-  DecPlan p;
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+// HVAE_DEC_V1=1 selects the version-1 bf16 sweep (transposed image copy), HVAE_DEC_SPLITS=k forces k item splits
+// (both for A/B measurements; read once per process).
+static bool dec_use_v1() {
+  static const int v = env_int("HVAE_DEC_V1", 0);
+  return v != 0;
+}
+static int dec_forced_splits() {
+  static const int v = env_int("HVAE_DEC_SPLITS", 0);
+  return v;
+}
+
+static int dec_forced_ds() {
+  static const int v = env_int("HVAE_DEC_DS", 0);
+  return v;
+}
+
+static int dec_forced_nw() {
+  static const int v = env_int("HVAE_DEC_NW", 0);
+  return v;
+}
+
+static bool v2_supported(int64_t D) { return D == 64 || D == 128 || D == 256 || D == 384 || D == 768; }
+
+static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
+  s = std::max<int64_t>(1, std::min<int64_t>(s, std::min<int64_t>(tiles, kMaxSplits)));
   p.tiles_per_split = cdiv(tiles, s);
   p.splits = (int)cdiv(tiles, p.tiles_per_split);
-  if (p.splits >= 8 && p.splits % 8) {  // keep "split shares an XCD" when possible
+}
+
+static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
+  DecPlan p{};
+  const bool bf = dtype == HVAE_BF16;
+  p.v2 = bf && !dec_use_v1() && v2_supported(D);
+  p.ds = p.v2 && (D > 384 || nb <= 64) ? 2 : 1;
+  if (p.v2 && D <= 384 && (dec_forced_ds() == 1 || dec_forced_ds() == 2)) p.ds = dec_forced_ds();
+  p.nw = p.v2 && p.ds == 2 && nb > 64 && D <= 384 ? 8 : 4;
+  if (p.v2 && p.ds == 2 && D <= 384 && (dec_forced_nw() == 4 || dec_forced_nw() == 8)) p.nw = dec_forced_nw();
+  p.upb = bf ? (p.v2 ? 32 * p.nw / p.ds : kBfUsersPerBlock) : kF32UsersPerBlock;
+  const int64_t ti = bf ? kBfTI : kF32TI;
+  const int64_t target = bf ? 256 : 512;
+  const int64_t nub = cdiv(nb, p.upb), tiles = cdiv(N, ti);
+  int64_t s = cdiv(target, nub);
+  s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 2));
+  // each split writes nb (D + 2) floats of partials: keep them below ~2x the E bytes it streams
+  s = std::min<int64_t>(s, std::max<int64_t>(1, (bf ? N : 2 * N) / std::max<int64_t>(1, 2 * nb)));
+  if (s >= 8) s = s / 8 * 8;
+  if (dec_forced_splits() > 0) s = dec_forced_splits();
+  dec_set_splits(p, tiles, s);
+  if (p.splits >= 8 && p.splits % 8 && dec_forced_splits() <= 0) {  // keep "split shares an XCD" when possible
     const int64_t s8 = (int64_t)p.splits / 8 * 8;
-    p.tiles_per_split = cdiv(tiles, s8);
-    p.splits = (int)cdiv(tiles, p.tiles_per_split);
+    dec_set_splits(p, tiles, s8);
   }
   p.blocks = nub * p.splits;
   p.lds = 0;
@@ -747,6 +1154,31 @@ static int launch_bf16(const float* U, int64_t ldu, const void* E, const float* 
   return HVAE_OK;
 }
 
+template <int D, int DS, int NW, bool WO>
+static int launch_bf16_v2_nw(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                             const DecPlan& p, DecOut o, hipStream_t st) {
+  constexpr int lds = d2_lds_bytes<D, DS, NW>();
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec2_bf16<D, DS, NW, WO>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr_set = true;
+  }
+  k_dec2_bf16<D, DS, NW, WO><<<(unsigned)p.blocks, 64 * NW, lds, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N,
+                                                                       p.splits, p.tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec2_bf16");
+  return HVAE_OK;
+}
+
+template <int D, int DS, bool WO>
+static int launch_bf16_v2(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                          const DecPlan& p, DecOut o, hipStream_t st) {
+  if constexpr (DS == 2 && d2_stages<D, 2, 8>() >= 3) {
+    if (p.nw == 8) return launch_bf16_v2_nw<D, 2, 8, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+  }
+  return launch_bf16_v2_nw<D, DS, 4, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+}
+
 template <int D, bool WO>
 static int launch_f32(const float* U, int64_t ldu, const void* E, int64_t nb, int64_t N, const DecPlan& p,
                       DecOut o, hipStream_t st) {
@@ -765,7 +1197,26 @@ static int launch_f32(const float* U, int64_t ldu, const void* E, int64_t nb, in
 template <bool WO>
 static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb,
                     int64_t N, int64_t D, const DecPlan& p, DecOut o, hipStream_t st) {
-  if (dtype == HVAE_BF16) {
+  if (dtype == HVAE_BF16 && p.v2) {
+    if (p.ds == 1) {
+      switch (D) {
+        case 64: return launch_bf16_v2<64, 1, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        case 128: return launch_bf16_v2<128, 1, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        case 256: return launch_bf16_v2<256, 1, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        case 384: return launch_bf16_v2<384, 1, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        default: break;
+      }
+    } else {
+      switch (D) {
+        case 64: return launch_bf16_v2<64, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        case 128: return launch_bf16_v2<128, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        case 256: return launch_bf16_v2<256, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        case 384: return launch_bf16_v2<384, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        case 768: return launch_bf16_v2<768, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        default: break;
+      }
+    }
+  } else if (dtype == HVAE_BF16) {
     switch (D) {
       case 64: return launch_bf16<64, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 128: return launch_bf16<128, WO>(U, ldu, E, enorm, nb, N, p, o, st);
@@ -792,7 +1243,7 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
 using namespace hvae;
 
 extern "C" int hvae_decoder_supported(int dtype, int64_t D) {
-  if (dtype == HVAE_BF16) return D == 64 || D == 128 || D == 256 || D == 384;
+  if (dtype == HVAE_BF16) return D == 64 || D == 128 || D == 256 || D == 384 || (D == 768 && !dec_use_v1());
   if (dtype == HVAE_F32) return D == 32 || D == 64 || D == 128 || D == 256 || D == 384;
   return 0;
 }
@@ -848,6 +1299,7 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
                    (!O || ((uintptr_t)O % 16) == 0),
                "hvae decoder: U/E/O must be 16-B aligned with ldu %% 4 == 0");
   HVAE_REQUIRE(N < (1ll << 31), "hvae decoder: N too large");
+  HVAE_REQUIRE(dtype != HVAE_BF16 || N * D * 2 < (1ll << 31), "hvae decoder: bf16 E image over 2 GiB");
   HVAE_REQUIRE(!x || (E32 && x->row_ptr && x->nb == nb && x->n_items == N), "hvae decoder: bad CSR batch");
   if (nb == 0) return HVAE_OK;
   DecPlan p = dec_plan(dtype, nb, N, D);
@@ -857,9 +1309,8 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
     int64_t fit = p.splits;
     while (fit > 1 && ws_bytes < dec_ws_bytes((int)fit, nb, D)) fit = fit * 3 / 4;
     const int64_t tiles = cdiv(N, dtype == HVAE_BF16 ? kBfTI : kF32TI);
-    p.tiles_per_split = cdiv(tiles, fit);
-    p.splits = (int)cdiv(tiles, p.tiles_per_split);
-    p.blocks = cdiv(nb, dtype == HVAE_BF16 ? kBfUsersPerBlock : kF32UsersPerBlock) * p.splits;
+    dec_set_splits(p, tiles, fit);
+    p.blocks = cdiv(nb, p.upb) * p.splits;
   }
   const bool bf = dtype == HVAE_BF16;
   const bool want_o = O || dU;

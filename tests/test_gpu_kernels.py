@@ -201,6 +201,16 @@ def test_reparam_kl(ops, hip_device):
 @pytest.mark.parametrize("nb,N,D", [(3, 50, 384), (64, 890, 384), (200, 12101, 384), (130, 1000, 128),
                                     (17, 333, 64), (300, 5000, 256)])
 def test_decoder(ops, hip_device, dtype, nb, N, D):
+    _check_decoder(ops, hip_device, dtype, nb, N, D)
+
+
+@pytest.mark.parametrize("nb,N,D", [(64, 2000, 768), (300, 5001, 768), (7, 100, 768)])
+def test_decoder_bf16_d768(ops, hip_device, nb, N, D):
+    """Syn-10M's d = 768 (BASELINE configs[3]): the D-split bf16 sweep (two waves per user group)."""
+    _check_decoder(ops, hip_device, "bf16", nb, N, D)
+
+
+def _check_decoder(ops, hip_device, dtype, nb, N, D):
     E = torch.as_tensor(synth_embeddings(N, D, seed=N))
     g = torch.Generator().manual_seed(nb)
     U = torch.randn(nb, D, generator=g) * 3.0
@@ -266,6 +276,15 @@ def test_decoder_bwd_sparse(ops, hip_device):
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("nb,N,D", [(40, 700, 384), (64, 12101, 384), (5, 3000, 128), (256, 2000, 64)])
 def test_decoder_train_fused(ops, hip_device, dtype, nb, N, D):
+    _check_decoder_train_fused(ops, hip_device, dtype, nb, N, D)
+
+
+@pytest.mark.parametrize("nb,N,D", [(64, 3000, 768), (130, 4000, 768)])
+def test_decoder_train_fused_d768(ops, hip_device, nb, N, D):
+    _check_decoder_train_fused(ops, hip_device, "bf16", nb, N, D)
+
+
+def _check_decoder_train_fused(ops, hip_device, dtype, nb, N, D):
     """Sweep + merge + sparse terms in one finalize launch == decoder_fwd + decoder_bwd == torch autograd."""
     X = synth_csr(nb, N, lam=5.0, seed=nb + N)
     x = torch.as_tensor(X.toarray(), dtype=torch.float32)
