@@ -44,6 +44,11 @@ WORKLOADS = {
     # configs[2]: synthetic 1M users x 100K items, d=384, batch 4096 (hidden [512], latent 128)
     "syn1m": dict(users=1_000_000, items=100_000, d=384, latent=128, hidden=[512], batch=4096, lam=15.0,
                   dropout=0.3, beta=0.2, lr=1e-3),
+    # configs[3]: synthetic 10M users x 1M items, d=768, batch 4096 per GPU. Each rank generates only its
+    # own 10M / 8 users (a dense 10M-row matrix per rank would not fit host memory 8 times over); the CPU
+    # baseline runs B = 256 (the dense B x N batch of the reference loader is 16 GB at 4096)
+    "syn10m": dict(users=10_000_000, items=1_000_000, d=768, latent=128, hidden=[512], batch=4096, lam=15.0,
+                   dropout=0.3, beta=0.2, lr=1e-3, shard_gen=True, cpu_batch=256),
 }
 
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md, spec)
@@ -57,8 +62,11 @@ def log(*a):
 
 def make_data(w: dict, rank: int, world: int):
     from gen import synth_csr, synth_embeddings
-    X = synth_csr(w["users"], w["items"], lam=w["lam"], seed=0)
     E = synth_embeddings(w["items"], w["d"], seed=1)
+    if w.get("shard_gen"):  # this rank's users only (a 1/8 shard: the 8-GPU split), from a per-rank seed
+        X = synth_csr(w["users"] // 8, w["items"], lam=w["lam"], seed=1000 + rank)
+        return X, E, np.arange(X.shape[0])
+    X = synth_csr(w["users"], w["items"], lam=w["lam"], seed=0)
     users = np.arange(rank, w["users"], world)  # each rank owns a disjoint user shard
     return X, E, users
 
@@ -83,7 +91,7 @@ def cpu_baseline(w: dict, X, E, seconds: float) -> dict:
     from oracle import ref_cpu as R
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    B = w["batch"]
+    B = w.get("cpu_batch", w["batch"])
     p = R.init_params(w["items"], E, w["latent"], w["hidden"], seed=0)
     state = {}
     rng = np.random.default_rng(0)

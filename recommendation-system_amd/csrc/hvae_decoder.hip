@@ -861,8 +861,13 @@ struct FinArgs {
   const float* kl_rows; float beta; float* loss3; double* accum3; unsigned* ticket;  // fused loss (optional)
 };
 
+// GRP: the merge of many split partials (> 8) by split groups (memory-level parallelism at small
+// batches); otherwise one thread per column walks the splits in order (fewer registers, more blocks
+// per CU at large batches)
+template <bool GRP>
 __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   __shared__ float wsh[kMaxSplits];
+  __shared__ __attribute__((aligned(16))) float opart[GRP ? 8 * 1024 : 4];  // per-split-group O sums
   __shared__ float red[4];
   __shared__ float pbuf[256];
   __shared__ int any_flag;
@@ -895,7 +900,7 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     L = block_sum<256>(L, red);  // its barriers also publish wsh and any_flag
     lse_b = M + logf(L);
     const float inv = 1.0f / L;
-    if (a.pO) {
+    if (a.pO && !GRP) {
       // sum_s w_s O_s in split order; loads batched 8 splits x 4 columns deep so that
       // they are in flight together (a one-at-a-time chain is HBM-latency bound)
       const int nk = (int)min<int64_t>(4, (D - tid + 255) / 256);
@@ -920,6 +925,56 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
           if (k < nk) acc[k] += wsh[s0] * base[(int64_t)s0 * sstride + 256 * k];
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = acc[k] * inv;
+    }
+    if constexpr (GRP) if (a.pO) {
+      // sum_s w_s O_s (many splits): 8 split groups x 32 float4-column lanes, thread (sg, cq) sums splits sg, sg + 8, ...
+      // over float4 columns cq + 32 i, 4 splits' loads in flight together (one HBM latency per 32 splits
+      // instead of a chain); the 8 group sums are then added in group order through LDS (deterministic)
+      constexpr int SG = 8;
+      const int sg = tid >> 5, cq = tid & 31;
+      const int nq = (int)(D >> 2);
+      float4 acc4[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int s0 = sg; s0 < a.splits; s0 += SG * 4) {
+        float4 v[4][8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int sj = s0 + SG * j;
+          const float4* row = reinterpret_cast<const float4*>(a.pO + ((int64_t)sj * a.nb + b) * D);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int q = cq + 32 * i;
+            v[j][i] = (sj < a.splits && q < nq) ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int sj = s0 + SG * j;
+          const float wv = sj < a.splits ? wsh[sj] : 0.f;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            acc4[i].x += wv * v[j][i].x; acc4[i].y += wv * v[j][i].y;
+            acc4[i].z += wv * v[j][i].z; acc4[i].w += wv * v[j][i].w;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int q = cq + 32 * i;
+        if (q < nq) reinterpret_cast<float4*>(opart + sg * 1024)[q] = acc4[i];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t d = tid + 256 * k;
+        float t = 0.f;
+        if (d < D) {
+#pragma unroll
+          for (int g = 0; g < SG; ++g) t += opart[g * 1024 + d];
+        }
+        o[k] = t * inv;
+      }
     }
   } else {
     if (a.flag && a.flag[b]) any_flag = 1;
@@ -1362,7 +1417,8 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
     if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   }
   ProbeScope probe("decoder_finalize", st);
-  k_dec_finalize<<<(unsigned)nb, 256, 0, st>>>(a);
+  if (p.splits > 8) k_dec_finalize<true><<<(unsigned)nb, 256, 0, st>>>(a);
+  else k_dec_finalize<false><<<(unsigned)nb, 256, 0, st>>>(a);
   HVAE_LAUNCH_CHECK("k_dec_finalize");
   return HVAE_OK;
 }
@@ -1403,7 +1459,7 @@ extern "C" int hvae_decoder_bwd(const hvae_csr_batch* x, const float* U, int64_t
   a.lse_out = const_cast<float*>(lse);  // rewritten with the same value
   a.recon_rows = recon_rows;
   a.dU = dU;
-  k_dec_finalize<<<(unsigned)x->nb, 256, 0, as_stream(stream)>>>(a);
+  k_dec_finalize<false><<<(unsigned)x->nb, 256, 0, as_stream(stream)>>>(a);
   HVAE_LAUNCH_CHECK("k_dec_finalize");
   return HVAE_OK;
 }

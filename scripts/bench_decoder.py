@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--D", type=int, default=384)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--train", action="store_true", help="time hvae_decoder_train (sweep + finalize with the CSR "
+                                                          "batch's sparse terms) instead of hvae_decoder_fwd")
+    ap.add_argument("--probe", default="decoder_sweep", choices=["decoder_sweep", "decoder_finalize"])
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -39,18 +42,26 @@ def main():
     else:
         E = ops.decoder_image(E32)
         enorm = ops.row_norm_max(E)
-    ops.decoder_fwd(U, E, enorm)  # warm-up (and kernel attributes)
+    if args.train:
+        sys.path.insert(0, str(ROOT / "tests" / "golden"))
+        from gen import synth_csr
+        x = ops.csr_from_scipy(synth_csr(args.nb, args.N, lam=3.0, seed=5), dev)
+        step = lambda: ops.decoder_train(x, U, E, enorm, E32, 1.0 / args.nb)  # noqa: E731
+    else:
+        step = lambda: ops.decoder_fwd(U, E, enorm)  # noqa: E731
+    step()  # warm-up (and kernel attributes)
     torch.cuda.synchronize()
-    check(lib().hvae_probe_arm(b"decoder_sweep", 4 * args.reps), "probe_arm")
+    check(lib().hvae_probe_arm(args.probe.encode(), 4 * args.reps), "probe_arm")
     for _ in range(args.reps):
-        ops.decoder_fwd(U, E, enorm)
+        step()
     torch.cuda.synchronize()
     avg, n = C.c_double(), C.c_int()
     check(lib().hvae_probe_collect(C.byref(avg), C.byref(n)), "probe_collect")
     check(lib().hvae_probe_arm(None, 0), "probe_disarm")
     us = avg.value
     flops = 4.0 * args.nb * args.N * args.D
-    print(json.dumps({"nb": args.nb, "N": args.N, "D": args.D, "dtype": args.dtype, "launches": n.value,
+    print(json.dumps({"nb": args.nb, "N": args.N, "D": args.D, "dtype": args.dtype, "probe": args.probe,
+                      "launches": n.value,
                       "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 1)}), flush=True)
 
 
