@@ -191,6 +191,23 @@ int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, flo
                   const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
                   int64_t ldc, const hvae_epilogue* epi, void* ws, size_t ws_bytes, void* stream);
 size_t hvae_gemm_f32_workspace(int64_t M, int64_t N, int64_t K);
+/* One problem of hvae_gemm_f32_pair: hvae_gemm_f32's arguments, with its own workspace. */
+typedef struct hvae_gemm_desc {
+  int trans_a, trans_b;
+  int64_t M, N, K;
+  float alpha;
+  const float* A; int64_t lda;
+  const float* B; int64_t ldb;
+  float beta;
+  float* C; int64_t ldc;
+  const hvae_epilogue* epi;
+  void* ws; size_t ws_bytes;
+} hvae_gemm_desc;
+/* Two independent GEMMs of one layer's backward -- the weight gradient (w: trans_a = 1,
+ * trans_b = 0) and the data gradient (x: both 0) -- in one launch (the two matmuls autograd
+ * runs for each nn.Linear of model.py:100-155 in backward). Other pairings run as two
+ * hvae_gemm_f32 launches. Split-K problems need distinct workspaces. */
+int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc* x, void* stream);
 
 /* out[n] = beta * out[n] + sum_m X[m, n]  (bias gradients; deterministic) */
 int hvae_colsum(const float* X, int64_t M, int64_t N, int64_t ldx, float beta, float* out,

@@ -353,17 +353,21 @@ constexpr float kMinL = 8.75651e-27f;
 
 template <int D, int DS>
 constexpr int d2_tile_bytes() { return ((D + 127) / 128) * 8192; }
-template <int DS, int NW>
-constexpr int d2_xbytes() { return DS == 2 ? 2 * NW * 4096 : 0; }
+// DS = 2 exchange buffers: double-buffered by tile parity, or single (one more barrier per tile) where the
+// tile is large (d = 768) so that the ring keeps three stages
+template <int D>
+constexpr int d2_xbufs() { return D > 384 ? 1 : 2; }
+template <int D, int DS, int NW>
+constexpr int d2_xbytes() { return DS == 2 ? d2_xbufs<D>() * NW * 4096 : 0; }
 template <int D, int DS, int NW>
 constexpr int d2_stages() {
-  return (160 * 1024 - d2_xbytes<DS, NW>() - 1024) / d2_tile_bytes<D, DS>() >= 6
+  return (160 * 1024 - d2_xbytes<D, DS, NW>()) / d2_tile_bytes<D, DS>() >= 6
              ? 6
-             : (160 * 1024 - d2_xbytes<DS, NW>() - 1024) / d2_tile_bytes<D, DS>();
+             : (160 * 1024 - d2_xbytes<D, DS, NW>()) / d2_tile_bytes<D, DS>();
 }
 template <int D, int DS, int NW>
 constexpr int d2_lds_bytes() {
-  return d2_stages<D, DS, NW>() * d2_tile_bytes<D, DS>() + d2_xbytes<DS, NW>() + 1024;
+  return d2_stages<D, DS, NW>() * d2_tile_bytes<D, DS>() + d2_xbytes<D, DS, NW>();
 }
 
 // LDS image of one 32-item tile (version 2): per 128-column segment (8 KiB) 8-row x 32-column
@@ -398,8 +402,8 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   static_assert(DW % 32 == 0 && KS % 2 == 0, "D / DS must be a multiple of 32");
   static_assert(NS >= 2, "LDS ring too small");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  float* xbuf = reinterpret_cast<float*>(lds + NS * TB);                        // [2][4 w][4 r4][64 lane][4]
-  float* usq_sh = reinterpret_cast<float*>(lds + NS * TB + d2_xbytes<DS, NW>());  // [NW w][32]
+  constexpr int XB = d2_xbufs<D>();
+  float* xbuf = reinterpret_cast<float*>(lds + NS * TB);                        // [XB][NW w][4 r4][64 lane][4]
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -429,8 +433,18 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
     uf[ks] = make_uint4(pack_bf16x2(a.x, a.y), pack_bf16x2(a.z, a.w), pack_bf16x2(b.x, b.y),
                         pack_bf16x2(b.z, b.w));
   }
+  if constexpr (DS == 2) {  // |u| over the partner's half too (the score bound needs the whole row)
+    const int obase = (1 - dh) * DW;
+#pragma unroll 1
+    for (int ks = 0; ks < KS; ++ks) {
+      if (user < nb) {
+        const float4 a = *reinterpret_cast<const float4*>(U + user * ldu + obase + 16 * ks + 8 * h);
+        const float4 b = *reinterpret_cast<const float4*>(U + user * ldu + obase + 16 * ks + 8 * h + 4);
+        usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+      }
+    }
+  }
   usq += __shfl_xor(usq, 32, 64);
-  if (DS == 2 && h == 0) usq_sh[w * 32 + col] = usq;
 
   // LDS-DMA source offsets of this lane's pieces (tile-relative) and the buffer
   // resource over bf16 E [N][D] (bounds = N D 2 bytes: tail rows read 0)
@@ -503,14 +517,14 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   };
   // DS = 2: this wave's partial S^T of a tile <-> its partner's, [r4][lane] float4 rows
   auto xput = [&](int par, const f32x16& s) {
-    float* xb = xbuf + ((par * NW + w) * 4) * 256;
+    float* xb = xbuf + (((par % XB) * NW + w) * 4) * 256;
 #pragma unroll
     for (int r4 = 0; r4 < 4; ++r4)
       *reinterpret_cast<float4*>(xb + r4 * 256 + lane * 4) = make_float4(s[4 * r4], s[4 * r4 + 1], s[4 * r4 + 2],
                                                                          s[4 * r4 + 3]);
   };
   auto xadd = [&](int par, f32x16& s) {
-    const float* xb = xbuf + ((par * NW + (w ^ HALF)) * 4) * 256;
+    const float* xb = xbuf + (((par % XB) * NW + (w ^ HALF)) * 4) * 256;
 #pragma unroll
     for (int r4 = 0; r4 < 4; ++r4) {
       const float4 v = *reinterpret_cast<const float4*>(xb + r4 * 256 + lane * 4);
@@ -580,7 +594,6 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
     s_cur = gemm1(lds, [](int) {});
     if (DS == 2) xput((int)(t_beg & 1), s_cur);
   }
-  if (DS == 2) usq += usq_sh[(w ^ HALF) * 32 + col];
   bound = sqrtf(usq) * emax * 1.02f;
 
   for (int64_t t = t_beg; t < t_end; ++t) {
@@ -592,13 +605,19 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
     lds_fence();
     const int nxt = cur == NS - 1 ? 0 : cur + 1;
     if (NS >= 3) issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
+    if constexpr (DS == 2 && XB == 1) {  // single exchange buffer: everyone has read S(t) before S(t+1) lands
+      if (wave_active) xadd((int)(t & 1), s_cur);
+      lds_fence();
+      __builtin_amdgcn_s_barrier();
+      lds_fence();
+    }
     if (wave_active) {
-      if (DS == 2) xadd((int)(t & 1), s_cur);
+      if (DS == 2 && XB == 2) xadd((int)(t & 1), s_cur);
       if (t == ntiles - 1 && (N % kBfTI) != 0) {  // rows past N (read as 0) leave the softmax
-        const int64_t ib = t * kBfTI + 4 * h;
+        const int lim = (int)(N - t * kBfTI) - 4 * h;  // rows of this lane's half at or past it are tail
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          if (ib + (r & 3) + 8 * (r >> 2) >= N) s_cur[r] = -INFINITY;
+          s_cur[r] = ((r & 3) + 8 * (r >> 2) >= lim) ? -INFINITY : s_cur[r];
       }
       if (t == t_beg) {
         // Fixed per-user offset, set once per split: m >= bound - kOffsetSpan keeps every
@@ -626,12 +645,7 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
       f32x16 s_nx = s_cur;
       if (more) {
         constexpr int NG = KS / 2;
-        if constexpr (DS == 1) {  // all of U and O in registers: no room for the interleave (it spills)
-          smax_rows(0, 16);
-          s_nx = gemm1(lds + nxt * TB, [&](int) {});
-        } else {
-          s_nx = gemm1(lds + nxt * TB, [&](int g) { smax_rows(16 * g / NG, 16 * (g + 1) / NG); });
-        }
+        s_nx = gemm1(lds + nxt * TB, [&](int g) { smax_rows(16 * g / NG, 16 * (g + 1) / NG); });
         if (DS == 2) xput((int)((t + 1) & 1), s_nx);
       } else {
         smax_rows(0, 16);

@@ -544,6 +544,166 @@ __global__ void __launch_bounds__(1024) k_rg_scan_small(int32_t* __restrict__ cn
   }
 }
 
+// Whole plan in one block for small batches (rg->cap <= kPlanSmallCap nonzeros): the batch's
+// (item, batch row) pairs are gathered into LDS, bitonic-sorted by item then row, and the slots,
+// segments and sorted contributions are read off the sorted list -- the same outputs as
+// count / scan / scatter / sort, in one launch and without touching the per-item counters.
+constexpr int kPlanSmallCap = 4096;
+constexpr int kPlanSmallRows = 4096;
+
+// exclusive block scan of v over 1024 threads (result + total)
+__device__ __forceinline__ int block_excl_scan_1024(int v, int* wsum, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int incl = wave_incl_scan(v, lane);
+  __syncthreads();
+  if (lane == 63) wsum[w] = incl;
+  __syncthreads();
+  int pre = 0;
+  total = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    if (k < w) pre += wsum[k];
+    total += wsum[k];
+  }
+  return pre + incl - v;
+}
+
+__global__ void __launch_bounds__(1024) k_rg_plan_small(const int64_t* __restrict__ row_ptr,
+                                                        const int32_t* __restrict__ col_idx,
+                                                        const float* __restrict__ vals,
+                                                        const int32_t* __restrict__ rows,
+                                                        const int64_t* __restrict__ rows_offset, int64_t nb,
+                                                        int32_t* __restrict__ slot_of, int32_t* __restrict__ item_of,
+                                                        int32_t* __restrict__ seg_off,
+                                                        int32_t* __restrict__ contrib_row,
+                                                        float* __restrict__ contrib_val,
+                                                        int32_t* __restrict__ contrib_slot,
+                                                        int32_t* __restrict__ n_unique) {
+  __shared__ unsigned long long key[kPlanSmallCap];
+  __shared__ float kv[kPlanSmallCap];
+  __shared__ int roff[kPlanSmallRows + 1];
+  __shared__ int64_t rbeg[kPlanSmallRows];
+  __shared__ int wsum[16];
+  const int tid = threadIdx.x;
+  const int nbi = (int)nb;
+  // row lengths -> exclusive offsets (4 rows per thread)
+  int len4[4], tot4 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = tid * 4 + i;
+    len4[i] = 0;
+    if (b < nbi) {
+      const int64_t r = batch_row(rows, rows_offset, b);
+      const int64_t beg = row_ptr[r];
+      rbeg[b] = beg;
+      len4[i] = (int)(row_ptr[r + 1] - beg);
+    }
+    tot4 += len4[i];
+  }
+  int T = 0;
+  int o = block_excl_scan_1024(tot4, wsum, T);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int b = tid * 4 + i;
+    if (b < nbi) roff[b] = o;
+    o += len4[i];
+  }
+  if (tid == 0) roff[nbi] = T;
+  __syncthreads();
+  int P = 64;
+  while (P < T) P <<= 1;
+  // entries: key = item << 32 | batch row; the row of entry e by binary search in roff
+  for (int e = tid; e < P; e += 1024) {
+    if (e < T) {
+      int lo = 0, hi = nbi - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (roff[mid] <= e) lo = mid; else hi = mid - 1;
+      }
+      const int64_t src = rbeg[lo] + (e - roff[lo]);
+      key[e] = ((unsigned long long)(uint32_t)col_idx[src] << 32) | (uint32_t)lo;
+      kv[e] = vals[src];
+    } else {
+      key[e] = ~0ull;
+      kv[e] = 0.f;
+    }
+  }
+  __syncthreads();
+  if (P <= 1024) {
+    // one element per thread: distances < 64 in registers (wave shuffles), larger ones through LDS
+    const int lane = tid & 63;
+    unsigned long long a = tid < P ? key[tid] : ~0ull;
+    float av = tid < P ? kv[tid] : 0.f;
+    for (int k = 2; k <= P; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        unsigned long long b;
+        float bv;
+        if (j < 64) {
+          const uint32_t lo = __shfl_xor((uint32_t)a, j, 64), hi = __shfl_xor((uint32_t)(a >> 32), j, 64);
+          b = ((unsigned long long)hi << 32) | lo;
+          bv = __shfl_xor(av, j, 64);
+        } else {
+          __syncthreads();
+          key[tid] = a;
+          kv[tid] = av;
+          __syncthreads();
+          b = key[tid ^ j];
+          bv = kv[tid ^ j];
+        }
+        const bool keep_min = ((tid & k) == 0) == ((tid & j) == 0);
+        if (keep_min ? (b < a) : (b > a)) { a = b; av = bv; }
+      }
+    (void)lane;
+    __syncthreads();
+    if (tid < P) { key[tid] = a; kv[tid] = av; }
+    __syncthreads();
+  } else
+  for (int k = 2; k <= P; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < P; i += 1024) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const bool up = (i & k) == 0;
+          const unsigned long long a = key[i], c = key[ixj];
+          if ((a > c) == up) {
+            key[i] = c; key[ixj] = a;
+            const float t = kv[i]; kv[i] = kv[ixj]; kv[ixj] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  // segment heads -> slots (4 consecutive entries per thread)
+  int f4[4], nf = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid * 4 + i;
+    f4[i] = (e < T) && (e == 0 || (key[e] >> 32) != (key[e - 1] >> 32));
+    nf += f4[i];
+  }
+  int NU = 0;
+  int sl = block_excl_scan_1024(nf, wsum, NU) - 1;  // slot of the entry before this thread's first
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int e = tid * 4 + i;
+    if (e >= T) break;
+    sl += f4[i];
+    const int item = (int)(key[e] >> 32);
+    if (f4[i]) {
+      item_of[sl] = item;
+      seg_off[sl] = e;
+      slot_of[item] = sl;
+    }
+    contrib_row[e] = (int32_t)(key[e] & 0xffffffffu);
+    contrib_val[e] = kv[e];
+    contrib_slot[e] = sl;
+  }
+  if (tid == 0) {
+    *n_unique = NU;
+    seg_off[NU] = T;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_rg_scatter(const int64_t* __restrict__ row_ptr,
                                                     const int32_t* __restrict__ col_idx,
                                                     const float* __restrict__ vals,
@@ -774,6 +934,58 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
   }
 }
 
+// Small batches (the one-block plan): one wave per segment sums its contributions in ascending
+// batch row straight into the segment's row (no chunk partials, no span pass). Loads batched 8 deep.
+template <int NV>
+__global__ void __launch_bounds__(256) k_rg_apply_seg(const int32_t* __restrict__ n_unique,
+                                                      const int32_t* __restrict__ seg_off,
+                                                      const int32_t* __restrict__ contrib_row,
+                                                      const float* __restrict__ contrib_val,
+                                                      const float* __restrict__ da, int64_t H,
+                                                      float* __restrict__ out_rows) {
+  const int nu = *n_unique;
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
+  for (int s = gw; s < nu; s += nw) {
+    const int beg = seg_off[s], len = seg_off[s + 1] - beg;
+    float4 acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i0 = 0; i0 < len; i0 += 64) {
+      const int n = min(64, len - i0);
+      const int mb = lane < n ? contrib_row[beg + i0 + lane] : 0;
+      const float mx = lane < n ? contrib_val[beg + i0 + lane] : 0.f;
+      for (int j0 = 0; j0 < n; j0 += 8) {
+        float4 d[8][NV];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int b = __shfl(mb, min(j0 + j, 63));
+#pragma unroll
+          for (int k = 0; k < NV; ++k) {
+            const int64_t col = 4 * (int64_t)(lane + 64 * k);
+            d[j][k] = (j0 + j < n && col < H) ? *reinterpret_cast<const float4*>(da + (int64_t)b * H + col)
+                                              : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float x = (j0 + j < n) ? __shfl(mx, min(j0 + j, 63)) : 0.f;
+#pragma unroll
+          for (int k = 0; k < NV; ++k) {
+            acc[k].x += x * d[j][k].x; acc[k].y += x * d[j][k].y;
+            acc[k].z += x * d[j][k].z; acc[k].w += x * d[j][k].w;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int64_t col = 4 * (int64_t)(lane + 64 * k);
+      if (col < H) *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + col) = acc[k];
+    }
+  }
+}
+
 // Segments cut by chunk edges: first chunk's partial (head if the segment starts the
 // chunk, else tail) + the head partials of the following chunks, in chunk order.
 __global__ void __launch_bounds__(256) k_rg_span(const int32_t* __restrict__ n_unique,
@@ -959,6 +1171,15 @@ extern "C" int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad*
     HVAE_HIP(hipMemsetAsync(rg->n_unique, 0, sizeof(int32_t), st));
     return HVAE_OK;
   }
+  if (rg->cap <= kPlanSmallCap && x->nb <= kPlanSmallRows) {  // the whole plan in one block
+    HVAE_REQUIRE(rg->contrib_slot, "hvae_w1_rowgrad_plan: null contrib_slot");
+    ProbeScope probe("rowgrad_plan", st);
+    k_rg_plan_small<<<1, 1024, 0, st>>>(x->row_ptr, x->col_idx, x->vals, x->rows, x->rows_offset, x->nb,
+                                        rg->slot_of, rg->item_of, rg->seg_off, rg->contrib_row, rg->contrib_val,
+                                        rg->contrib_slot, rg->n_unique);
+    HVAE_LAUNCH_CHECK("k_rg_plan_small");
+    return HVAE_OK;
+  }
   const unsigned rgrid = (unsigned)cdiv(x->nb, 4);
   k_rg_count<<<rgrid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->rows, x->rows_offset, x->nb, rg->cnt);
   HVAE_LAUNCH_CHECK("k_rg_count");
@@ -1004,9 +1225,16 @@ extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowg
   HVAE_REQUIRE(rg->contrib_slot && rg->part && rg->part_floats >= hvae_rowgrad_part_floats(rg->cap, H),
                "hvae_w1_rowgrad_apply: part scratch too small for H");
   hipStream_t st = as_stream(stream);
+  ProbeScope probe("rowgrad_apply", st);
+  if (rg->cap <= kPlanSmallCap) {
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, 4), 1024));
+    HVAE_NV_DISPATCH(H, (k_rg_apply_seg<NV><<<grid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
+                                                                  rg->contrib_val, da, H, rg->rows)));
+    HVAE_LAUNCH_CHECK("k_rg_apply_seg");
+    return HVAE_OK;
+  }
   const int ch = rg_chunk(rg->cap);
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(rg->cap, ch), 4), 4096));
-  ProbeScope probe("rowgrad_apply", st);
   HVAE_NV_DISPATCH(H, (k_rg_apply<NV><<<grid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
                                                             rg->contrib_val, rg->contrib_slot, da, H, ch, rg->rows,
                                                             rg->part)));

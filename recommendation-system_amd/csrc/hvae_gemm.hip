@@ -100,21 +100,44 @@ __device__ __forceinline__ float4 load4(const float* __restrict__ p, int64_t idx
   return r;
 }
 
+// One GEMM problem of a launch (hvae_gemm_f32, or one half of hvae_gemm_f32_pair).
+struct GemmP {
+  int64_t M, N, K, kps;
+  float alpha;
+  const float* A; int64_t lda;
+  const float* B; int64_t ldb;
+  float beta;
+  float* C; int64_t ldc;
+  float* slab; unsigned* tickets;
+  EpiArgs ep;
+  bool vec_a, vec_b;
+  unsigned gx, gy, gz;  // tiles along N, along M, k splits
+};
+
+template <int BM>
+constexpr int gemm_smem_floats() { return 2 * GTile<BM>::IMG; }
+
+// The block (bx, by, bz) of problem g: tile rows by*BM.., columns bx*BN.., k split bz.
 template <bool TA, bool TB, int BM, int BN>
-__global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t K, int64_t k_per_split,
-                                                  float alpha, const float* __restrict__ A, int64_t lda,
-                                                  const float* __restrict__ B, int64_t ldb, float beta,
-                                                  float* __restrict__ C, int64_t ldc,
-                                                  float* __restrict__ slab, unsigned* __restrict__ tickets,
-                                                  EpiArgs ep, bool vec_a, bool vec_b) {
+__device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned by, unsigned bz,
+                                           float* __restrict__ sA_, float* __restrict__ sB_) {
   using TAo = GTile<BM>;
   using TBo = GTile<BN>;
   constexpr int IM = BM / 32, JN = BN / 32;  // 16x16 MFMA tiles per wave
-  __shared__ __attribute__((aligned(16))) float sA[2][TAo::IMG];
-  __shared__ __attribute__((aligned(16))) float sB[2][TBo::IMG];
+  const int64_t M = g.M, N = g.N, K = g.K, k_per_split = g.kps, lda = g.lda, ldb = g.ldb, ldc = g.ldc;
+  const float alpha = g.alpha, beta = g.beta;
+  const float* __restrict__ A = g.A;
+  const float* __restrict__ B = g.B;
+  float* __restrict__ C = g.C;
+  float* __restrict__ slab = g.slab;
+  unsigned* __restrict__ tickets = g.tickets;
+  const EpiArgs& ep = g.ep;
+  const bool vec_a = g.vec_a, vec_b = g.vec_b;
+  auto sA = [&](int buf) { return sA_ + buf * TAo::IMG; };
+  auto sB = [&](int buf) { return sB_ + buf * TBo::IMG; };
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int64_t m0 = (int64_t)blockIdx.y * BM, n0 = (int64_t)blockIdx.x * BN;
-  const int64_t kb = (int64_t)blockIdx.z * k_per_split;
+  const int64_t m0 = (int64_t)by * BM, n0 = (int64_t)bx * BN;
+  const int64_t kb = (int64_t)bz * k_per_split;
   const int64_t ke = min(K, kb + k_per_split);
   const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
 
@@ -124,7 +147,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
 #pragma unroll
     for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const bool do_rowsum = ep.opa_rowsum != nullptr && blockIdx.x == 0;
+  const bool do_rowsum = ep.opa_rowsum != nullptr && bx == 0;
   float rowsum = 0.f;  // thread t < BM: sum over this block's k range of op(A)[m0 + t][k]
   // Operand element (r = m or n, k): row-major sources stage f -> (r = f / (GBK/4), k = 4 (f % (GBK/4)));
   // k-major sources stage f -> (k = f / (R/4), r = 4 (f % (R/4))).
@@ -155,8 +178,8 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
     }
   };
   auto lstore = [&](int buf, const float4 (&ra)[LA], const float4 (&rb)[LB]) {
-    float* a_ = sA[buf];
-    float* b_ = sB[buf];
+    float* a_ = sA(buf);
+    float* b_ = sB(buf);
 #pragma unroll
     for (int i = 0; i < LA; ++i) {
       const int f = t + 256 * i;
@@ -182,8 +205,8 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
   };
   // one staged k-tile: MFMA chain in k order (+ the fused row sums)
   auto compute = [&](int buf) {
-    const float* a_ = sA[buf];
-    const float* b_ = sB[buf];
+    const float* a_ = sA(buf);
+    const float* b_ = sB(buf);
     auto a_at = [&](int m, int k) -> float { return TA ? a_[k * TAo::SK + m] : a_[m * GSR + k]; };
     auto b_at = [&](int k, int n) -> float { return TB ? b_[n * GSR + k] : b_[k * TBo::SK + n]; };
     if (do_rowsum && t < BM) {
@@ -242,7 +265,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
   }
 
   if (do_rowsum && t < BM && m0 + t < M) {
-    if (slab) st_shared_f(&slab[(int64_t)gridDim.z * M * N + (int64_t)blockIdx.z * M + m0 + t], rowsum);
+    if (slab) st_shared_f(&slab[(int64_t)g.gz * M * N + (int64_t)bz * M + m0 + t], rowsum);
     else ep.opa_rowsum[m0 + t] = alpha * rowsum;
   }
   const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP && ep.kind <= HVAE_EPI_DROP_BWD) ? load_step(ep.step_dev) : 0;
@@ -271,13 +294,13 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
       for (int r = 0; r < 4; ++r) {
         const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
         const int64_t col = n0 + wn + j * 16 + (lane & 15);
-        if (row < M && col < N) st_shared_f(&slab[((int64_t)blockIdx.z * M + row) * N + col], acc[i][j][r]);
+        if (row < M && col < N) st_shared_f(&slab[((int64_t)bz * M + row) * N + col], acc[i][j][r]);
       }
-  const unsigned tile = blockIdx.y * gridDim.x + blockIdx.x;
-  if (!last_block_arrives(&tickets[tile], gridDim.z)) return;
+  const unsigned tile = by * g.gx + bx;
+  if (!last_block_arrives(&tickets[tile], g.gz)) return;
   // the tile's elements per thread: one coherent load each per split, all in flight together
   constexpr int Q = BM * BN / 256;
-  const int S = gridDim.z;
+  const int S = (int)g.gz;
   float sum[Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) sum[q] = 0.f;
@@ -301,10 +324,37 @@ __global__ void __launch_bounds__(256) k_gemm_f32(int64_t M, int64_t N, int64_t 
     if (beta != 0.f) c += beta * C[row * ldc + col];
     C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c, C);
   }
-  if (ep.opa_rowsum && blockIdx.x == 0 && t < BM && m0 + t < M) {
+  if (ep.opa_rowsum && bx == 0 && t < BM && m0 + t < M) {
     float r = 0.f;
     for (int z = 0; z < S; ++z) r += ld_shared_f(&slab[(int64_t)S * M * N + (int64_t)z * M + m0 + t]);
     ep.opa_rowsum[m0 + t] = alpha * r;
+  }
+}
+
+template <bool TA, bool TB, int BM, int BN>
+__global__ void __launch_bounds__(256) k_gemm_f32(GemmP g) {
+  __shared__ __attribute__((aligned(16))) float sA[gemm_smem_floats<BM>()];
+  __shared__ __attribute__((aligned(16))) float sB[gemm_smem_floats<BN>()];
+  gemm_block<TA, TB, BM, BN>(g, blockIdx.x, blockIdx.y, blockIdx.z, sA, sB);
+}
+
+// Two independent GEMMs in one launch (a weight gradient dW = dY^T X and the data gradient
+// dX = dY W of one layer): the first g0.gx*g0.gy*g0.gz blocks run g0, the rest g1. Both depend
+// only on inputs already complete, so the launch costs max(t0, t1) instead of t0 + t1 plus a
+// kernel boundary.
+template <int BM0, int BM1>
+__global__ void __launch_bounds__(256) k_gemm_f32_pair(GemmP g0, GemmP g1) {
+  constexpr int SA = gemm_smem_floats<BM0>() > gemm_smem_floats<BM1>() ? gemm_smem_floats<BM0>()
+                                                                       : gemm_smem_floats<BM1>();
+  __shared__ __attribute__((aligned(16))) float sA[SA];
+  __shared__ __attribute__((aligned(16))) float sB[SA];
+  const unsigned n0 = g0.gx * g0.gy * g0.gz;
+  unsigned b = blockIdx.x;
+  if (b < n0) {
+    gemm_block<true, false, BM0, BM0>(g0, b % g0.gx, (b / g0.gx) % g0.gy, b / (g0.gx * g0.gy), sA, sB);
+  } else {
+    b -= n0;
+    gemm_block<false, false, BM1, BM1>(g1, b % g1.gx, (b / g1.gx) % g1.gy, b / (g1.gx * g1.gy), sA, sB);
   }
 }
 
@@ -362,15 +412,14 @@ extern "C" size_t hvae_gemm_f32_workspace(int64_t M, int64_t N, int64_t K) {
   return s > 1 ? (size_t)s * (M * N + M) * sizeof(float) : 0;
 }
 
-extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
-                             const float* A, int64_t lda, const float* B, int64_t ldb, float beta,
-                             float* C, int64_t ldc, const hvae_epilogue* epi, void* ws,
-                             size_t ws_bytes, void* stream) {
+// Validate one problem and fill its launch record (tile size in *bt).
+static int gemm_setup(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
+                      int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
+                      const hvae_epilogue* epi, void* ws, size_t ws_bytes, GemmP& g, int& bt) {
   HVAE_REQUIRE(M >= 0 && N >= 0 && K >= 0 && C, "hvae_gemm_f32: bad shape / null C");
   HVAE_REQUIRE(ldc >= N, "hvae_gemm_f32: ldc < N");
   HVAE_REQUIRE(M < (1ll << 31) / 64 * 64 && N < (1ll << 31), "hvae_gemm_f32: too large");
-  if (M == 0 || N == 0) return HVAE_OK;
-  HVAE_REQUIRE(K == 0 || (A && B), "hvae_gemm_f32: null A/B");
+  HVAE_REQUIRE(K == 0 || (A && B) || M == 0 || N == 0, "hvae_gemm_f32: null A/B");
   HVAE_REQUIRE(trans_a ? lda >= M : lda >= K, "hvae_gemm_f32: bad lda");
   HVAE_REQUIRE(trans_b ? ldb >= K : ldb >= N, "hvae_gemm_f32: bad ldb");
   EpiArgs ep{};
@@ -397,7 +446,6 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
     HVAE_REQUIRE(ep.kind != HVAE_EPI_BIAS_GELU_DROP || ep.pre_out, "hvae_gemm_f32: no pre_out");
     HVAE_REQUIRE(ep.kind != HVAE_EPI_GELU_DROP_BWD || ep.pre_in, "hvae_gemm_f32: no pre_in");
   }
-  hipStream_t st = as_stream(stream);
   int splits = gemm_splits(M, N, K);
   if (splits > 1) {
     const int64_t fit = ws ? (int64_t)(ws_bytes / ((size_t)(M * N + M) * sizeof(float))) : 0;
@@ -409,30 +457,83 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
     kps = cdiv(cdiv(K, splits), GBK) * GBK;
     splits = (int)cdiv(K, kps);
   }
-  const bool vec_a = (((uintptr_t)A) % 16 == 0) && (lda % 4 == 0);
-  const bool vec_b = (((uintptr_t)B) % 16 == 0) && (ldb % 4 == 0);
-  const int bt = gemm_tile(M, N, K);
-  dim3 grid((unsigned)cdiv(N, bt), (unsigned)cdiv(M, bt), (unsigned)std::max(splits, 1));
-  float* slab = splits > 1 ? (float*)ws : nullptr;
-  unsigned* tickets = nullptr;
-  if (slab) {
-    HVAE_REQUIRE((uint64_t)grid.x * grid.y <= (uint64_t)kTicketSlice, "hvae_gemm_f32: too many split tiles");
-    tickets = ticket_slice();
-    if (!tickets) return HVAE_ERR_HIP;
+  bt = gemm_tile(M, N, K);
+  g.M = M; g.N = N; g.K = K; g.kps = (K == 0) ? 0 : kps;
+  g.alpha = alpha; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.beta = beta; g.C = C; g.ldc = ldc;
+  g.ep = ep;
+  g.vec_a = (((uintptr_t)A) % 16 == 0) && (lda % 4 == 0);
+  g.vec_b = (((uintptr_t)B) % 16 == 0) && (ldb % 4 == 0);
+  g.gx = (unsigned)cdiv(N, bt); g.gy = (unsigned)cdiv(M, bt); g.gz = (unsigned)std::max(splits, 1);
+  g.slab = splits > 1 ? (float*)ws : nullptr;
+  g.tickets = nullptr;
+  if (g.slab) {
+    HVAE_REQUIRE((uint64_t)g.gx * g.gy <= (uint64_t)kTicketSlice, "hvae_gemm_f32: too many split tiles");
+    g.tickets = ticket_slice();
+    if (!g.tickets) return HVAE_ERR_HIP;
   }
-  if (K == 0) kps = 0;
+  return HVAE_OK;
+}
+
+extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
+                             const float* A, int64_t lda, const float* B, int64_t ldb, float beta,
+                             float* C, int64_t ldc, const hvae_epilogue* epi, void* ws,
+                             size_t ws_bytes, void* stream) {
+  if (M == 0 || N == 0) {
+    HVAE_REQUIRE(M >= 0 && N >= 0 && C, "hvae_gemm_f32: bad shape / null C");
+    return HVAE_OK;
+  }
+  GemmP g{};
+  int bt = 32;
+  if (int rc = gemm_setup(trans_a, trans_b, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, epi, ws, ws_bytes, g,
+                          bt))
+    return rc;
+  hipStream_t st = as_stream(stream);
+  dim3 grid(g.gx, g.gy, g.gz);
   ProbeScope probe("gemm", st);
-#define HVAE_GEMM_CALL(TA_, TB_)                                                                        \
-  (bt == 64 ? (k_gemm_f32<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(M, N, K, kps, alpha, A, lda, B, ldb, beta, \
-                                                                 C, ldc, slab, tickets, ep, vec_a, vec_b))  \
-            : (k_gemm_f32<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(M, N, K, kps, alpha, A, lda, B, ldb, beta, \
-                                                                 C, ldc, slab, tickets, ep, vec_a, vec_b)))
+#define HVAE_GEMM_CALL(TA_, TB_)                                                 \
+  (bt == 64 ? (k_gemm_f32<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(g))            \
+            : (k_gemm_f32<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(g)))
   if (!trans_a && !trans_b) HVAE_GEMM_CALL(false, false);
   else if (!trans_a && trans_b) HVAE_GEMM_CALL(false, true);
   else if (trans_a && !trans_b) HVAE_GEMM_CALL(true, false);
   else HVAE_GEMM_CALL(true, true);
 #undef HVAE_GEMM_CALL
   HVAE_LAUNCH_CHECK("k_gemm_f32");
+  return HVAE_OK;
+}
+
+static int gemm_desc(const hvae_gemm_desc* d, void* stream) {
+  return hvae_gemm_f32(d->trans_a, d->trans_b, d->M, d->N, d->K, d->alpha, d->A, d->lda, d->B, d->ldb, d->beta,
+                       d->C, d->ldc, d->epi, d->ws, d->ws_bytes, stream);
+}
+
+extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc* x, void* stream) {
+  HVAE_REQUIRE(w && x, "hvae_gemm_f32_pair: null descriptor");
+  // one launch for the (A^T B, A B) pair of a layer's backward; any other pairing runs as two launches
+  const bool shared_ws = w->ws && w->ws == x->ws && gemm_splits(w->M, w->N, w->K) > 1 &&
+                         gemm_splits(x->M, x->N, x->K) > 1;  // both split-K into one slab: two launches
+  const bool fused = w->trans_a && !w->trans_b && !x->trans_a && !x->trans_b && w->M > 0 && w->N > 0 &&
+                     x->M > 0 && x->N > 0 && !shared_ws;
+  if (!fused) {
+    if (int rc = gemm_desc(w, stream)) return rc;
+    return gemm_desc(x, stream);
+  }
+  GemmP g0{}, g1{};
+  int bt0 = 32, bt1 = 32;
+  if (int rc = gemm_setup(1, 0, w->M, w->N, w->K, w->alpha, w->A, w->lda, w->B, w->ldb, w->beta, w->C, w->ldc,
+                          w->epi, w->ws, w->ws_bytes, g0, bt0))
+    return rc;
+  if (int rc = gemm_setup(0, 0, x->M, x->N, x->K, x->alpha, x->A, x->lda, x->B, x->ldb, x->beta, x->C, x->ldc,
+                          x->epi, x->ws, x->ws_bytes, g1, bt1))
+    return rc;
+  hipStream_t st = as_stream(stream);
+  const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
+  ProbeScope probe("gemm", st);
+  if (bt0 == 64 && bt1 == 64) k_gemm_f32_pair<64, 64><<<nblk, 256, 0, st>>>(g0, g1);
+  else if (bt0 == 64) k_gemm_f32_pair<64, 32><<<nblk, 256, 0, st>>>(g0, g1);
+  else if (bt1 == 64) k_gemm_f32_pair<32, 64><<<nblk, 256, 0, st>>>(g0, g1);
+  else k_gemm_f32_pair<32, 32><<<nblk, 256, 0, st>>>(g0, g1);
+  HVAE_LAUNCH_CHECK("k_gemm_f32_pair");
   return HVAE_OK;
 }
 

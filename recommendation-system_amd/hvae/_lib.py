@@ -57,6 +57,14 @@ class Epilogue(C.Structure):
     ]
 
 
+class GemmDesc(C.Structure):
+    _fields_ = [
+        ("trans_a", cint), ("trans_b", cint), ("M", i64), ("N", i64), ("K", i64), ("alpha", f32),
+        ("A", vp), ("lda", i64), ("B", vp), ("ldb", i64), ("beta", f32), ("C", vp), ("ldc", i64),
+        ("epi", C.POINTER(Epilogue)), ("ws", vp), ("ws_bytes", sz),
+    ]
+
+
 class Adam(C.Structure):
     _fields_ = [
         ("lr", f64), ("beta1", f64), ("beta2", f64), ("eps", f64), ("weight_decay", f64),
@@ -87,6 +95,7 @@ SIGNATURES = {
     "hvae_gemm_f32": (cint, [cint, cint, i64, i64, i64, f32, vp, i64, vp, i64, f32, vp, i64, P(Epilogue), vp,
                              sz, vp]),
     "hvae_gemm_f32_workspace": (sz, [i64, i64, i64]),
+    "hvae_gemm_f32_pair": (cint, [P(GemmDesc), P(GemmDesc), vp]),
     "hvae_colsum": (cint, [vp, i64, i64, i64, f32, vp, vp, sz, vp]),
     "hvae_colsum_workspace": (sz, [i64, i64]),
     "hvae_reparam_kl_fwd": (cint, [vp, vp, i64, i64, i64, cint, vp, u64, vp, vp, vp, vp, vp]),

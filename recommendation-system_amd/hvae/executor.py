@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 from . import _lib, ops
-from ._lib import CsrBatch, Epilogue, check, lib, ptr
+from ._lib import CsrBatch, Epilogue, GemmDesc, check, lib, ptr
 
 ALIGN = 4  # floats: every flat segment starts 16-B aligned
 
@@ -460,27 +460,42 @@ class FusedTrainer:
             return
         # ----------------------------------------------------- backward ---
         G = self.G
+
+        def layer_bwd(wgrad: tuple, wrowsum, xgrad: tuple, xepi=None):
+            """A layer's weight gradient (trans_a GEMM on the side stream) and data gradient: with one stream,
+            both in one launch (hvae_gemm_f32_pair) -- they read only finished inputs."""
+            if side is not main:
+                self._fork(main, side)
+                gemm(1, 0, *wgrad, rowsum=wrowsum, side_=True)
+                gemm(0, 0, *xgrad, epi=xepi)
+                return
+            we = (Epilogue(_lib.EPI_NONE, None, None, None, 0.0, None, 0, None, 0, 0, ptr(wrowsum))
+                  if wrowsum is not None else None)
+
+            def desc(ta, args, e):
+                M, N, K, A, lda, Bm, ldb, Cm, ldc = args
+                return GemmDesc(ta, 0, M, N, K, 1.0, A, lda, Bm, ldb, 0.0, Cm, ldc,
+                                C.pointer(e) if e is not None else None, ws, wsn)
+            dw, dx = desc(1, wgrad, we), desc(0, xgrad, xepi)
+            check(L_.hvae_gemm_f32_pair(C.byref(dw), C.byref(dx), st), "gemm_pair")
+
         if lay.has_proj:
-            gemm(1, 0, d, d, B, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d,
-                 rowsum=G["projection_layer.3.bias"], side_=True)
             epi3 = Epilogue(_lib.EPI_GELU_DROP_BWD, None, None, ptr(bf.p1), p_drop, ptr(ext.get("proj_mask")), seed,
                             step, _lib.TAG_PROJ_DROP, tr, None)
-            gemm(0, 0, B, d, d, ptr(bf.dU), d, ptr(Wb), d, ptr(bf.dp1), d, epi3)
-            self._fork(main, side)
-            gemm(1, 0, d, Lt, B, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt,
-                 rowsum=G["projection_layer.0.bias"], side_=True)
+            layer_bwd((d, d, B, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d),
+                      G["projection_layer.3.bias"], (B, d, d, ptr(bf.dU), d, ptr(Wb), d, ptr(bf.dp1), d), epi3)
             # dz = dp1 Wa with the reparameterisation + KL backward as its epilogue -> dheads = [dmu | dlogvar]
             epi_r = Epilogue(_lib.EPI_REPARAM_BWD, None, None, ptr(bf.heads), 0.0, None, 0, None, 0, tr, None,
                              ptr(bf.eps), beta / B)
-            gemm(0, 0, B, Lt, d, ptr(bf.dp1), d, ptr(Wa), Lt, ptr(bf.dheads), 2 * Lt, epi_r)
+            layer_bwd((d, Lt, B, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt),
+                      G["projection_layer.0.bias"], (B, Lt, d, ptr(bf.dp1), d, ptr(Wa), Lt, ptr(bf.dheads), 2 * Lt),
+                      epi_r)
         else:
             dmu, dlv = bf.dheads, bf.dheads[:, Lt:]
             check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B, tr,
                                          ptr(dmu), ptr(dlv), 2 * Lt, st), "reparam_kl_bwd")
-        self._fork(main, side)
-        gemm(1, 0, 2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl,
-             rowsum=self.gb_heads, side_=True)
-        gemm(0, 0, B, Hl, 2 * Lt, ptr(bf.dheads), 2 * Lt, ptr(self.W_heads), Hl, ptr(bf.dh[-1]), Hl)
+        layer_bwd((2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl), self.gb_heads,
+                  (B, Hl, 2 * Lt, ptr(bf.dheads), 2 * Lt, ptr(self.W_heads), Hl, ptr(bf.dh[-1]), Hl))
         for k in range(len(H) - 1, -1, -1):
             i = 4 * k
             check(L_.hvae_ln_gelu_drop_bwd(ptr(bf.dh[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]),
@@ -490,10 +505,9 @@ class FusedTrainer:
                                            ptr(G[f"encoder.{i}.bias"]), ws, wsn, st), "ln_gelu_drop_bwd")
             if k > 0:
                 W = self.P[f"encoder.{i}.weight"]
-                self._fork(main, side)
-                gemm(1, 0, H[k], H[k - 1], B, ptr(bf.da[k]), H[k], ptr(bf.h[k - 1]), H[k - 1],
-                     ptr(G[f"encoder.{i}.weight"]), H[k - 1], side_=True)
-                gemm(0, 0, B, H[k - 1], H[k], ptr(bf.da[k]), H[k], ptr(W), H[k - 1], ptr(bf.dh[k - 1]), H[k - 1])
+                layer_bwd((H[k], H[k - 1], B, ptr(bf.da[k]), H[k], ptr(bf.h[k - 1]), H[k - 1],
+                           ptr(G[f"encoder.{i}.weight"]), H[k - 1]), None,
+                          (B, H[k - 1], H[k], ptr(bf.da[k]), H[k], ptr(W), H[k - 1], ptr(bf.dh[k - 1]), H[k - 1]))
         if ev_plan is not None:
             main.wait_event(ev_plan)
         check(L_.hvae_w1_rowgrad_apply(ptr(bf.da[0]), H[0], bf.rg.ref, st), "w1_rowgrad_apply")

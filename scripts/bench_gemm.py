@@ -20,29 +20,33 @@ import torch  # noqa: E402
 from hvae import _lib, ops  # noqa: E402
 from hvae._lib import check, lib  # noqa: E402
 
-B, H, L, D = 64, 512, 128, 384
-# (name, M, N, K, trans_a, trans_b) -- nn.Linear forward is NT, data grads NN, weight grads TN
-SHAPES = [
-    ("fwd_heads", B, 2 * L, H, False, True),
-    ("fwd_proj_a", B, D, L, False, True),
-    ("fwd_proj_b", B, D, D, False, True),
-    ("bwd_dWb", D, D, B, True, False),
-    ("bwd_dp1", B, D, D, False, False),
-    ("bwd_dWa", D, L, B, True, False),
-    ("bwd_dz", B, L, D, False, False),
-    ("bwd_dWh", 2 * L, H, B, True, False),
-    ("bwd_dh", B, H, 2 * L, False, False),
-]
+H, L, D = 512, 128, 384
+
+
+def shapes(B):
+    # (name, M, N, K, trans_a, trans_b) -- nn.Linear forward is NT, data grads NN, weight grads TN
+    return [
+        ("fwd_heads", B, 2 * L, H, False, True),
+        ("fwd_proj_a", B, D, L, False, True),
+        ("fwd_proj_b", B, D, D, False, True),
+        ("bwd_dWb", D, D, B, True, False),
+        ("bwd_dp1", B, D, D, False, False),
+        ("bwd_dWa", D, L, B, True, False),
+        ("bwd_dz", B, L, D, False, False),
+        ("bwd_dWh", 2 * L, H, B, True, False),
+        ("bwd_dh", B, H, 2 * L, False, False),
+    ]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
+    ap.add_argument("--batch", type=int, default=64)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     out = {}
-    for name, M, N, K, ta, tb in SHAPES:
+    for name, M, N, K, ta, tb in shapes(args.batch):
         a = torch.randn(K, M, generator=g).to(dev).t() if ta else torch.randn(M, K, generator=g).to(dev)
         b = torch.randn(N, K, generator=g).to(dev).t() if tb else torch.randn(K, N, generator=g).to(dev)
         rs = torch.empty(M, device=dev)

@@ -1,0 +1,4 @@
+set -e
+mkdir -p gpurun_out
+timeout -k 10 200 python scripts/bench_gemm.py --batch 4096 --reps 50 2>&1 | grep -v amdgpu.ids > gpurun_out/gemm4096.log
+timeout -k 10 200 python scripts/bench_gemm.py --batch 64 --reps 100 2>&1 | grep -v amdgpu.ids > gpurun_out/gemm64.log

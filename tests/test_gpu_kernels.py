@@ -79,6 +79,33 @@ def test_gemm_tn_bias_rowsum(ops, hip_device, M, N, K):
     assert _maxrel(rs, dY.double().sum(0)) < 1e-5
 
 
+@pytest.mark.parametrize("B,M,N,Kx", [(64, 384, 384, 384), (4096, 256, 512, 256), (64, 384, 128, 384),
+                                     (50, 70, 33, 45)])
+def test_gemm_pair_equals_two_launches(ops, hip_device, B, M, N, Kx):
+    """hvae_gemm_f32_pair (dW = dY^T X with the bias gradient, and dX = dY W in one launch) is bitwise the
+    two hvae_gemm_f32 launches it replaces, including split-K on the weight gradient at large B."""
+    import ctypes as C
+    from hvae import _lib
+    from hvae._lib import GemmDesc, check, lib, ptr, stream_of
+    g = torch.Generator().manual_seed(B + M)
+    dY = torch.randn(B, M, generator=g).to(hip_device)
+    X = torch.randn(B, N, generator=g).to(hip_device)
+    W = torch.randn(M, Kx, generator=g).to(hip_device)
+    rs1 = torch.empty(M, device=hip_device)
+    dW1 = ops.gemm(dY.t(), X, epi=ops.epilogue(_lib.EPI_NONE, opa_rowsum=rs1))
+    dX1 = ops.gemm(dY, W)
+    rs2 = torch.empty(M, device=hip_device)
+    dW2 = torch.empty(M, N, device=hip_device)
+    dX2 = torch.empty(B, Kx, device=hip_device)
+    ws = ops.workspace(hip_device, int(lib().hvae_gemm_f32_workspace(M, N, B)))
+    epi = _lib.Epilogue(_lib.EPI_NONE, None, None, None, 0.0, None, 0, None, 0, 0, ptr(rs2))
+    dw = GemmDesc(1, 0, M, N, B, 1.0, ptr(dY), M, ptr(X), N, 0.0, ptr(dW2), N, C.pointer(epi), ptr(ws), ws.numel())
+    dx = GemmDesc(0, 0, B, Kx, M, 1.0, ptr(dY), M, ptr(W), Kx, 0.0, ptr(dX2), Kx, None, None, 0)
+    check(lib().hvae_gemm_f32_pair(C.byref(dw), C.byref(dx), stream_of(dY)), "gemm_pair")
+    torch.cuda.synchronize()
+    assert torch.equal(dW1, dW2) and torch.equal(rs1, rs2) and torch.equal(dX1, dX2)
+
+
 def test_colsum(ops, hip_device):
     X = torch.randn(3000, 77)
     out = ops.colsum(X.to(hip_device))
@@ -413,7 +440,7 @@ def test_clip_step_counters(ops, hip_device):
     assert (int(step.item()), int(snap.item()), int(boff.item())) == (44, 43, 128 + 3 * 64)
 
 
-@pytest.mark.parametrize("nb,N,lam,hot", [(40, 300, 5.0, 0), (300, 2000, 8.0, 100), (5000, 500, 2.0, 4500),
+@pytest.mark.parametrize("nb,N,lam,hot", [(40, 300, 5.0, 0), (64, 12101, 3.0, 40), (300, 2000, 8.0, 100), (5000, 500, 2.0, 4500),
                                          (40000, 3000, 1.0, 3000), (40000, 3000, 1.0, 6000)])
 def test_rowgrad_plan_apply_segments(ops, hip_device, nb, N, lam, hot):
     """Segments of every sort path (wave <= 64; bitmap rank for nb <= 32768; beyond that block bitonic
