@@ -32,13 +32,30 @@ struct ClipArgs {
 __global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
   __shared__ double red[4];
   const int64_t nr = a.rows ? (int64_t)(*a.n_unique) * a.H : 0;
-  const int64_t tot = a.n + nr;
   double s = 0.0;
+  const int64_t gtid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += stride) {
-    const float v = (i < a.n) ? a.g[i] : a.rows[i - a.n];
-    s += (double)v * (double)v;
-  }
+  // sum of squares of one segment: float4 loads, 4 of them in flight per thread per round (a
+  // one-load-per-iteration loop is a chain of memory latencies), scalar tail; fixed order
+  auto seg = [&](const float* __restrict__ x, int64_t n) {
+    const bool vec = ((uintptr_t)x % 16) == 0;
+    const int64_t n4 = vec ? n / 4 : 0;
+    const float4* x4 = reinterpret_cast<const float4*>(x);
+    for (int64_t i = gtid; i < n4; i += 4 * stride) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t j = i + u * stride;
+        v[u] = j < n4 ? x4[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        s += ((double)v[u].x * v[u].x + (double)v[u].y * v[u].y) + ((double)v[u].z * v[u].z + (double)v[u].w * v[u].w);
+    }
+    for (int64_t i = 4 * n4 + gtid; i < n; i += stride) s += (double)x[i] * (double)x[i];
+  };
+  if (a.n) seg(a.g, a.n);
+  if (nr) seg(a.rows, nr);
   s = wave_sum_d(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();

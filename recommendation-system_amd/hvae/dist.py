@@ -17,9 +17,14 @@ forward/backward:
 The row lists are exchanged at a fixed size M per epoch: every rank counts the
 unique items of each of its batches on the host when the epoch order is drawn,
 and one all-reduce(MAX) per epoch gives the largest list of any rank and batch.
-So a step has no host synchronisation: two captured graphs (forward/backward;
-merge/clip/Adam) with the three collectives launched between them. Entries
-past a rank's own count carry weight 0.
+Entries past a rank's own count carry weight 0.
+
+A step then makes ONE collective: each rank packs [dense gradients | row count |
+item ids | gradient rows] into one fp32 buffer at the end of its forward/backward
+graph, a single all_gather_into_tensor moves it (per-collective latency, not
+bytes, dominates at these sizes on xGMI), and the update graph averages the
+dense parts in rank order and merges the row lists. So a step has no host
+synchronisation: two captured graphs with one collective between them.
 
 Then every rank clips and steps Adam on identical gradients, so the replicas
 stay bit-identical. The merge function is injectable so that the collective
@@ -62,6 +67,7 @@ class DPExchange:
         self.M = 0
         self._merged = None
         self._buf = None
+        self._pk = None
 
     # -- collectives (gloo cannot take device tensors for every op: stage through host) --
     def _stage(self, t: torch.Tensor) -> torch.Tensor:
@@ -84,6 +90,47 @@ class DPExchange:
         if o is not out:
             out.copy_(o)
 
+    # -- one-collective step: pack (graph 1) -> all-gather (eager) -> unpack + merge (graph 2) --
+    def _packed(self, n_small: int):
+        """(send [L], recv [W, L]) for the epoch's M; L = n_small + 1 + M + M * H (fp32 words)."""
+        M, W, H = self.M, self.world, self.H
+        L = n_small + 1 + M + M * H
+        if self._pk is None or self._pk[0].numel() != L:
+            self._pk = (torch.zeros(L, dtype=torch.float32, device=self.device),
+                        torch.zeros(W, L, dtype=torch.float32, device=self.device))
+        return self._pk
+
+    def pack(self, g_small: torch.Tensor, n_unique: torch.Tensor, item_of: torch.Tensor, rows: torch.Tensor) -> None:
+        """Device copies of this rank's step gradients into the send buffer (capturable)."""
+        M, ns = self.M, g_small.numel()
+        assert M > 0, "plan_epoch() first"
+        assert item_of.numel() >= M and rows.shape[0] >= M, "row-gradient buffers shorter than the exchange size"
+        send, _ = self._packed(ns)
+        send[:ns].copy_(g_small.reshape(-1))
+        send[ns:ns + 1].view(torch.int32).copy_(n_unique.reshape(1).to(torch.int32))
+        send[ns + 1:ns + 1 + M].view(torch.int32).copy_(item_of[:M])
+        send[ns + 1 + M:].view(M, self.H).copy_(rows[:M])
+
+    def communicate(self, n_small: int) -> None:
+        """The step's one collective (eager, between the two graphs)."""
+        send, recv = self._packed(n_small)
+        if self.world == 1:
+            recv[0].copy_(send)
+            return
+        self._all_gather(recv.reshape(-1), send)
+
+    def unpack_merge(self, g_small: torch.Tensor):
+        """Dense gradients <- mean over ranks (summed in rank order); row lists -> merged row gradient."""
+        M, W, H, ns = self.M, self.world, self.H, g_small.numel()
+        _, recv = self._packed(ns)
+        torch.sum(recv[:, :ns], dim=0, out=g_small.reshape(-1))
+        g_small.div_(W)
+        b = self._buf
+        b["n"].copy_(recv[:, ns].contiguous().view(torch.int32))
+        b["items"].view(W, M).copy_(recv[:, ns + 1:ns + 1 + M].contiguous().view(torch.int32))
+        b["rows"].view(W, M, H).copy_(recv[:, ns + 1 + M:].reshape(W, M, H))
+        return self.merge()
+
     def plan_epoch(self, counts_per_batch: np.ndarray) -> int:
         """One host collective per epoch: the largest row list of any rank and batch. (Re)allocates the
         exchange and merge buffers when it grows, so that nothing is allocated inside a captured step."""
@@ -104,6 +151,7 @@ class DPExchange:
                 "j": torch.arange(M, dtype=torch.int32, device=dev),
             }
             self._merged = self.make_merged(self.n_items, H, W * M, dev)
+            self._pk = None
         return self.M
 
     def exchange(self, n_unique: torch.Tensor, item_of: torch.Tensor, rows: torch.Tensor) -> None:

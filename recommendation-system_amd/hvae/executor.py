@@ -356,19 +356,22 @@ class FusedTrainer:
             if self.dp is None:
                 self._launch_update(bf.rg, bf, advance)
             else:
+                self._launch_pack(bf)
                 self._launch_exchange(bf)
                 self._launch_dp_update(bf, advance)
         elif advance:
             self._advance(advance)
 
+    def _launch_pack(self, bf: _StepBuffers):
+        """End of a data-parallel forward/backward: this rank's gradients into the exchange buffer."""
+        self.dp.pack(self.g_small, bf.rg.n_unique, bf.rg.item_of, bf.rg.rows)
+
     def _launch_exchange(self, bf: _StepBuffers):
-        """Data-parallel collectives of a step (eager, between the two graphs): AVG of the dense gradients,
-        all-gather of the row lists."""
-        self.dp.all_reduce_dense(self.g_small)
-        self.dp.exchange(bf.rg.n_unique, bf.rg.item_of, bf.rg.rows)
+        """The step's one collective (eager, between the two graphs): all-gather of the packed gradients."""
+        self.dp.communicate(self.g_small.numel())
 
     def _launch_dp_update(self, bf: _StepBuffers, advance: int):
-        merged = self.dp.merge()
+        merged = self.dp.unpack_merge(self.g_small)
         self._launch_update(merged, bf, advance)
 
     def _fork(self, src, dst):
@@ -665,6 +668,7 @@ class FusedTrainer:
         else:
             with torch.cuda.graph(g):
                 self._launch_fwd_bwd(bf, csr, train, beta, p_drop, None)
+                self._launch_pack(bf)
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2):
                 self._launch_dp_update(bf, bf.B)

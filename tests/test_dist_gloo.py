@@ -60,6 +60,55 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
+def _worker_packed(rank, world, port, q):
+    """The one-collective step: pack -> all_gather -> unpack_merge gives what all_reduce + exchange give."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from hvae.dist import DPExchange
+    ex = DPExchange(dist.group.WORLD, torch.device("cpu"), N, H, merge_fn=_cpu_merge,
+                    make_merged=lambda n, h, cap, dev: _Dense(cap))
+    g = torch.Generator().manual_seed(200 + rank)
+    small = torch.randn(777, generator=g)
+    mine = small.clone()
+    k = 4 + 9 * rank
+    items = torch.sort(torch.randperm(N, generator=g)[:k]).values.int()
+    cap = 32
+    item_of = torch.zeros(cap, dtype=torch.int32)
+    item_of[:k] = items
+    rows = torch.zeros(cap, H)
+    rows[:k] = torch.randn(k, H, generator=g)
+    rows[k:] = 1e30
+    ex.plan_epoch(np.array([k, 2]))
+    ex.pack(small, torch.tensor([k], dtype=torch.int32), item_of, rows)
+    ex.communicate(small.numel())
+    merged = ex.unpack_merge(small)
+    dense_mine = torch.zeros(N, H, dtype=torch.float64)
+    dense_mine[items.long()] = rows[:k].double()
+    q.put((rank, mine, small, dense_mine, merged.dense.clone()))
+    dist.destroy_process_group()
+
+
+def test_dp_packed_exchange_gloo_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_packed, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    mean_small = (res[0][1] + res[1][1]) / 2
+    mean_dense = (res[0][3] + res[1][3]) / 2
+    for _, _, small, _, merged in res:
+        assert torch.allclose(small, mean_small, atol=1e-6)
+        assert torch.allclose(merged, mean_dense, atol=1e-12)
+    assert torch.equal(res[0][4], res[1][4]) and torch.equal(res[0][2], res[1][2])
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

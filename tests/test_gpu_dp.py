@@ -24,6 +24,15 @@ def _free_port():
 
 
 def _worker(rank, world, port, q):
+    try:
+        _worker_body(rank, world, port, q)
+    except BaseException:  # surface the rank's error in the parent's output before the queue breaks
+        import traceback
+        traceback.print_exc()
+        raise
+
+
+def _worker_body(rank, world, port, q):
     import sys
     from pathlib import Path
     root = Path(__file__).resolve().parents[1]
