@@ -316,6 +316,14 @@ typedef struct hvae_adam {
   const int64_t* step_dev; /* completed optimizer steps                        */
   const float* coef_dev;   /* clip multiplier or NULL (=> 1)                    */
 } hvae_adam;
+/* hvae_clip_grad_norm_step that also records the coming Adam step's scalars
+ * (lr / (1 - b1^t), sqrt(1 - b2^t)) for t = *step_dev + 1 in tab[t] (float2 entries, the
+ * lazy-Adam step table), computed once in double, so hvae_adam_lazy reads them instead of
+ * evaluating pow() in every thread. Pass hvae_adam_lazy step_dev = step_snap as usual. */
+int hvae_clip_grad_norm_step_adam(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg, int64_t H,
+                                  float max_norm, float* norm_out, float* coef_out, int64_t* step_dev,
+                                  int64_t* step_snap, int64_t* boff, int64_t advance, const hvae_adam* cfg,
+                                  float* tab, void* ws, size_t ws_bytes, void* stream);
 int hvae_adam_dense(const hvae_adam* cfg, float* p, float* m, float* v, const float* g, int64_t n,
                     void* stream);
 /* Dense Adam over the item-major W1t [N, H] whose gradient is row-sparse:

@@ -21,12 +21,21 @@ constexpr int kNormBlocks = 512;
 //   step_snap = step; step += 1; boff += advance
 // so that the Adam launches that follow read the pre-increment step from
 // step_snap and no separate counter launch is needed.
+// torch's per-step Adam scalars for step t, in double as torch computes them (Python floats):
+// (step_size = lr / (1 - b1^t), sqrt(1 - b2^t)), rounded to fp32 where the kernels use them.
+__device__ __forceinline__ float2 adam_step_consts(double lr, double b1, double b2, int64_t t) {
+  const double bc1 = 1.0 - pow(b1, (double)t);
+  const double bc2 = 1.0 - pow(b2, (double)t);
+  return make_float2((float)(lr / bc1), (float)sqrt(bc2));
+}
+
 struct ClipArgs {
   const float* g; int64_t n;
   const float* rows; const int32_t* n_unique; int64_t H;
   double* part; unsigned* ticket;
   float max_norm; float* norm_out; float* coef_out;
   int64_t* step; int64_t* step_snap; int64_t* boff; int64_t advance;
+  float2* tab; double lr, b1, b2;  // optional: record the coming Adam step's scalars in tab[step + 1]
 };
 
 __global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
@@ -77,6 +86,9 @@ __global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
       const int64_t st = *a.step;
       if (a.step_snap) *a.step_snap = st;
       *a.step = st + 1;
+      // computed once here, so the Adam launch that follows reads them instead of every
+      // thread of it evaluating two double pow()s
+      if (a.tab) a.tab[st + 1] = adam_step_consts(a.lr, a.b1, a.b2, st + 1);
     }
     if (a.boff) *a.boff += a.advance;
   }
@@ -89,7 +101,11 @@ struct AdamK {
 };
 
 // torch.optim.Adam single-tensor arithmetic, element-wise.
+// No FMA contraction: every kernel that applies a step (dense, flat, lazy rows, replays) must round
+// identically whatever code shape the compiler sees around it, or the lazy update would drift off
+// the dense one by an ulp (hipcc contracts a*b+c freely by default).
 __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g, const AdamK& k) {
+#pragma clang fp contract(off)
   if (k.wd != 0.f) g = g + k.wd * p;
   m = m + k.omb1 * (g - m);                 // exp_avg.lerp_(grad, 1 - beta1)
   v = v * k.b2 + k.omb2 * g * g;            // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
@@ -105,11 +121,10 @@ struct AdamArgs {
 
 __device__ __forceinline__ AdamK adam_consts(const AdamArgs& a) {
   const int64_t t = load_step(a.step_dev) + 1;
-  const double bc1 = 1.0 - pow(a.b1, (double)t);
-  const double bc2 = 1.0 - pow(a.b2, (double)t);
+  const float2 c = adam_step_consts(a.lr, a.b1, a.b2, t);
   AdamK k;
-  k.lr_over_bc1 = (float)(a.lr / bc1);
-  k.bc2_sqrt = (float)sqrt(bc2);
+  k.lr_over_bc1 = c.x;
+  k.bc2_sqrt = c.y;
   k.omb1 = (float)(1.0 - a.b1);
   k.b2 = (float)a.b2;
   k.omb2 = (float)(1.0 - a.b2);
@@ -233,56 +248,52 @@ __device__ __forceinline__ AdamK adam_consts_tab(const AdamArgs& a, float2 c) {
   return k;
 }
 
-// replay steps (from, to] of row j with g = 0; one wave per row, lane owns float4
-// columns. The per-step constants come 64 steps at a time (one coalesced load,
-// then a lane broadcast per step), so a replay costs compute, not load latency.
-__device__ __forceinline__ void lazy_row_catchup(const AdamArgs& a, const float2* __restrict__ tab, float* p,
-                                                 float* m, float* v, int64_t j, int64_t H, int from, int to,
-                                                 int lane) {
-  if (from >= to) return;
-  const int64_t H4 = H / 4;
-  for (int64_t c = lane; c - lane < H4; c += 64) {  // wave-uniform trip count (shuffles below)
-    const bool on = c < H4;
-    const int64_t i = j * H4 + (on ? c : 0);
-    float4 pp = on ? reinterpret_cast<float4*>(p)[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 mm = on ? reinterpret_cast<float4*>(m)[i] : pp;
-    float4 vv = on ? reinterpret_cast<float4*>(v)[i] : pp;
-    for (int t0 = from + 1; t0 <= to; t0 += 64) {
-      const int n = min(64, to - t0 + 1);
-      const float2 mine = lane < n ? tab[t0 + lane] : make_float2(0.f, 1.f);
-      for (int q = 0; q < n; ++q) {
-        const AdamK k = adam_consts_tab(a, make_float2(__shfl(mine.x, q), __shfl(mine.y, q)));
-        adam_elem(pp.x, mm.x, vv.x, 0.f, k);
-        adam_elem(pp.y, mm.y, vv.y, 0.f, k);
-        adam_elem(pp.z, mm.z, vv.z, 0.f, k);
-        adam_elem(pp.w, mm.w, vv.w, 0.f, k);
-      }
-    }
-    if (on) {
-      reinterpret_cast<float4*>(p)[i] = pp;
-      reinterpret_cast<float4*>(m)[i] = mm;
-      reinterpret_cast<float4*>(v)[i] = vv;
-    }
-  }
+// Column-parallel row updates: a block covers rpb rows x h4s float4 columns (thread t -> row t / h4s,
+// column t % h4s, columns past h4s looped), so a row's replay work is spread over H/4 threads instead
+// of one wave and the kernel fills the machine. The threads of a row read last_step[j] at the start of
+// a group and one of them advances it after a barrier, so no thread sees a half-updated row.
+struct RowMap {
+  int rpb, h4s;
+};
+static inline RowMap row_map(int64_t H) {
+  const int h4 = (int)(H / 4);
+  RowMap r;
+  r.h4s = h4 < 256 ? h4 : 256;
+  r.rpb = 256 / r.h4s;
+  return r;
 }
 
-// one g = 0 step with the constants of the running step (not yet in the table)
-__device__ __forceinline__ void lazy_row_zero_step(const AdamK& k, float* p, float* m, float* v, int64_t j,
-                                                   int64_t H, int lane) {
-  const int64_t H4 = H / 4;
-  for (int64_t c = lane; c < H4; c += 64) {
-    const int64_t i = j * H4 + c;
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    adam_elem(pp.x, mm.x, vv.x, 0.f, k);
-    adam_elem(pp.y, mm.y, vv.y, 0.f, k);
-    adam_elem(pp.z, mm.z, vv.z, 0.f, k);
-    adam_elem(pp.w, mm.w, vv.w, 0.f, k);
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
+// float4 column i of a row: replay steps (from, to] with g = 0 (constants from the step table,
+// loaded 8 at a time), then, if `step`, one more step with constants kx and gradient gx.
+__device__ __forceinline__ void col_update(const AdamArgs& a, const float2* __restrict__ tab, float* __restrict__ p,
+                                           float* __restrict__ m, float* __restrict__ v, int64_t i, int from, int to,
+                                           bool step, const AdamK& kx, float4 gx) {
+  float4 pp = reinterpret_cast<float4*>(p)[i];
+  float4 mm = reinterpret_cast<float4*>(m)[i];
+  float4 vv = reinterpret_cast<float4*>(v)[i];
+  for (int s0 = from + 1; s0 <= to; s0 += 8) {
+    float2 c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) c[u] = (s0 + u <= to) ? tab[s0 + u] : make_float2(0.f, 1.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (s0 + u > to) break;
+      const AdamK k = adam_consts_tab(a, c[u]);
+      adam_elem(pp.x, mm.x, vv.x, 0.f, k);
+      adam_elem(pp.y, mm.y, vv.y, 0.f, k);
+      adam_elem(pp.z, mm.z, vv.z, 0.f, k);
+      adam_elem(pp.w, mm.w, vv.w, 0.f, k);
+    }
   }
+  if (step) {
+    adam_elem(pp.x, mm.x, vv.x, gx.x, kx);
+    adam_elem(pp.y, mm.y, vv.y, gx.y, kx);
+    adam_elem(pp.z, mm.z, vv.z, gx.z, kx);
+    adam_elem(pp.w, mm.w, vv.w, gx.w, kx);
+  }
+  reinterpret_cast<float4*>(p)[i] = pp;
+  reinterpret_cast<float4*>(m)[i] = mm;
+  reinterpret_cast<float4*>(v)[i] = vv;
 }
 
 // Bring rows up to the completed step count *step: the batch's rows (item_of /
@@ -290,25 +301,32 @@ __device__ __forceinline__ void lazy_row_zero_step(const AdamK& k, float* p, flo
 __global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* __restrict__ tab, float* p, float* m,
                                                       float* v, int32_t* __restrict__ last_step,
                                                       const int32_t* __restrict__ item_of,
-                                                      const int32_t* __restrict__ n_unique, int64_t N, int64_t H) {
+                                                      const int32_t* __restrict__ n_unique, int64_t N, int64_t H,
+                                                      RowMap rm) {
   const int to = (int)load_step(a.step_dev);
   const int64_t nrows = item_of ? (int64_t)*n_unique : N;
-  const int lane = threadIdx.x & 63;
-  const int64_t gw = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
-  for (int64_t r = gw; r < nrows; r += nw) {
-    const int64_t j = item_of ? item_of[r] : r;
-    const int from = last_step[j];
-    lazy_row_catchup(a, tab, p, m, v, j, H, from, to, lane);
-    if (lane == 0 && from < to) last_step[j] = to;
+  const int64_t H4 = H / 4;
+  const int rr = threadIdx.x / rm.h4s, c0 = threadIdx.x % rm.h4s;
+  const AdamK none{};
+  for (int64_t g0 = (int64_t)blockIdx.x * rm.rpb; g0 < nrows; g0 += (int64_t)gridDim.x * rm.rpb) {
+    const int64_t r = g0 + rr;
+    const bool act = rr < rm.rpb && r < nrows;
+    const int64_t j = act ? (item_of ? (int64_t)item_of[r] : r) : 0;
+    const int from = act ? last_step[j] : to;
+    if (from < to)
+      for (int64_t c = c0; c < H4; c += rm.h4s)
+        col_update(a, tab, p, m, v, j * H4 + c, from, to, false, none, make_float4(0.f, 0.f, 0.f, 0.f));
+    __syncthreads();
+    if (act && c0 == 0 && from < to) last_step[j] = to;
   }
 }
 
 // The step's update with lazy W1t. Blocks [0, nb_rows) take the gradient rows
-// (wave per slot: replay missed steps, then step t = *step + 1 with the clipped
-// gradient); blocks [nb_rows, nb_rows + nb_sweep) bring one of kLazySweep row
-// ranges (rotating with t) through step t with g = 0 -- skipping rows with a
-// gradient, which the first group owns -- so that no row ever lags more than
-// kLazySweep steps; the rest run the dense segment. Block 0 records tab[t].
+// (replay missed steps, then step t = *step + 1 with the clipped gradient);
+// blocks [nb_rows, nb_rows + nb_sweep) bring one of kLazySweep row ranges (rotating
+// with t) through step t with g = 0 -- skipping rows with a gradient, which the first
+// group owns -- so that no row ever lags more than kLazySweep steps; the rest run the
+// dense segment. Row work is column-parallel (RowMap).
 constexpr int kLazySweep = 8;
 __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restrict__ tab, float* __restrict__ p,
                                                    float* __restrict__ m, float* __restrict__ v,
@@ -317,56 +335,74 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
                                                    const int32_t* __restrict__ item_of,
                                                    const int32_t* __restrict__ n_unique, int64_t N, int64_t H,
                                                    const float* __restrict__ g_dense, int64_t dense_off,
-                                                   int64_t n_dense, int nb_rows, int nb_sweep) {
-  const AdamK k = adam_consts(a);
-  const float coef = a.coef_dev ? *a.coef_dev : 1.f;
+                                                   int64_t n_dense, int nb_rows, int nb_sweep, RowMap rm) {
   const int t = (int)load_step(a.step_dev) + 1;
-  const int lane = threadIdx.x & 63;
-  if (blockIdx.x == 0 && threadIdx.x == 0) tab[t] = make_float2(k.lr_over_bc1, k.bc2_sqrt);
+  // tab[t] is written by hvae_clip_grad_norm_step_adam just before; a zero entry means no one did
+  const float2 c0t = tab[t];
+  const bool have = c0t.x != 0.f || c0t.y != 0.f;
+  const AdamK k = have ? adam_consts_tab(a, c0t) : adam_consts(a);
+  const float coef = a.coef_dev ? *a.coef_dev : 1.f;
+  if (!have && blockIdx.x == 0 && threadIdx.x == 0) tab[t] = make_float2(k.lr_over_bc1, k.bc2_sqrt);
   const int nu = *n_unique;
+  const int64_t H4 = H / 4;
+  const int rr = threadIdx.x / rm.h4s, cc = threadIdx.x % rm.h4s;
   if ((int)blockIdx.x < nb_rows) {
-    const int64_t H4 = H / 4;
-    for (int s = blockIdx.x * 4 + (threadIdx.x >> 6); s < nu; s += nb_rows * 4) {
-      const int64_t j = item_of[s];
-      const int from = last_step[j];
-      lazy_row_catchup(a, tab, p, m, v, j, H, from, t - 1, lane);
-      for (int64_t c = lane; c < H4; c += 64) {
-        const int64_t i = j * H4 + c;
-        float4 gv = *reinterpret_cast<const float4*>(rows + (int64_t)s * H + 4 * c);
-        gv.x *= coef; gv.y *= coef; gv.z *= coef; gv.w *= coef;
-        float4 pp = reinterpret_cast<float4*>(p)[i];
-        float4 mm = reinterpret_cast<float4*>(m)[i];
-        float4 vv = reinterpret_cast<float4*>(v)[i];
-        adam_elem(pp.x, mm.x, vv.x, gv.x, k);
-        adam_elem(pp.y, mm.y, vv.y, gv.y, k);
-        adam_elem(pp.z, mm.z, vv.z, gv.z, k);
-        adam_elem(pp.w, mm.w, vv.w, gv.w, k);
-        reinterpret_cast<float4*>(p)[i] = pp;
-        reinterpret_cast<float4*>(m)[i] = mm;
-        reinterpret_cast<float4*>(v)[i] = vv;
-      }
-      if (lane == 0) last_step[j] = t;
+    for (int64_t g0 = (int64_t)blockIdx.x * rm.rpb; g0 < nu; g0 += (int64_t)nb_rows * rm.rpb) {
+      const int64_t sidx = g0 + rr;
+      const bool act = rr < rm.rpb && sidx < nu;
+      const int64_t j = act ? (int64_t)item_of[sidx] : 0;
+      const int from = act ? last_step[j] : t;
+      if (act)
+        for (int64_t c = cc; c < H4; c += rm.h4s) {
+          float4 gv = *reinterpret_cast<const float4*>(rows + sidx * H + 4 * c);
+          gv.x *= coef; gv.y *= coef; gv.z *= coef; gv.w *= coef;
+          col_update(a, tab, p, m, v, j * H4 + c, from, t - 1, true, k, gv);
+        }
+      __syncthreads();
+      if (act && cc == 0) last_step[j] = t;
     }
   } else if ((int)blockIdx.x < nb_rows + nb_sweep) {
     const int64_t chunk = (N + kLazySweep - 1) / kLazySweep;
     const int64_t r0 = (int64_t)((t - 1) % kLazySweep) * chunk, r1 = min(N, r0 + chunk);
-    const int64_t gw = (int64_t)(blockIdx.x - nb_rows) * 4 + (threadIdx.x >> 6), nw = (int64_t)nb_sweep * 4;
-    for (int64_t j = r0 + gw; j < r1; j += nw) {
-      const int sl = slot_of[j];
-      if (sl >= 0 && sl < nu && item_of[sl] == (int32_t)j) continue;  // has a gradient: first group's row
-      const int from = last_step[j];
-      if (from >= t) continue;
-      lazy_row_catchup(a, tab, p, m, v, j, H, from, t - 1, lane);
-      lazy_row_zero_step(k, p, m, v, j, H, lane);
-      if (lane == 0) last_step[j] = t;
+    for (int64_t g0 = r0 + (int64_t)(blockIdx.x - nb_rows) * rm.rpb; g0 < r1; g0 += (int64_t)nb_sweep * rm.rpb) {
+      const int64_t j = g0 + rr;
+      bool act = rr < rm.rpb && j < r1;
+      int from = t;
+      if (act) {
+        const int sl = slot_of[j];
+        if (sl >= 0 && sl < nu && item_of[sl] == (int32_t)j) act = false;  // has a gradient: first group's row
+        else from = last_step[j];
+      }
+      act = act && from < t;
+      if (act)
+        for (int64_t c = cc; c < H4; c += rm.h4s)
+          col_update(a, tab, p, m, v, j * H4 + c, from, t - 1, true, k, make_float4(0.f, 0.f, 0.f, 0.f));
+      __syncthreads();
+      if (act && cc == 0) last_step[j] = t;
     }
   } else {
+    // the small dense parameters: float4 where the segment is 16-B aligned, scalar tail
     float* pd = p + dense_off;
     float* md = m + dense_off;
     float* vd = v + dense_off;
     const int nb_rest = nb_rows + nb_sweep;
+    const int64_t gtid = (int64_t)(blockIdx.x - nb_rest) * blockDim.x + threadIdx.x;
     const int64_t stride = (int64_t)(gridDim.x - nb_rest) * blockDim.x;
-    for (int64_t i = (int64_t)(blockIdx.x - nb_rest) * blockDim.x + threadIdx.x; i < n_dense; i += stride) {
+    const bool vec = ((((uintptr_t)pd) | ((uintptr_t)md) | ((uintptr_t)vd) | ((uintptr_t)g_dense)) % 16) == 0;
+    const int64_t n4 = vec ? n_dense / 4 : 0;
+    for (int64_t i = gtid; i < n4; i += stride) {
+      float4 pp = reinterpret_cast<float4*>(pd)[i], mm = reinterpret_cast<float4*>(md)[i];
+      float4 vv = reinterpret_cast<float4*>(vd)[i];
+      const float4 gg = reinterpret_cast<const float4*>(g_dense)[i];
+      adam_elem(pp.x, mm.x, vv.x, gg.x * coef, k);
+      adam_elem(pp.y, mm.y, vv.y, gg.y * coef, k);
+      adam_elem(pp.z, mm.z, vv.z, gg.z * coef, k);
+      adam_elem(pp.w, mm.w, vv.w, gg.w * coef, k);
+      reinterpret_cast<float4*>(pd)[i] = pp;
+      reinterpret_cast<float4*>(md)[i] = mm;
+      reinterpret_cast<float4*>(vd)[i] = vv;
+    }
+    for (int64_t i = 4 * n4 + gtid; i < n_dense; i += stride) {
       float pp = pd[i], mm = md[i], vv = vd[i];
       adam_elem(pp, mm, vv, g_dense[i] * coef, k);
       pd[i] = pp; md[i] = mm; vd[i] = vv;
@@ -427,6 +463,31 @@ extern "C" int hvae_clip_grad_norm_step(const float* g_dense, int64_t n_dense, c
                      ws, ws_bytes, stream);
 }
 
+extern "C" int hvae_clip_grad_norm_step_adam(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg,
+                                             int64_t H, float max_norm, float* norm_out, float* coef_out,
+                                             int64_t* step_dev, int64_t* step_snap, int64_t* boff, int64_t advance,
+                                             const hvae_adam* cfg, float* tab, void* ws, size_t ws_bytes,
+                                             void* stream) {
+  HVAE_REQUIRE(step_dev && step_snap && cfg && tab, "hvae_clip_grad_norm_step_adam: null step counters / cfg / tab");
+  HVAE_REQUIRE(advance == 0 || boff, "hvae_clip_grad_norm_step_adam: advance without boff");
+  HVAE_REQUIRE(coef_out && n_dense >= 0 && (n_dense == 0 || g_dense), "hvae_clip_grad_norm: bad args");
+  HVAE_REQUIRE(!rg || (rg->rows && rg->n_unique && H > 0), "hvae_clip_grad_norm: bad rowgrad");
+  if (!ws || ws_bytes < kNormBlocks * sizeof(double))
+    HVAE_FAIL(HVAE_ERR_WORKSPACE, "hvae_clip_grad_norm: workspace too small");
+  ClipArgs a{};
+  a.g = g_dense; a.n = n_dense;
+  a.rows = rg ? rg->rows : nullptr; a.n_unique = rg ? rg->n_unique : nullptr; a.H = H;
+  a.part = (double*)ws;
+  if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
+  a.max_norm = max_norm; a.norm_out = norm_out; a.coef_out = coef_out;
+  a.step = step_dev; a.step_snap = step_snap; a.boff = boff; a.advance = advance;
+  a.tab = (float2*)tab; a.lr = cfg->lr; a.b1 = cfg->beta1; a.b2 = cfg->beta2;
+  ProbeScope probe("clip", as_stream(stream));
+  k_clip_norm<<<kNormBlocks, 256, 0, as_stream(stream)>>>(a);
+  HVAE_LAUNCH_CHECK("k_clip_norm");
+  return HVAE_OK;
+}
+
 extern "C" int hvae_adam_dense(const hvae_adam* cfg, float* p, float* m, float* v, const float* g,
                                int64_t n, void* stream) {
   HVAE_REQUIRE(cfg && (n == 0 || (p && m && v && g)), "hvae_adam_dense: bad args");
@@ -480,11 +541,12 @@ extern "C" int hvae_adam_lazy_catchup(const hvae_adam* cfg, const float* tab, fl
   HVAE_REQUIRE(!rows || (rows->item_of && rows->n_unique), "hvae_adam_lazy_catchup: bad row list");
   if (N == 0) return HVAE_OK;
   const int64_t nrows = rows ? rows->cap : N;
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(nrows, 4), 16384));
+  const RowMap rm = row_map(H);
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(nrows, rm.rpb), 16384));
   ProbeScope probe("adam_catchup", as_stream(stream));
   k_adam_catchup<<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v, last_step,
                                                       rows ? rows->item_of : nullptr,
-                                                      rows ? rows->n_unique : nullptr, N, H);
+                                                      rows ? rows->n_unique : nullptr, N, H, rm);
   HVAE_LAUNCH_CHECK("k_adam_catchup");
   return HVAE_OK;
 }
@@ -501,13 +563,14 @@ extern "C" int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len,
   HVAE_REQUIRE(tab_len >= 2, "hvae_adam_lazy: step table too short");
   const int64_t N = rg->n_items;
   HVAE_REQUIRE(rg->slot_of, "hvae_adam_lazy: rowgrad without slot_of");
-  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, 4), 4096));
-  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, kLazySweep), 4), 4096));
-  const int64_t b_dense = std::min<int64_t>(cdiv(n_dense, 256), 2048);
+  const RowMap rm = row_map(H);
+  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, rm.rpb), 4096));
+  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, kLazySweep), rm.rpb), 4096));
+  const int64_t b_dense = std::min<int64_t>(cdiv(cdiv(n_dense, 4), 256), 512);
   ProbeScope probe("adam_rows", as_stream(stream));
   k_adam_lazy<<<(unsigned)(b_rows + b_sweep + b_dense), 256, 0, as_stream(stream)>>>(
       to_args(cfg), (float2*)tab, p, m, v, last_step, rg->rows, rg->slot_of, rg->item_of, rg->n_unique, N, H,
-      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep);
+      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep, rm);
   HVAE_LAUNCH_CHECK("k_adam_lazy");
   return HVAE_OK;
 }

@@ -118,6 +118,8 @@ SIGNATURES = {
     "hvae_adam_dense": (cint, [P(Adam), vp, vp, vp, vp, i64, vp]),
     "hvae_adam_rows": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp]),
     "hvae_adam_flat": (cint, [P(Adam), vp, vp, vp, P(RowGrad), i64, i64, vp, i64, i64, vp]),
+    "hvae_clip_grad_norm_step_adam": (cint, [vp, i64, P(RowGrad), i64, f32, vp, vp, vp, vp, vp, i64, P(Adam), vp,
+                                             vp, sz, vp]),
     "hvae_adam_lazy": (cint, [P(Adam), vp, i64, vp, vp, vp, vp, P(RowGrad), i64, vp, i64, i64, vp]),
     "hvae_adam_lazy_catchup": (cint, [P(Adam), vp, vp, vp, vp, vp, P(RowGrad), i64, i64, vp]),
     "hvae_counter_add": (cint, [vp, i64, vp]),

@@ -526,11 +526,18 @@ class FusedTrainer:
         st = torch.cuda.current_stream(self.device).cuda_stream
         H = lay.hidden
         ws, wsn = ptr(bf.ws), bf.ws.numel()
-        check(L_.hvae_clip_grad_norm_step(ptr(self.g_small), lay.n_small, rg.ref, H[0], self.max_norm,
-                                          ptr(self.norm), ptr(self.coef), ptr(self.step_dev), ptr(self.step_snap),
-                                          ptr(self.boff) if advance else None, advance, ws, wsn, st),
-              "clip_grad_norm_step")
         cfg = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_snap, self.coef)
+        if self.lazy_adam:  # the clip's last block also writes the step's Adam scalars into the step table
+            check(L_.hvae_clip_grad_norm_step_adam(ptr(self.g_small), lay.n_small, rg.ref, H[0], self.max_norm,
+                                                   ptr(self.norm), ptr(self.coef), ptr(self.step_dev),
+                                                   ptr(self.step_snap), ptr(self.boff) if advance else None, advance,
+                                                   C.byref(cfg), ptr(self.adam_tab), ws, wsn, st),
+                  "clip_grad_norm_step_adam")
+        else:
+            check(L_.hvae_clip_grad_norm_step(ptr(self.g_small), lay.n_small, rg.ref, H[0], self.max_norm,
+                                              ptr(self.norm), ptr(self.coef), ptr(self.step_dev),
+                                              ptr(self.step_snap), ptr(self.boff) if advance else None, advance,
+                                              ws, wsn, st), "clip_grad_norm_step")
         # W1t (row-sparse gradient, offset 0 of the flat buffer) and the dense segment in one launch
         if self.lazy_adam:
             check(L_.hvae_adam_lazy(C.byref(cfg), ptr(self.adam_tab), self.tab_len, ptr(self.flat), ptr(self.m),
