@@ -435,7 +435,7 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   }
   if constexpr (DS == 2) {  // |u| over the partner's half too (the score bound needs the whole row)
     const int obase = (1 - dh) * DW;
-#pragma unroll 1
+#pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       if (user < nb) {
         const float4 a = *reinterpret_cast<const float4*>(U + user * ldu + obase + 16 * ks + 8 * h);
@@ -875,6 +875,8 @@ struct FinArgs {
   const float* kl_rows; float beta; float* loss3; double* accum3; unsigned* ticket;  // fused loss (optional)
 };
 
+constexpr int kFinEB = 16;  // CSR entries per batch of the finalize's sparse-term loads
+
 // GRP: the merge of many split partials (> 8) by split groups (memory-level parallelism at small
 // batches); otherwise one thread per column walks the splits in order (fewer registers, more blocks
 // per CU at large batches)
@@ -888,6 +890,21 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
   const int64_t D = a.D;
+  // the batch row's CSR entries: located and the first kFinEB fetched now, under the merge's loads
+  int64_t sp_beg = 0, sp_end = 0;
+  int sp_j[kFinEB];
+  float sp_x[kFinEB];
+  if (a.row_ptr) {
+    const int64_t r = batch_row(a.rows, a.rows_offset, b);
+    sp_beg = a.row_ptr[r];
+    sp_end = a.row_ptr[r + 1];
+  }
+#pragma unroll
+  for (int u = 0; u < kFinEB; ++u) {
+    const int64_t e = sp_beg + u;
+    sp_j[u] = e < sp_end ? a.col_idx[e] : 0;
+    sp_x[u] = e < sp_end ? a.vals[e] : 0.f;
+  }
   if (tid == 0) any_flag = 0;
   __syncthreads();
   float lse_b;
@@ -1012,20 +1029,33 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     }
   }
   if (!a.row_ptr) return;
-  // ---- sparse terms against the fp32 E
-  const int64_t r = batch_row(a.rows, a.rows_offset, b);
-  const int64_t beg = a.row_ptr[r], end = a.row_ptr[r + 1];
+  // ---- sparse terms against the fp32 E, in ascending entry order; entries EB at a time with all their
+  // E loads in flight together (the first chunk's indices were fetched before the merge)
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float n = 0.f;
-#pragma unroll 4
-  for (int64_t e = beg; e < end; ++e) {
-    const int64_t j = a.col_idx[e];
-    const float x = a.vals[e];
-    n += x;
+  for (int64_t e0 = sp_beg; e0 < sp_end; e0 += kFinEB) {
+    if (e0 != sp_beg) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t d = tid + 256 * k;
-      if (d < D) acc[k] += x * a.E32[j * D + d];
+      for (int u = 0; u < kFinEB; ++u) {
+        const int64_t e = e0 + u;
+        sp_j[u] = e < sp_end ? a.col_idx[e] : 0;
+        sp_x[u] = e < sp_end ? a.vals[e] : 0.f;
+      }
+    }
+    float ev[kFinEB][4];
+#pragma unroll
+    for (int u = 0; u < kFinEB; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int64_t d = tid + 256 * k;
+        ev[u][k] = (e0 + u < sp_end && d < D) ? a.E32[(int64_t)sp_j[u] * D + d] : 0.f;
+      }
+#pragma unroll
+    for (int u = 0; u < kFinEB; ++u) {
+      if (e0 + u >= sp_end) break;
+      n += sp_x[u];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += sp_x[u] * ev[u][k];
     }
   }
   float dot = 0.f;
