@@ -166,7 +166,7 @@ def main():
     B = w["batch"]
     n_per_epoch = len(users) // B
     beta = ConstBeta(w["beta"])
-    gen = torch.Generator().manual_seed(rank)
+    gen = torch.Generator(device=device).manual_seed(rank)  # epoch orders drawn on the GPU
 
     def run(nsteps):
         done = 0

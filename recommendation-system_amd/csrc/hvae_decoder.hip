@@ -343,7 +343,7 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
 // wave) and small batches (64 users per block keeps all 4 waves busy).
 constexpr float kLog2e = 1.4426950408889634f;
 #ifndef DEC2_G1_AHEAD
-#define DEC2_G1_AHEAD 1
+#define DEC2_G1_AHEAD 2
 #endif
 #ifndef DEC2_G2_AHEAD
 #define DEC2_G2_AHEAD 1
@@ -398,6 +398,7 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   constexpr int NS = d2_stages<D, DS, NW>();
   constexpr int UPB = 32 * NW / DS;
   constexpr int HALF = NW / 2;          // DS = 2: partner wave = w ^ HALF
+  constexpr bool kSpread = DS == 2 && NS >= 3;  // LDS-DMA pieces issued between GEMM1's MFMA pairs
   static_assert(NW == 4 || (NW == 8 && DS == 2), "8-wave blocks split D");
   static_assert(DW % 32 == 0 && KS % 2 == 0, "D / DS must be a multiple of 32");
   static_assert(NS >= 2, "LDS ring too small");
@@ -461,14 +462,20 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(E), (short)0, (int)(N * D * 2), 0x00020000);
   const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
-  auto issue = [&](int64_t t, int slot_i) {
+  // pieces [i0, i1) of this wave's share of tile t into ring slot slot_i
+  auto issue_range = [&](int64_t t, int slot_i, int i0, int i1) {
     const uint32_t soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(kBfTI * D * 2)));
     const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
 #pragma unroll
-    for (int i = 0; i < PW; ++i)
-      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                   :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
+    for (int i = i0; i < i1; ++i)
+      if (i == i0)  // soff may be fresh from v_readfirstlane: 5 wait states before a buffer op reads it
+        asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
+      else
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
   };
+  auto issue = [&](int64_t t, int slot_i) { issue_range(t, slot_i, 0, PW); };
   auto lds_fence = [] { asm volatile("" ::: "memory"); };
 
   // GEMM2 operand addressing (T10): group g16 = lane >> 4 reads 4 item rows x 16 d columns;
@@ -604,7 +611,14 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
     __builtin_amdgcn_s_barrier();
     lds_fence();
     const int nxt = cur == NS - 1 ? 0 : cur + 1;
-    if (NS >= 3) issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
+    // NS >= 3: tile t + NS - 1 goes into the slot every wave finished with (GEMM2(t - 1), before the
+    // barrier above). DS = 2 spreads its LDS-DMA pieces over GEMM1(t + 1)'s MFMA pairs (below), where
+    // their issue cost hides behind the MFMA pipe (d = 768: 2.82 -> 2.71 ms); DS = 1 issues them in one
+    // burst here (spread over GEMM1's row reads they cost more, 586 -> 611 us at Syn-1M; over GEMM2's
+    // transposed reads, 580 -> 610 us; after GEMM2's issue, 589 -> 597 us).
+    const int64_t t_dma = min(t + NS - 1, t_end - 1);
+    const int s_dma = cur == 0 ? NS - 1 : cur - 1;
+    if (NS >= 3 && (!kSpread || !wave_active)) issue(t_dma, s_dma);  // idle waves still load their share
     if constexpr (DS == 2 && XB == 1) {  // single exchange buffer: everyone has read S(t) before S(t+1) lands
       if (wave_active) xadd((int)(t & 1), s_cur);
       lds_fence();
@@ -642,14 +656,15 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
           if (r & 1) pk[r >> 1] = pack_bf16x2(pv[r - 1], pv[r]);
         }
       };
-      f32x16 s_nx = s_cur;
-      if (more) {
-        constexpr int NG = KS / 2;
-        s_nx = gemm1(lds + nxt * TB, [&](int g) { smax_rows(16 * g / NG, 16 * (g + 1) / NG); });
-        if (DS == 2) xput((int)((t + 1) & 1), s_nx);
-      } else {
-        smax_rows(0, 16);
-      }
+      // One code path for every tile: the last tile of a split also runs a GEMM1 (over a stale ring slot,
+      // result unused), so that the softmax stays spread over the MFMA pairs instead of being hoisted
+      // (with its 16 live exponent arguments) into a block shared with a separate last-tile path.
+      constexpr int NG = KS / 2;
+      f32x16 s_nx = gemm1(lds + nxt * TB, [&](int g) {
+        smax_rows(16 * g / NG, 16 * (g + 1) / NG);
+        if (kSpread && PW * g / NG < PW * (g + 1) / NG) issue_range(t_dma, s_dma, PW * g / NG, PW * (g + 1) / NG);
+      });
+      if (DS == 2 && more) xput((int)((t + 1) & 1), s_nx);
       bf16x8 pf[2];
       pf[0] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
       pf[1] = __builtin_bit_cast(bf16x8, make_uint4(pk[4], pk[5], pk[6], pk[7]));

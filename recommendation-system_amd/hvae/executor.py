@@ -602,7 +602,10 @@ class FusedTrainer:
         if n == 0:
             return {"total_loss": float("nan"), "recon_loss": float("nan"), "kl_loss": float("nan")}
         if shuffle:
-            order = torch.randperm(n, generator=generator)
+            # a device generator draws the order on the GPU (no host stall at the epoch boundary); the
+            # default CPU generator keeps DataLoader(shuffle=True)'s exact order
+            order = torch.randperm(n, generator=generator,
+                                   device=generator.device if generator is not None else "cpu")
             data.perm.copy_(data.users[order.to(self.device)])
         else:
             order = None
@@ -626,7 +629,7 @@ class FusedTrainer:
         M = 0
         if dp is not None:  # fixed exchange size for the epoch: one host all-reduce, no per-step sync
             from .dist import batch_unique_counts
-            users_h = data.users_host if order is None else data.users_host[order.numpy()]
+            users_h = data.users_host if order is None else data.users_host[order.cpu().numpy()]
             counts = batch_unique_counts(data.host_indptr, data.host_indices,
                                          users_h[: n_full * B + (tail if tail else 0)], B)
             M = dp.plan_epoch(counts)
