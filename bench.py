@@ -53,6 +53,7 @@ WORKLOADS = {
 
 PEAK_HBM_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md, spec)
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA
+PEAK_FP8_TFLOPS = 5000.0   # dense fp8 (block-scaled e4m3) MFMA
 PEAK_F32_TFLOPS = 157.3    # f32 MFMA = f32 vector rate
 
 
@@ -126,7 +127,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--workload", default="all_beauty", choices=sorted(WORKLOADS))
     ap.add_argument("--batch-size", type=int, default=None)
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe-steps", type=int, default=50)
@@ -217,7 +218,8 @@ def main():
     #    unique W1t rows and of the 1/8 of W1t rows its rotating g = 0 sweep brings up to date (plus 4 B of
     #    slot lookup and 4 B of step stamp per swept row), and p, m, v, g (28 B) of the dense small params;
     #    with HVAE_DENSE_ADAM=1 (dense torch semantics every step) all N rows.
-    #  decoder_sweep: 4 B N D flops (S = U E^T, O = P E); bytes = bf16 E read once + U read + O written.
+    #  decoder_sweep: 4 B N D flops (S = U E^T, O = P E); bytes = E read once (bf16 2 B, fp8 1 B, fp32 4 B per
+    #    element) + U read + O written.
     uniq = mean_unique_items(X, users, B, gen_seed=rank)
     n_small = fused.layout.n_small
     if fused.lazy_adam:
@@ -226,8 +228,8 @@ def main():
     else:
         adam_bytes = 24.0 * N * H + 4.0 * N + 28.0 * n_small
     dec_flops = 4.0 * B * N * D
-    dec_bytes = (2.0 if args.precision == "bf16" else 4.0) * N * D + 8.0 * B * D
-    dec_peak = PEAK_BF16_TFLOPS if args.precision == "bf16" else PEAK_F32_TFLOPS
+    dec_bytes = {"bf16": 2.0, "fp8": 1.0, "fp32": 4.0}[args.precision] * N * D + 8.0 * B * D
+    dec_peak = {"bf16": PEAK_BF16_TFLOPS, "fp8": PEAK_FP8_TFLOPS, "fp32": PEAK_F32_TFLOPS}[args.precision]
     t_adam, t_dec = kernels["adam_rows"][0], kernels["decoder_sweep"][0]
     roof = {
         "adam_rows": {"bound": "hbm", "achieved": adam_bytes / t_adam / 1e9, "peak": PEAK_HBM_GBS,
@@ -245,7 +247,8 @@ def main():
     dom = max(roof, key=lambda k: kernels[k][0])
     r = roof[dom]
     traffic = None
-    pmc = ROOT / "profiles" / f"pmc_{args.workload}.json"
+    pmc = ROOT / "profiles" / (f"pmc_{args.workload}.json" if args.precision == "bf16"
+                               else f"pmc_{args.workload}_{args.precision}.json")
     if pmc.exists():
         try:
             traffic = json.loads(pmc.read_text()).get(dom, {}).get("hbm_bytes_per_launch")

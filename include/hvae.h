@@ -37,7 +37,7 @@ enum {
   HVAE_ERR_WORKSPACE = -4    /* workspace smaller than the *_workspace() query */
 };
 
-enum { HVAE_F32 = 0, HVAE_BF16 = 1 };
+enum { HVAE_F32 = 0, HVAE_BF16 = 1, HVAE_FP8 = 2 };
 
 /* ----------------------------------------------------------------- misc -- */
 int hvae_version(void);
@@ -237,13 +237,20 @@ int hvae_reparam_kl_bwd(const float* dz, const float* mu, const float* logvar, i
  * Replaces torch.matmul(u, E.t()) (src/ml/model.py:198), F.log_softmax
  * (src/ml/model.py:281) and their autograd. dtype HVAE_BF16: E is a bf16 copy,
  * U is rounded to bf16, MFMA 32x32x16 bf16 with f32 accumulation, and
- * e_maxnorm (device scalar, hvae_row_norm_max) bounds the scores; HVAE_F32:
- * exact-f32 MFMA (e_maxnorm unused). ws >= hvae_decoder_workspace() bytes. */
+ * e_maxnorm (device scalar, hvae_row_norm_max) bounds the scores; HVAE_FP8:
+ * block-scaled e4m3 MFMA 32x32x64 (E with one power-of-two scale, U with one
+ * per user, P block floating point per user and 64-item tile), e_maxnorm as
+ * for bf16 (take it from the image's bf16 part); HVAE_F32: exact-f32 MFMA
+ * (e_maxnorm unused). ws >= hvae_decoder_workspace() bytes. */
 /* The decoder's image of the frozen embeddings, built once per model:
  *   HVAE_BF16: E rounded to bf16 [N, D], then (at a 256-B aligned offset) the
  *              same values tile-transposed, [ceil(N/32)][D][32] with items in the
  *              MFMA k order, so that both products of the sweep read LDS tiles
  *              with plain 16-B reads;
+ *   HVAE_FP8:  the bf16 E [N, D] as above (score bound, exact fixups), then at a
+ *              256-B aligned offset ceil(N/64) tiles of 128 D bytes of e4m3 in
+ *              MFMA fragment order (both products' operands), then the int
+ *              exponent ke of E's scale (E8 = E 2^ke); D % 64 == 0;
  *   HVAE_F32:  E itself [N, D].
  * Every `E` argument of the decoder functions below is this image. */
 size_t hvae_decoder_image_bytes(int dtype, int64_t N, int64_t D);

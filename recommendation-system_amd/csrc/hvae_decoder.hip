@@ -716,6 +716,263 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------------------- fp8 ---
+// The same sweep on the block-scaled fp8 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, OCP e4m3 operands,
+// twice the bf16 rate; BASELINE configs[4]). Both products carry exact power-of-two scales:
+//   GEMM1 S^T = E_tile U^T: E8 = E 2^ke (one exponent for the whole matrix, from max|E|), u8 = u 2^ku
+//     (one exponent per user, from max|u_b|); the MFMA's scale operands undo both, so S^T is fp32 scores
+//     of the quantised operands.
+//   GEMM2 O^T += E_tile^T P^T: P is block floating point, q = p 2^-e with one exponent e per user and
+//     64-item tile (max q in [128, 256]), passed as that user's B scale; p itself never needs a range.
+// Scale semantics (scripts/probe_fp8_mfma.hip on MI355X): element j of lane half h belongs to k-block
+// j >> 4, whose scale lane (row | column) + 32 (j >> 4) supplies; the decoder gives both lanes of a row or
+// column the same exponent, so it depends only on A and B sharing the (h, j) -> k slot map.
+// Tiles of 64 items (GEMM2's K); the image stores both operands in MFMA fragment order (below), so
+// every operand read is a pair of conflict-free 1-KiB ds_read_b128 rows and the LDS-DMA is a plain copy.
+// 4 waves x 32 users per block, each over all D (D <= 384: U 48 + O 192 registers); the softmax of tile
+// t is spread over GEMM1(t+1)'s MFMAs, as in k_dec2_bf16.
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+constexpr int kF8TI = 64;  // items per tile
+
+template <int D>
+constexpr int f8_tile_bytes() { return 128 * D; }  // GEMM1 fragments (64 D) + GEMM2 fragments (64 D)
+template <int D>
+constexpr int f8_stages() { return (160 * 1024) / f8_tile_bytes<D>() >= 6 ? 6 : (160 * 1024) / f8_tile_bytes<D>(); }
+// fp8 image: bf16 E [N][D] (exact fixups, score bound) | fp8 tiles [ntiles][128 D] | int ke
+static inline int64_t f8_offset_bytes(int64_t N, int64_t D) { return et_offset_bytes(N, D); }
+static inline int64_t f8_tail_offset(int64_t N, int64_t D) {
+  return f8_offset_bytes(N, D) + (N + kF8TI - 1) / kF8TI * 128 * D;
+}
+// item (within its tile) of element j of lane half h in a GEMM2 fragment: the row order of the two
+// 32x32 S^T accumulators (j < 16: first, j >= 16: second), so P packs from them in place
+__host__ __device__ constexpr int f8_item_of(int h, int j) {
+  return 32 * (j >> 4) + (j & 3) + 8 * ((j & 15) >> 2) + 4 * h;
+}
+__device__ __forceinline__ int pack_fp8x4(float a, float b, float c, float d) {
+  const int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);
+}
+
+template <int D, bool WITH_O>
+__global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, int64_t ldu,
+                                                 const unsigned char* __restrict__ T8, const int* __restrict__ e_exp,
+                                                 const float* __restrict__ e_maxnorm, int64_t nb, int64_t N,
+                                                 int splits, int64_t tiles_per_split, DecOut out) {
+  constexpr int KS = D / 64;             // GEMM1 k-steps
+  constexpr int DB = D / 32;             // GEMM2 d-blocks
+  constexpr int TB = f8_tile_bytes<D>();
+  constexpr int PW = TB / 4096;          // 1-KiB LDS-DMA pieces per wave per tile
+  constexpr int NS = f8_stages<D>();
+  static_assert(D % 64 == 0 && D <= 384 && NS >= 3, "fp8 decoder: D in {64, ..., 384}");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int split = blockIdx.x % splits;
+  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 128 + w * 32;
+  const int64_t user = u0 + col;
+  const bool wave_active = u0 < nb;
+  const int64_t ntiles = (N + kF8TI - 1) / kF8TI;
+  const int64_t t_beg = (int64_t)split * tiles_per_split;
+  const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
+  const float emax = *e_maxnorm;  // scalars before any LDS-DMA is in flight
+  const int ke = *e_exp;
+  const int sa = 127 - ke;        // A scale (E8 = E 2^ke)
+
+  // U: lane (col, h) holds u[64 ks + 32 h + j], j < 32, as e4m3 of u 2^ku
+  float amax = 0.f, usq = 0.f;
+  if (user < nb) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int q4 = 0; q4 < 8; ++q4) {
+        const float4 a = *reinterpret_cast<const float4*>(U + user * ldu + 64 * ks + 32 * h + 4 * q4);
+        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+        usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
+      }
+  }
+  amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+  usq += __shfl_xor(usq, 32, 64);
+  int eu = 0;
+  (void)frexpf(amax, &eu);                               // amax = m 2^eu, m in [0.5, 1)
+  const int ku = amax > 0.f ? min(127, 8 - eu) : 0;      // max |u 2^ku| <= 256 (e4m3 max 448)
+  const int sbu = 127 - ku;
+  const float qu = ldexpf(1.f, ku);
+  i32x8 uf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+    for (int q4 = 0; q4 < 8; ++q4) {
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (user < nb) a = *reinterpret_cast<const float4*>(U + user * ldu + 64 * ks + 32 * h + 4 * q4);
+      uf[ks][q4] = pack_fp8x4(a.x * qu, a.y * qu, a.z * qu, a.w * qu);
+    }
+
+  // LDS-DMA: tile bytes [(w PW + i) KiB, +1 KiB) of the tile into the same place of the ring slot
+  int voff[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) voff[i] = (w * PW + i) * 1024 + lane * 16;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(T8), (short)0, (int)(ntiles * TB), 0x00020000);
+  const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
+  auto issue = [&](int64_t t, int slot_i) {
+    const uint32_t soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)TB));
+    const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
+#pragma unroll
+    for (int i = 0; i < PW; ++i)
+      if (i == 0)  // soff may be fresh from v_readfirstlane: 5 wait states before a buffer op reads it
+        asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
+      else
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
+  };
+  auto lds_fence = [] { asm volatile("" ::: "memory"); };
+  // fragment f of a tile slot: 16 B at lane * 16 of its two 1-KiB rows
+  auto frag = [&](const unsigned char* buf, int f) {
+    const uint4 x = *reinterpret_cast<const uint4*>(buf + f * 2048 + lane * 16);
+    const uint4 y = *reinterpret_cast<const uint4*>(buf + f * 2048 + 1024 + lane * 16);
+    i32x8 r;
+    r[0] = (int)x.x; r[1] = (int)x.y; r[2] = (int)x.z; r[3] = (int)x.w;
+    r[4] = (int)y.x; r[5] = (int)y.y; r[6] = (int)y.z; r[7] = (int)y.w;
+    return r;
+  };
+  // GEMM1: S^T of items 0-31 (s0) and 32-63 (s1) of the tile; fragments 2 ks + half
+  auto gemm1 = [&](const unsigned char* buf, f32x16& s0, f32x16& s1, auto&& fill) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
+    i32x8 a0 = frag(buf, 0), a1 = frag(buf, 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const i32x8 c0 = a0, c1 = a1;
+      if (ks + 1 < KS) { a0 = frag(buf, 2 * ks + 2); a1 = frag(buf, 2 * ks + 3); }
+      s0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c0, uf[ks], s0, 0, 0, 0, sa, 0, sbu);
+      s1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c1, uf[ks], s1, 0, 0, 0, sa, 0, sbu);
+      fill(ks);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  f32x16 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  float m = 0.f, mL = 0.f, lsum = 0.f;
+  f32x16 c0, c1;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) { c0[r] = 0.f; c1[r] = 0.f; }
+
+  constexpr int PRE = NS - 1;  // tiles in flight before the loop
+  if (t_beg < t_end) {
+#pragma unroll
+    for (int i = 0; i < PRE; ++i) issue(min(t_beg + i, t_end - 1), i);
+    wait_vmcnt<(PRE - 1) * PW>();
+  }
+  lds_fence();
+  __builtin_amdgcn_s_barrier();
+  lds_fence();
+  if (t_beg < t_end && wave_active) gemm1(lds, c0, c1, [](int) {});
+  const float bound = sqrtf(usq) * emax * 1.02f;
+
+  int cur = 0;
+  for (int64_t t = t_beg; t < t_end; ++t) {
+    wait_vmcnt<(NS - 3) * PW>();  // tile t + 1 has landed
+    lds_fence();
+    __builtin_amdgcn_s_barrier();
+    lds_fence();
+    const int nxt = cur == NS - 1 ? 0 : cur + 1;
+    // tile t + NS - 1 into the slot of tile t - 1 (every wave finished its GEMM2 before the barrier)
+    issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
+    if (wave_active) {
+      if (t == ntiles - 1 && (N % kF8TI) != 0) {  // items past N (read as 0) leave the softmax
+        const int lim = (int)(N - t * kF8TI) - 4 * h;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int it = (r & 3) + 8 * (r >> 2);
+          c0[r] = it >= lim ? -INFINITY : c0[r];
+          c1[r] = it + 32 >= lim ? -INFINITY : c1[r];
+        }
+      }
+      float mx = fmaxf(c0[0], c1[0]);
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(c0[r], c1[r]));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (t == t_beg) {  // fixed per-split offset, as k_dec2_bf16
+        m = fmaxf(mx, bound - kOffsetSpan);
+        mL = m * kLog2e;
+      }
+      // P block exponent of this (user, tile): q = exp2(s log2e - mL - e) <= 2^8
+      const int e = max(-119, min(127, (int)ceilf(__builtin_fmaf(mx, kLog2e, -mL)) - 8));
+      const float cE = mL + (float)e;
+      float qv[32];
+      int pk[8];
+      float qsum = 0.f;
+      auto smax = [&](int j0, int j1) {
+#pragma unroll
+        for (int j = j0; j < j1; ++j) {
+          const float s = j < 16 ? c0[j & 15] : c1[j & 15];
+          qv[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s, kLog2e, -cE));
+          qsum += qv[j];
+          if ((j & 3) == 3) pk[j >> 2] = pack_fp8x4(qv[j - 3], qv[j - 2], qv[j - 1], qv[j]);
+        }
+      };
+      f32x16 n0, n1;
+      gemm1(lds + nxt * TB, n0, n1, [&](int g) { smax(32 * g / KS / 4 * 4, 32 * (g + 1) / KS / 4 * 4); });
+      lsum += ldexpf(qsum, e);
+      if constexpr (WITH_O) {
+        i32x8 pf;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pf[i] = pk[i];
+        const int sbp = 127 + e;
+        const unsigned char* buf = lds + cur * TB + 64 * D;
+        i32x8 a = frag(buf, 0);
+#pragma unroll
+        for (int db = 0; db < DB; ++db) {
+          const i32x8 c = a;
+          if (db + 1 < DB) a = frag(buf, db + 1);
+          o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
+        }
+      }
+      c0 = n0;
+      c1 = n1;
+    }
+    cur = nxt;
+  }
+
+  if (!wave_active) return;
+  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  if (user >= nb) return;
+  if (h == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
+  if (out.direct) {
+    const float inv = 1.0f / ltot;
+    if (h == 0) out.lse[user] = m + logf(ltot);
+    if (WITH_O) {
+#pragma unroll
+      for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int dd = 32 * d + 8 * g4 + 4 * h;
+          *reinterpret_cast<float4*>(out.O + user * D + dd) =
+              make_float4(o[d][4 * g4] * inv, o[d][4 * g4 + 1] * inv, o[d][4 * g4 + 2] * inv, o[d][4 * g4 + 3] * inv);
+        }
+    }
+  } else {
+    const int64_t pi = (int64_t)split * nb + user;
+    if (h == 0) { out.m[pi] = m; out.l[pi] = ltot; }
+    if (WITH_O) {
+#pragma unroll
+      for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int dd = 32 * d + 8 * g4 + 4 * h;
+          *reinterpret_cast<float4*>(out.O + pi * D + dd) =
+              make_float4(o[d][4 * g4], o[d][4 * g4 + 1], o[d][4 * g4 + 2], o[d][4 * g4 + 3]);
+        }
+    }
+  }
+}
+
 // ------------------------------------------------------------------- f32 ---
 // Same algorithm on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 sums):
 // 4 waves x 16 users, 16-item tiles, LDS rows padded to D+2 floats
@@ -1153,6 +1410,47 @@ __global__ void __launch_bounds__(256) k_build_image(const float* __restrict__ E
   }
 }
 
+// fp8 tiles of the fp8 image: per 64-item tile, GEMM1 fragments f = 2 ks + half (lane l: item 32 half + (l & 31),
+// d = 64 ks + 32 (l >> 5) + j) then GEMM2 fragments db (lane l: d = 32 db + (l & 31), item f8_item_of(l >> 5, j)),
+// each fragment [2 parts][64 lanes][16 B] with element j = 16 part + byte. E8 = e4m3(E 2^ke), ke from max |E|.
+__global__ void __launch_bounds__(256) k_build_f8(const float* __restrict__ E32, int64_t N, int64_t D, int64_t ntiles,
+                                                  const unsigned* __restrict__ amax_bits, unsigned char* __restrict__ T8,
+                                                  int* __restrict__ ke_out) {
+  const float amax = __uint_as_float(*amax_bits);
+  int ea = 0;
+  (void)frexpf(amax, &ea);
+  const int ke = amax > 0.f ? min(127, 8 - ea) : 0;  // max |E 2^ke| <= 256
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ke_out = ke;
+  const float qs = ldexpf(1.f, ke);
+  const int64_t TB = 128 * D, words = ntiles * TB / 4;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
+    const int64_t t = (i * 4) / TB;
+    const int r0 = (int)((i * 4) % TB);
+    float v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int rr = r0 + k;
+      const int g = rr < 64 * D ? rr : rr - 64 * (int)D;
+      const int f = g >> 11, part = (g >> 10) & 1, ln = (g >> 4) & 63, j = 16 * part + (g & 15);
+      int64_t item;
+      int64_t d;
+      if (rr < 64 * D) { item = t * kF8TI + 32 * (f & 1) + (ln & 31); d = 64 * (f >> 1) + 32 * (ln >> 5) + j; }
+      else { item = t * kF8TI + f8_item_of(ln >> 5, j); d = 32 * f + (ln & 31); }
+      v[k] = item < N ? E32[item * D + d] * qs : 0.f;
+    }
+    reinterpret_cast<int*>(T8)[i] = pack_fp8x4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_abs_max(const float* __restrict__ x, int64_t n, unsigned* __restrict__ out_bits) {
+  float best = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    best = fmaxf(best, fabsf(x[i]));
+  best = wave_max(best);
+  if ((threadIdx.x & 63) == 0) atomicMax(out_bits, __float_as_uint(best));
+}
+
 // max_i ||E_i||_2 over an fp32 or bf16 [N, D] matrix (score bound of the bf16 path).
 __global__ void __launch_bounds__(256) k_row_norm_max(int dtype, const void* __restrict__ E, int64_t N, int64_t D,
                                                       unsigned* __restrict__ out_bits) {
@@ -1217,6 +1515,19 @@ static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
 
 static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   DecPlan p{};
+  if (dtype == HVAE_FP8) {  // k_dec_fp8: 128 users per block, 64-item tiles
+    p.upb = 128;
+    const int64_t nub = cdiv(nb, p.upb), tiles = cdiv(N, kF8TI);
+    int64_t s = cdiv(256, nub);
+    s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 2));
+    s = std::min<int64_t>(s, std::max<int64_t>(1, N / std::max<int64_t>(1, 2 * nb)));
+    if (s >= 8) s = s / 8 * 8;
+    if (dec_forced_splits() > 0) s = dec_forced_splits();
+    dec_set_splits(p, tiles, s);
+    if (p.splits >= 8 && p.splits % 8 && dec_forced_splits() <= 0) dec_set_splits(p, tiles, (int64_t)p.splits / 8 * 8);
+    p.blocks = nub * p.splits;
+    return p;
+  }
   const bool bf = dtype == HVAE_BF16;
   p.v2 = bf && !dec_use_v1() && v2_supported(D);
   p.ds = p.v2 && (D > 384 || nb <= 64) ? 2 : 1;
@@ -1294,6 +1605,22 @@ static int launch_bf16_v2(const float* U, int64_t ldu, const void* E, const floa
 }
 
 template <int D, bool WO>
+static int launch_fp8(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                      const DecPlan& p, DecOut o, hipStream_t st) {
+  constexpr int lds = f8_stages<D>() * f8_tile_bytes<D>();
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec_fp8<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr_set = true;
+  }
+  const unsigned char* T8 = (const unsigned char*)E + f8_offset_bytes(N, D);
+  const int* ke = (const int*)((const char*)E + f8_tail_offset(N, D));
+  k_dec_fp8<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, T8, ke, enorm, nb, N, p.splits, p.tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec_fp8");
+  return HVAE_OK;
+}
+
+template <int D, bool WO>
 static int launch_f32(const float* U, int64_t ldu, const void* E, int64_t nb, int64_t N, const DecPlan& p,
                       DecOut o, hipStream_t st) {
   constexpr int lds = 2 * f32_tile_bytes<D>();
@@ -1311,7 +1638,14 @@ static int launch_f32(const float* U, int64_t ldu, const void* E, int64_t nb, in
 template <bool WO>
 static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb,
                     int64_t N, int64_t D, const DecPlan& p, DecOut o, hipStream_t st) {
-  if (dtype == HVAE_BF16 && p.v2) {
+  if (dtype == HVAE_FP8) {
+    switch (D) {
+      case 128: return launch_fp8<128, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      case 256: return launch_fp8<256, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      case 384: return launch_fp8<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      default: break;
+    }
+  } else if (dtype == HVAE_BF16 && p.v2) {
     if (p.ds == 1) {
       switch (D) {
         case 64: return launch_bf16_v2<64, 1, WO>(U, ldu, E, enorm, nb, N, p, o, st);
@@ -1349,7 +1683,7 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
     }
   }
   HVAE_FAIL(HVAE_ERR_UNSUPPORTED, "hvae_decoder_fwd: no %s kernel for D=%lld",
-            dtype == HVAE_BF16 ? "bf16" : "f32", (long long)D);
+            dtype == HVAE_FP8 ? "fp8" : dtype == HVAE_BF16 ? "bf16" : "f32", (long long)D);
 }
 
 }  // namespace hvae
@@ -1359,6 +1693,7 @@ using namespace hvae;
 extern "C" int hvae_decoder_supported(int dtype, int64_t D) {
   if (dtype == HVAE_BF16) return D == 64 || D == 128 || D == 256 || D == 384 || (D == 768 && !dec_use_v1());
   if (dtype == HVAE_F32) return D == 32 || D == 64 || D == 128 || D == 256 || D == 384;
+  if (dtype == HVAE_FP8) return D == 128 || D == 256 || D == 384;
   return 0;
 }
 
@@ -1375,13 +1710,29 @@ extern "C" int hvae_row_norm_max(int dtype, const void* E, int64_t N, int64_t D,
 
 extern "C" size_t hvae_decoder_image_bytes(int dtype, int64_t N, int64_t D) {
   if (dtype == HVAE_F32) return (size_t)N * D * sizeof(float);
+  if (dtype == HVAE_FP8) return (size_t)f8_tail_offset(N, D) + 256;
   return (size_t)et_offset_bytes(N, D) + (size_t)cdiv(N, kBfTI) * D * kBfTI * sizeof(bf16_t);
 }
 
 extern "C" int hvae_decoder_image(int dtype, const float* E32, int64_t N, int64_t D, void* out, void* stream) {
   HVAE_REQUIRE(E32 && out && N > 0 && D > 0, "hvae_decoder_image: bad args");
-  HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32, "hvae_decoder_image: bad dtype");
+  HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32 || dtype == HVAE_FP8, "hvae_decoder_image: bad dtype");
   hipStream_t st = as_stream(stream);
+  if (dtype == HVAE_FP8) {
+    HVAE_REQUIRE(D % 64 == 0 && N * D * 2 < (1ll << 31), "hvae_decoder_image: fp8 needs D %% 64 == 0, N D < 2^30");
+    const int64_t ntiles = cdiv(N, kF8TI);
+    unsigned* amax = (unsigned*)((char*)out + f8_tail_offset(N, D) + 128);  // scratch word of the tail
+    HVAE_HIP(hipMemsetAsync(amax, 0, sizeof(unsigned), st));
+    k_abs_max<<<(unsigned)std::min<int64_t>(cdiv(N * D, 256), 4096), 256, 0, st>>>(E32, N * D, amax);
+    HVAE_LAUNCH_CHECK("k_abs_max");
+    k_build_image<<<(unsigned)std::min<int64_t>(cdiv(N * D, 256), 8192), 256, 0, st>>>(E32, N, D, (bf16_t*)out,
+                                                                                      nullptr, 0);
+    HVAE_LAUNCH_CHECK("k_build_image");
+    k_build_f8<<<(unsigned)std::min<int64_t>(cdiv(ntiles * 32 * D, 256), 8192), 256, 0, st>>>(
+        E32, N, D, ntiles, amax, (unsigned char*)out + f8_offset_bytes(N, D), (int*)((char*)out + f8_tail_offset(N, D)));
+    HVAE_LAUNCH_CHECK("k_build_f8");
+    return HVAE_OK;
+  }
   if (dtype == HVAE_F32) {
     HVAE_HIP(hipMemcpyAsync(out, E32, (size_t)N * D * sizeof(float), hipMemcpyDeviceToDevice, st));
     return HVAE_OK;
@@ -1405,15 +1756,15 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
                        const float* E32, const hvae_csr_batch* x, int64_t nb, int64_t N, int64_t D, float scale,
                        float* lse, float* O, float* recon_rows, float* dU, const float* kl_rows, float beta,
                        float* loss3, double* accum3, void* ws, size_t ws_bytes, hipStream_t st) {
-  HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32, "hvae decoder: bad dtype");
+  HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32 || dtype == HVAE_FP8, "hvae decoder: bad dtype");
   HVAE_REQUIRE(U && E && lse && N > 0 && D > 0 && ldu >= D, "hvae decoder: bad args");
-  HVAE_REQUIRE(dtype != HVAE_BF16 || e_maxnorm, "hvae decoder: bf16 needs e_maxnorm");
+  HVAE_REQUIRE(dtype == HVAE_F32 || e_maxnorm, "hvae decoder: bf16 / fp8 need e_maxnorm");
   HVAE_REQUIRE(D <= 1024, "hvae decoder: D > 1024 unsupported");
   HVAE_REQUIRE(ldu % 4 == 0 && ((uintptr_t)U % 16) == 0 && ((uintptr_t)E % 16) == 0 &&
                    (!O || ((uintptr_t)O % 16) == 0),
                "hvae decoder: U/E/O must be 16-B aligned with ldu %% 4 == 0");
   HVAE_REQUIRE(N < (1ll << 31), "hvae decoder: N too large");
-  HVAE_REQUIRE(dtype != HVAE_BF16 || N * D * 2 < (1ll << 31), "hvae decoder: bf16 E image over 2 GiB");
+  HVAE_REQUIRE(dtype == HVAE_F32 || N * D * 2 < (1ll << 31), "hvae decoder: bf16 / fp8 E image over 2 GiB");
   HVAE_REQUIRE(!x || (E32 && x->row_ptr && x->nb == nb && x->n_items == N), "hvae decoder: bad CSR batch");
   if (nb == 0) return HVAE_OK;
   DecPlan p = dec_plan(dtype, nb, N, D);
@@ -1422,11 +1773,11 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   if (p.splits > 1 && ws_bytes < dec_ws_bytes(p.splits, nb, D)) {  // fewer splits that fit
     int64_t fit = p.splits;
     while (fit > 1 && ws_bytes < dec_ws_bytes((int)fit, nb, D)) fit = fit * 3 / 4;
-    const int64_t tiles = cdiv(N, dtype == HVAE_BF16 ? kBfTI : kF32TI);
+    const int64_t tiles = cdiv(N, dtype == HVAE_FP8 ? kF8TI : dtype == HVAE_BF16 ? kBfTI : kF32TI);
     dec_set_splits(p, tiles, fit);
     p.blocks = cdiv(nb, p.upb) * p.splits;
   }
-  const bool bf = dtype == HVAE_BF16;
+  const bool bf = dtype != HVAE_F32;  // fixed-offset sweeps (bf16, fp8): flags, bf16 E for the exact fixup
   const bool want_o = O || dU;
   char* w = (char*)ws;
   DecOut o{};

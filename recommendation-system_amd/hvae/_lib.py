@@ -18,6 +18,7 @@ LIB_PATH = Path(os.environ.get("HVAE_LIB", _HERE / "libhvae.so"))
 HVAE_OK = 0
 HVAE_F32 = 0
 HVAE_BF16 = 1
+HVAE_FP8 = 2
 
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU_DROP, EPI_GELU_DROP_BWD, EPI_DROP_BWD, EPI_REPARAM_BWD = range(6)
 

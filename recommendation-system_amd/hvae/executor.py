@@ -256,13 +256,18 @@ class FusedTrainer:
                 raise NotImplementedError(f"no bf16 streaming decoder for embedding dim {d}")
             self.dec_dtype = _lib.HVAE_BF16
             self.E_dec = ops.decoder_image(self.E32)  # bf16 E + its tile-transposed copy
+        elif precision == "fp8":
+            if not ops.decoder_supported(_lib.HVAE_FP8, d):
+                raise NotImplementedError(f"no fp8 streaming decoder for embedding dim {d}")
+            self.dec_dtype = _lib.HVAE_FP8
+            self.E_dec = ops.decoder_image(self.E32, _lib.HVAE_FP8)  # bf16 E + e4m3 fragment tiles
         elif precision == "fp32":
             if not ops.decoder_supported(_lib.HVAE_F32, d):
                 raise NotImplementedError(f"no fp32 streaming decoder for embedding dim {d}")
             self.dec_dtype = _lib.HVAE_F32
             self.E_dec = self.E32
         else:
-            raise ValueError(f"precision must be 'bf16' or 'fp32', got {precision!r}")
+            raise ValueError(f"precision must be 'bf16', 'fp8' or 'fp32', got {precision!r}")
         self.precision = precision
         self.enorm = ops.row_norm_max(self.E_dec)
         self._bufs: dict[tuple, _StepBuffers] = {}

@@ -240,14 +240,17 @@ def reparam_kl_bwd(dz, mu, logvar, eps, kl_scale: float, train: bool, dmu=None, 
 
 # ------------------------------------------------------------------ decoder --
 class DecoderImage:
-    """The frozen embeddings as the bf16 decoder reads them (hvae_decoder_image): bf16 E [N, D] followed by
-    its tile-transposed copy. `bf16` is a view of the first part."""
+    """The frozen embeddings as the bf16 or fp8 decoder reads them (hvae_decoder_image): bf16 E [N, D]
+    followed by its tile-transposed copy (bf16) or by the e4m3 fragment-order tiles and E's scale exponent
+    (fp8). `bf16` is a view of the first part."""
 
-    def __init__(self, E32: torch.Tensor):
+    def __init__(self, E32: torch.Tensor, dtype: int = _lib.HVAE_BF16):
         require_hip(E32)
+        if dtype not in (_lib.HVAE_BF16, _lib.HVAE_FP8):
+            raise ValueError(f"decoder image dtype must be HVAE_BF16 or HVAE_FP8, got {dtype}")
         E32 = E32.contiguous()
         self.N, self.D = E32.shape
-        self.dtype = _lib.HVAE_BF16
+        self.dtype = dtype
         nbytes = int(lib().hvae_decoder_image_bytes(self.dtype, self.N, self.D))
         self.buf = torch.empty(nbytes, dtype=torch.uint8, device=E32.device)
         check(lib().hvae_decoder_image(self.dtype, ptr(E32), self.N, self.D, ptr(self.buf), stream_of(E32)),
@@ -259,14 +262,14 @@ class DecoderImage:
         return self.buf.data_ptr()
 
 
-def decoder_image(E32: torch.Tensor) -> DecoderImage:
-    return DecoderImage(E32)
+def decoder_image(E32: torch.Tensor, dtype: int = _lib.HVAE_BF16) -> DecoderImage:
+    return DecoderImage(E32, dtype)
 
 
 def _dec_operand(E):
     """(dtype code, N, pointer holder) of a decoder E argument: a DecoderImage (bf16) or an fp32 [N, D]."""
     if isinstance(E, DecoderImage):
-        return _lib.HVAE_BF16, E.N, E
+        return E.dtype, E.N, E
     if E.dtype == torch.bfloat16:
         raise TypeError("the bf16 decoder takes a DecoderImage (ops.decoder_image), not a bf16 tensor")
     return _lib.HVAE_F32, E.shape[0], E

@@ -355,7 +355,7 @@ def main() -> None:
     parser.add_argument("--patience", type=int, default=20)
     parser.add_argument("--device", choices=["cuda", "cpu", "mps"])
     parser.add_argument("--ignore-embeddings", action="store_true")
-    parser.add_argument("--precision", choices=["bf16", "fp32"], default=None,
+    parser.add_argument("--precision", choices=["bf16", "fp8", "fp32"], default=None,
                         help="decoder MFMA precision (default: bf16 where a kernel exists)")
     args = parser.parse_args()
     train_hybrid_vae(data_dir=args.data, embeddings_path=args.embeddings, output_dir=args.output,
