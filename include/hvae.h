@@ -248,9 +248,9 @@ int hvae_reparam_kl_bwd(const float* dz, const float* mu, const float* logvar, i
  *              MFMA k order, so that both products of the sweep read LDS tiles
  *              with plain 16-B reads;
  *   HVAE_FP8:  the bf16 E [N, D] as above (score bound, exact fixups), then at a
- *              256-B aligned offset ceil(N/64) tiles of 128 D bytes of e4m3 in
- *              MFMA fragment order (both products' operands), then the int
- *              exponent ke of E's scale (E8 = E 2^ke); D % 64 == 0;
+ *              256-B aligned offset ceil(N/64) tiles of [64][D] e4m3 (16-B chunks
+ *              XOR-swizzled by item row; tail items 0), then the int exponent ke
+ *              of E's scale (E8 = E 2^ke); D in {128, 256, 384, 768};
  *   HVAE_F32:  E itself [N, D].
  * Every `E` argument of the decoder functions below is this image. */
 size_t hvae_decoder_image_bytes(int dtype, int64_t N, int64_t D);

@@ -723,28 +723,45 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
 //     (one exponent per user, from max|u_b|); the MFMA's scale operands undo both, so S^T is fp32 scores
 //     of the quantised operands.
 //   GEMM2 O^T += E_tile^T P^T: P is block floating point, q = p 2^-e with one exponent e per user and
-//     64-item tile (max q in [128, 256]), passed as that user's B scale; p itself never needs a range.
+//     64-item tile (max q in (128, 256]), passed as that user's B scale; p itself never needs a range.
 // Scale semantics (scripts/probe_fp8_mfma.hip on MI355X): element j of lane half h belongs to k-block
 // j >> 4, whose scale lane (row | column) + 32 (j >> 4) supplies; the decoder gives both lanes of a row or
 // column the same exponent, so it depends only on A and B sharing the (h, j) -> k slot map.
-// Tiles of 64 items (GEMM2's K); the image stores both operands in MFMA fragment order (below), so
-// every operand read is a pair of conflict-free 1-KiB ds_read_b128 rows and the LDS-DMA is a plain copy.
-// 4 waves x 32 users per block, each over all D (D <= 384: U 48 + O 192 registers); the softmax of tile
-// t is spread over GEMM1(t+1)'s MFMAs, as in k_dec2_bf16.
+// One row-major e4m3 image per 64-item tile (GEMM2's K), 16-B chunks XOR-swizzled by item (f8_sw): GEMM1
+// reads its A operand by rows (ds_read_b128), GEMM2 by columns with ds_read_b64_tr_b8 (lane 2q + p of a
+// 16-lane group addresses row q, bytes 8p..8p+7; lane i receives column i, row q in byte q:
+// scripts/probe_tr8.hip). Both kinds of read are bank-conflict free for D = 128, 256, 384, 768. The
+// LDS-DMA is a plain copy of the tile.
+// DS = 1 (D <= 384): 4 waves x 32 users, each over all D (U 48 + O 192 registers); the softmax of tile t
+// is spread over GEMM1(t+1)'s MFMAs, as in k_dec2_bf16. DS = 2 (D = 768): waves (ug, dh) = (w & 1, w >> 1)
+// split D in halves; partial S^T tiles are added through LDS; two 48-KiB tile slots, the next tile's
+// LDS-DMA overlapping the whole current tile (GEMM1, exchange, softmax, GEMM2 in sequence).
 typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
 constexpr int kF8TI = 64;  // items per tile
 
 template <int D>
-constexpr int f8_tile_bytes() { return 128 * D; }  // GEMM1 fragments (64 D) + GEMM2 fragments (64 D)
+constexpr int f8_tile_bytes() { return 64 * D; }
 template <int D>
-constexpr int f8_stages() { return (160 * 1024) / f8_tile_bytes<D>() >= 6 ? 6 : (160 * 1024) / f8_tile_bytes<D>(); }
-// fp8 image: bf16 E [N][D] (exact fixups, score bound) | fp8 tiles [ntiles][128 D] | int ke
+constexpr int f8_xbytes() { return D > 384 ? 4 * 8192 : 0; }  // DS = 2: [4 waves][s0, s1][64 lanes][16] floats
+template <int D>
+constexpr int f8_stages() {
+  return D > 384 ? 2 : ((160 * 1024) / f8_tile_bytes<D>() >= 6 ? 6 : (160 * 1024) / f8_tile_bytes<D>());
+}
+// fp8 image: bf16 E [N][D] (exact fixups, score bound) | e4m3 tiles [ntiles][64][D] (swizzled) | int ke
 static inline int64_t f8_offset_bytes(int64_t N, int64_t D) { return et_offset_bytes(N, D); }
 static inline int64_t f8_tail_offset(int64_t N, int64_t D) {
-  return f8_offset_bytes(N, D) + (N + kF8TI - 1) / kF8TI * 128 * D;
+  return f8_offset_bytes(N, D) + (N + kF8TI - 1) / kF8TI * 64 * D;
 }
-// item (within its tile) of element j of lane half h in a GEMM2 fragment: the row order of the two
-// 32x32 S^T accumulators (j < 16: first, j >= 16: second), so P packs from them in place
+// chunk swizzle of item row `it` (only its low 4 bits matter): 3 bits where D / 16 is a multiple of 8,
+// 4 bits where it is a multiple of 16 (rows 768 B / 256 B apart all start in the same bank)
+__host__ __device__ constexpr int f8_sw(int D, int it) {
+  return D % 256 == 0 ? (((it & 1) << 1) | (((it >> 1) & 1) << 2) | (((it >> 3) & 1) << 3) | ((it >> 2) & 1))
+                      : (((it >> 1) & 1) | ((((it >> 1) ^ (it >> 2)) & 1) << 1) | (((it >> 3) & 1) << 2));
+}
+__host__ __device__ constexpr int f8_off(int D, int it, int ch) { return it * D + 16 * (ch ^ f8_sw(D, it)); }
+// item (within its tile) of element j of lane half h of a GEMM2 B operand: the row order of the two 32x32
+// S^T accumulators (j < 16: first, j >= 16: second), so P packs from them in place
 __host__ __device__ constexpr int f8_item_of(int h, int j) {
   return 32 * (j >> 4) + (j & 3) + 8 * ((j & 15) >> 2) + 4 * h;
 }
@@ -753,23 +770,27 @@ __device__ __forceinline__ int pack_fp8x4(float a, float b, float c, float d) {
   return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);
 }
 
-template <int D, bool WITH_O>
+template <int D, int DS, bool WITH_O>
 __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, int64_t ldu,
                                                  const unsigned char* __restrict__ T8, const int* __restrict__ e_exp,
                                                  const float* __restrict__ e_maxnorm, int64_t nb, int64_t N,
                                                  int splits, int64_t tiles_per_split, DecOut out) {
-  constexpr int KS = D / 64;             // GEMM1 k-steps
-  constexpr int DB = D / 32;             // GEMM2 d-blocks
+  constexpr int DW = D / DS;             // dims owned by one wave
+  constexpr int KS = DW / 64;            // GEMM1 k-steps
+  constexpr int DB = DW / 32;            // GEMM2 d-blocks
   constexpr int TB = f8_tile_bytes<D>();
   constexpr int PW = TB / 4096;          // 1-KiB LDS-DMA pieces per wave per tile
   constexpr int NS = f8_stages<D>();
-  static_assert(D % 64 == 0 && D <= 384 && NS >= 3, "fp8 decoder: D in {64, ..., 384}");
+  constexpr int UPB = 128 / DS;          // users per block
+  static_assert(D % 64 == 0 && (DS == 1 ? (D <= 384 && NS >= 3) : (D == 768 && NS == 2)), "fp8 decoder shape");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ug = DS == 1 ? w : (w & 1), dh = DS == 1 ? 0 : (w >> 1);
+  const int dbase = dh * DW;
   const int split = blockIdx.x % splits;
-  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 128 + w * 32;
+  const int64_t u0 = (int64_t)(blockIdx.x / splits) * UPB + ug * 32;
   const int64_t user = u0 + col;
   const bool wave_active = u0 < nb;
   const int64_t ntiles = (N + kF8TI - 1) / kF8TI;
@@ -779,17 +800,15 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   const int ke = *e_exp;
   const int sa = 127 - ke;        // A scale (E8 = E 2^ke)
 
-  // U: lane (col, h) holds u[64 ks + 32 h + j], j < 32, as e4m3 of u 2^ku
+  // U: lane (col, h) holds u[dbase + 64 ks + 32 h + j], j < 32, as e4m3 of u 2^ku (ku from the whole row)
   float amax = 0.f, usq = 0.f;
   if (user < nb) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int q4 = 0; q4 < 8; ++q4) {
-        const float4 a = *reinterpret_cast<const float4*>(U + user * ldu + 64 * ks + 32 * h + 4 * q4);
-        amax = fmaxf(amax, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
-        usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
-      }
+    for (int q4 = 0; q4 < D / 8; ++q4) {  // this lane half's 32-column groups of the whole row
+      const float4 a = *reinterpret_cast<const float4*>(U + user * ldu + 64 * (q4 >> 3) + 32 * h + 4 * (q4 & 7));
+      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+      usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
+    }
   }
   amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
   usq += __shfl_xor(usq, 32, 64);
@@ -804,11 +823,11 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
 #pragma unroll
     for (int q4 = 0; q4 < 8; ++q4) {
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (user < nb) a = *reinterpret_cast<const float4*>(U + user * ldu + 64 * ks + 32 * h + 4 * q4);
+      if (user < nb) a = *reinterpret_cast<const float4*>(U + user * ldu + dbase + 64 * ks + 32 * h + 4 * q4);
       uf[ks][q4] = pack_fp8x4(a.x * qu, a.y * qu, a.z * qu, a.w * qu);
     }
 
-  // LDS-DMA: tile bytes [(w PW + i) KiB, +1 KiB) of the tile into the same place of the ring slot
+  // LDS-DMA: tile bytes [(w PW + i) KiB, +1 KiB) into the same place of the ring slot
   int voff[PW];
 #pragma unroll
   for (int i = 0; i < PW; ++i) voff[i] = (w * PW + i) * 1024 + lane * 16;
@@ -828,144 +847,237 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
                      :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
   };
   auto lds_fence = [] { asm volatile("" ::: "memory"); };
-  // fragment f of a tile slot: 16 B at lane * 16 of its two 1-KiB rows
-  auto frag = [&](const unsigned char* buf, int f) {
-    const uint4 x = *reinterpret_cast<const uint4*>(buf + f * 2048 + lane * 16);
-    const uint4 y = *reinterpret_cast<const uint4*>(buf + f * 2048 + 1024 + lane * 16);
+  auto barrier = [&] {
+    lds_fence();
+    __builtin_amdgcn_s_barrier();
+    lds_fence();
+  };
+
+  // GEMM1 A operand (ks, half): item row 32 half + col, chunks 4 (ks0 + ks) + 2 h + {0, 1}
+  const int swc = f8_sw(D, col);
+  auto rdA = [&](const unsigned char* buf, int ks, int half) {
+    const int ch = 4 * (dbase / 64 + ks) + 2 * h;
+    const unsigned char* row = buf + (32 * half + col) * D;
+    const uint4 x = *reinterpret_cast<const uint4*>(row + 16 * (ch ^ swc));
+    const uint4 y = *reinterpret_cast<const uint4*>(row + 16 * ((ch + 1) ^ swc));
     i32x8 r;
     r[0] = (int)x.x; r[1] = (int)x.y; r[2] = (int)x.z; r[3] = (int)x.w;
     r[4] = (int)y.x; r[5] = (int)y.y; r[6] = (int)y.z; r[7] = (int)y.w;
     return r;
   };
-  // GEMM1: S^T of items 0-31 (s0) and 32-63 (s1) of the tile; fragments 2 ks + half
+  // GEMM2 A operand (d-block db): four transposed reads, read c = items f8_item_of(h, 8 c + q) (q = 0..7)
+  const int g1 = (lane >> 4) & 1, qq = (lane & 15) >> 1, pp = lane & 1;
+  int trow[4], tsw[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int it = f8_item_of(h, 8 * c + qq);
+    trow[c] = it * D + 8 * pp;
+    tsw[c] = f8_sw(D, it);
+  }
+  auto rdB = [&](const unsigned char* buf, int db) {
+    const int ch = 2 * (dbase / 32 + db) + g1;
+    i32x8 r;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      auto* p = (__attribute__((address_space(3))) i32x2*)(void*)(buf + trow[c] + 16 * (ch ^ tsw[c]));
+      const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(p);
+      r[2 * c] = v[0];
+      r[2 * c + 1] = v[1];
+    }
+    return r;
+  };
+  // GEMM1 (this wave's dims): S^T of items 0-31 (s0) and 32-63 (s1) of the tile
   auto gemm1 = [&](const unsigned char* buf, f32x16& s0, f32x16& s1, auto&& fill) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
-    i32x8 a0 = frag(buf, 0), a1 = frag(buf, 1);
+    i32x8 a0 = rdA(buf, 0, 0), a1 = rdA(buf, 0, 1);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
       const i32x8 c0 = a0, c1 = a1;
-      if (ks + 1 < KS) { a0 = frag(buf, 2 * ks + 2); a1 = frag(buf, 2 * ks + 3); }
+      if (ks + 1 < KS) { a0 = rdA(buf, ks + 1, 0); a1 = rdA(buf, ks + 1, 1); }
       s0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c0, uf[ks], s0, 0, 0, 0, sa, 0, sbu);
       s1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c1, uf[ks], s1, 0, 0, 0, sa, 0, sbu);
       fill(ks);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-
   f32x16 o[WITH_O ? DB : 1];
 #pragma unroll
   for (int d = 0; d < (WITH_O ? DB : 1); ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  auto gemm2 = [&](const unsigned char* buf, const i32x8& pf, int sbp) {
+    if constexpr (WITH_O) {
+      i32x8 a = rdB(buf, 0);
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        const i32x8 c = a;
+        if (db + 1 < DB) a = rdB(buf, db + 1);
+        o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
+      }
+    }
+  };
+
   float m = 0.f, mL = 0.f, lsum = 0.f;
-  f32x16 c0, c1;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) { c0[r] = 0.f; c1[r] = 0.f; }
-
-  constexpr int PRE = NS - 1;  // tiles in flight before the loop
-  if (t_beg < t_end) {
-#pragma unroll
-    for (int i = 0; i < PRE; ++i) issue(min(t_beg + i, t_end - 1), i);
-    wait_vmcnt<(PRE - 1) * PW>();
-  }
-  lds_fence();
-  __builtin_amdgcn_s_barrier();
-  lds_fence();
-  if (t_beg < t_end && wave_active) gemm1(lds, c0, c1, [](int) {});
   const float bound = sqrtf(usq) * emax * 1.02f;
+  // per tile: mask items past N (read as 0), the fixed per-split offset on the first tile, the tile's
+  // P exponent e (q = exp2(s log2e - mL - e) <= 2^8); returns e
+  auto tile_prep = [&](int64_t t, f32x16& c0, f32x16& c1) {
+    if (t == ntiles - 1 && (N % kF8TI) != 0) {
+      const int lim = (int)(N - t * kF8TI) - 4 * h;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int it = (r & 3) + 8 * (r >> 2);
+        c0[r] = it >= lim ? -INFINITY : c0[r];
+        c1[r] = it + 32 >= lim ? -INFINITY : c1[r];
+      }
+    }
+    float mx = fmaxf(c0[0], c1[0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(c0[r], c1[r]));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    if (t == t_beg) {  // as k_dec2_bf16: p = exp(s - m) <= e^60, never rescaled; flagged if l ends tiny
+      m = fmaxf(mx, bound - kOffsetSpan);
+      mL = m * kLog2e;
+    }
+    return max(-119, min(127, (int)ceilf(__builtin_fmaf(mx, kLog2e, -mL)) - 8));
+  };
 
-  int cur = 0;
-  for (int64_t t = t_beg; t < t_end; ++t) {
-    wait_vmcnt<(NS - 3) * PW>();  // tile t + 1 has landed
-    lds_fence();
-    __builtin_amdgcn_s_barrier();
-    lds_fence();
-    const int nxt = cur == NS - 1 ? 0 : cur + 1;
-    // tile t + NS - 1 into the slot of tile t - 1 (every wave finished its GEMM2 before the barrier)
-    issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
-    if (wave_active) {
-      if (t == ntiles - 1 && (N % kF8TI) != 0) {  // items past N (read as 0) leave the softmax
-        const int lim = (int)(N - t * kF8TI) - 4 * h;
+  if constexpr (DS == 1) {
+    f32x16 c0, c1;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int it = (r & 3) + 8 * (r >> 2);
-          c0[r] = it >= lim ? -INFINITY : c0[r];
-          c1[r] = it + 32 >= lim ? -INFINITY : c1[r];
-        }
-      }
-      float mx = fmaxf(c0[0], c1[0]);
+    for (int r = 0; r < 16; ++r) { c0[r] = 0.f; c1[r] = 0.f; }
+    constexpr int PRE = NS - 1;  // tiles in flight before the loop
+    if (t_beg < t_end) {
 #pragma unroll
-      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(c0[r], c1[r]));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      if (t == t_beg) {  // fixed per-split offset, as k_dec2_bf16
-        m = fmaxf(mx, bound - kOffsetSpan);
-        mL = m * kLog2e;
-      }
-      // P block exponent of this (user, tile): q = exp2(s log2e - mL - e) <= 2^8
-      const int e = max(-119, min(127, (int)ceilf(__builtin_fmaf(mx, kLog2e, -mL)) - 8));
-      const float cE = mL + (float)e;
-      float qv[32];
-      int pk[8];
-      float qsum = 0.f;
-      auto smax = [&](int j0, int j1) {
+      for (int i = 0; i < PRE; ++i) issue(min(t_beg + i, t_end - 1), i);
+      wait_vmcnt<(PRE - 1) * PW>();
+    }
+    barrier();
+    if (t_beg < t_end && wave_active) gemm1(lds, c0, c1, [](int) {});
+    int cur = 0;
+    for (int64_t t = t_beg; t < t_end; ++t) {
+      wait_vmcnt<(NS - 3) * PW>();  // tile t + 1 has landed
+      barrier();
+      const int nxt = cur == NS - 1 ? 0 : cur + 1;
+      // tile t + NS - 1 into the slot of tile t - 1 (every wave finished its GEMM2 before the barrier)
+      issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
+      if (wave_active) {
+        const int e = tile_prep(t, c0, c1);
+        const float cE = mL + (float)e;
+        float qv[32];
+        int pk[8];
+        float qsum = 0.f;
+        auto smax = [&](int j0, int j1) {
 #pragma unroll
-        for (int j = j0; j < j1; ++j) {
-          const float s = j < 16 ? c0[j & 15] : c1[j & 15];
-          qv[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s, kLog2e, -cE));
-          qsum += qv[j];
-          if ((j & 3) == 3) pk[j >> 2] = pack_fp8x4(qv[j - 3], qv[j - 2], qv[j - 1], qv[j]);
-        }
-      };
-      f32x16 n0, n1;
-      gemm1(lds + nxt * TB, n0, n1, [&](int g) { smax(32 * g / KS / 4 * 4, 32 * (g + 1) / KS / 4 * 4); });
-      lsum += ldexpf(qsum, e);
-      if constexpr (WITH_O) {
+          for (int j = j0; j < j1; ++j) {
+            const float s = j < 16 ? c0[j & 15] : c1[j & 15];
+            qv[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s, kLog2e, -cE));
+            qsum += qv[j];
+            if ((j & 3) == 3) pk[j >> 2] = pack_fp8x4(qv[j - 3], qv[j - 2], qv[j - 1], qv[j]);
+          }
+        };
+        f32x16 n0, n1;
+        gemm1(lds + nxt * TB, n0, n1, [&](int g) { smax(32 * g / KS / 4 * 4, 32 * (g + 1) / KS / 4 * 4); });
+        lsum += ldexpf(qsum, e);
         i32x8 pf;
 #pragma unroll
         for (int i = 0; i < 8; ++i) pf[i] = pk[i];
-        const int sbp = 127 + e;
-        const unsigned char* buf = lds + cur * TB + 64 * D;
-        i32x8 a = frag(buf, 0);
-#pragma unroll
-        for (int db = 0; db < DB; ++db) {
-          const i32x8 c = a;
-          if (db + 1 < DB) a = frag(buf, db + 1);
-          o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
-        }
+        gemm2(lds + cur * TB, pf, 127 + e);
+        c0 = n0;
+        c1 = n1;
       }
-      c0 = n0;
-      c1 = n1;
+      cur = nxt;
     }
-    cur = nxt;
+  } else {
+    // DS = 2: two slots; tile t + 1's LDS-DMA runs under all of tile t
+    float* xbuf = reinterpret_cast<float*>(lds + NS * TB);  // [4 w][2 s][64 lane][16]
+    auto xput = [&](const f32x16& s0, const f32x16& s1) {
+      float* xb = xbuf + w * 2048;
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        *reinterpret_cast<float4*>(xb + r4 * 256 + lane * 4) = make_float4(s0[4 * r4], s0[4 * r4 + 1], s0[4 * r4 + 2],
+                                                                           s0[4 * r4 + 3]);
+        *reinterpret_cast<float4*>(xb + 1024 + r4 * 256 + lane * 4) =
+            make_float4(s1[4 * r4], s1[4 * r4 + 1], s1[4 * r4 + 2], s1[4 * r4 + 3]);
+      }
+    };
+    auto xadd = [&](f32x16& s0, f32x16& s1) {
+      const float* xb = xbuf + (w ^ 2) * 2048;
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const float4 v = *reinterpret_cast<const float4*>(xb + r4 * 256 + lane * 4);
+        const float4 u = *reinterpret_cast<const float4*>(xb + 1024 + r4 * 256 + lane * 4);
+        s0[4 * r4] += v.x; s0[4 * r4 + 1] += v.y; s0[4 * r4 + 2] += v.z; s0[4 * r4 + 3] += v.w;
+        s1[4 * r4] += u.x; s1[4 * r4 + 1] += u.y; s1[4 * r4 + 2] += u.z; s1[4 * r4 + 3] += u.w;
+      }
+    };
+    if (t_beg < t_end) {
+      issue(t_beg, 0);
+      issue(min(t_beg + 1, t_end - 1), 1);
+    }
+    int cur = 0;
+    for (int64_t t = t_beg; t < t_end; ++t) {
+      wait_vmcnt<PW>();  // tile t has landed (t + 1 may be in flight)
+      barrier();
+      f32x16 c0, c1;
+      if (wave_active) {
+        gemm1(lds + cur * TB, c0, c1, [](int) {});
+        xput(c0, c1);
+      }
+      barrier();
+      if (wave_active) {
+        xadd(c0, c1);
+        const int e = tile_prep(t, c0, c1);
+        const float cE = mL + (float)e;
+        i32x8 pf;
+        float qsum = 0.f;
+#pragma unroll
+        for (int j4 = 0; j4 < 8; ++j4) {
+          float q[4];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int j = 4 * j4 + b;
+            q[b] = __builtin_amdgcn_exp2f(__builtin_fmaf(j < 16 ? c0[j & 15] : c1[j & 15], kLog2e, -cE));
+            qsum += q[b];
+          }
+          pf[j4] = pack_fp8x4(q[0], q[1], q[2], q[3]);
+        }
+        lsum += ldexpf(qsum, e);
+        gemm2(lds + cur * TB, pf, 127 + e);
+      }
+      barrier();  // slot cur and the exchange buffer are free
+      issue(min(t + 2, t_end - 1), cur);
+      cur ^= 1;
+    }
   }
 
   if (!wave_active) return;
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);
   if (user >= nb) return;
-  if (h == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
+  if (h == 0 && dh == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
   if (out.direct) {
     const float inv = 1.0f / ltot;
-    if (h == 0) out.lse[user] = m + logf(ltot);
+    if (h == 0 && dh == 0) out.lse[user] = m + logf(ltot);
     if (WITH_O) {
 #pragma unroll
       for (int d = 0; d < (WITH_O ? DB : 1); ++d)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const int dd = 32 * d + 8 * g4 + 4 * h;
+          const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
           *reinterpret_cast<float4*>(out.O + user * D + dd) =
               make_float4(o[d][4 * g4] * inv, o[d][4 * g4 + 1] * inv, o[d][4 * g4 + 2] * inv, o[d][4 * g4 + 3] * inv);
         }
     }
   } else {
     const int64_t pi = (int64_t)split * nb + user;
-    if (h == 0) { out.m[pi] = m; out.l[pi] = ltot; }
+    if (h == 0 && dh == 0) { out.m[pi] = m; out.l[pi] = ltot; }
     if (WITH_O) {
 #pragma unroll
       for (int d = 0; d < (WITH_O ? DB : 1); ++d)
 #pragma unroll
         for (int g4 = 0; g4 < 4; ++g4) {
-          const int dd = 32 * d + 8 * g4 + 4 * h;
+          const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
           *reinterpret_cast<float4*>(out.O + pi * D + dd) =
               make_float4(o[d][4 * g4], o[d][4 * g4 + 1], o[d][4 * g4 + 2], o[d][4 * g4 + 3]);
         }
@@ -1410,9 +1522,8 @@ __global__ void __launch_bounds__(256) k_build_image(const float* __restrict__ E
   }
 }
 
-// fp8 tiles of the fp8 image: per 64-item tile, GEMM1 fragments f = 2 ks + half (lane l: item 32 half + (l & 31),
-// d = 64 ks + 32 (l >> 5) + j) then GEMM2 fragments db (lane l: d = 32 db + (l & 31), item f8_item_of(l >> 5, j)),
-// each fragment [2 parts][64 lanes][16 B] with element j = 16 part + byte. E8 = e4m3(E 2^ke), ke from max |E|.
+// e4m3 tiles of the fp8 image: per 64-item tile, rows of D bytes with 16-B chunks swizzled by f8_off;
+// E8 = e4m3(E 2^ke), ke from max |E|; items past N are 0. One thread per 4 bytes (4 consecutive d).
 __global__ void __launch_bounds__(256) k_build_f8(const float* __restrict__ E32, int64_t N, int64_t D, int64_t ntiles,
                                                   const unsigned* __restrict__ amax_bits, unsigned char* __restrict__ T8,
                                                   int* __restrict__ ke_out) {
@@ -1422,24 +1533,17 @@ __global__ void __launch_bounds__(256) k_build_f8(const float* __restrict__ E32,
   const int ke = amax > 0.f ? min(127, 8 - ea) : 0;  // max |E 2^ke| <= 256
   if (blockIdx.x == 0 && threadIdx.x == 0) *ke_out = ke;
   const float qs = ldexpf(1.f, ke);
-  const int64_t TB = 128 * D, words = ntiles * TB / 4;
+  const int64_t words = ntiles * kF8TI * D / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride) {
-    const int64_t t = (i * 4) / TB;
-    const int r0 = (int)((i * 4) % TB);
-    float v[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int rr = r0 + k;
-      const int g = rr < 64 * D ? rr : rr - 64 * (int)D;
-      const int f = g >> 11, part = (g >> 10) & 1, ln = (g >> 4) & 63, j = 16 * part + (g & 15);
-      int64_t item;
-      int64_t d;
-      if (rr < 64 * D) { item = t * kF8TI + 32 * (f & 1) + (ln & 31); d = 64 * (f >> 1) + 32 * (ln >> 5) + j; }
-      else { item = t * kF8TI + f8_item_of(ln >> 5, j); d = 32 * f + (ln & 31); }
-      v[k] = item < N ? E32[item * D + d] * qs : 0.f;
-    }
-    reinterpret_cast<int*>(T8)[i] = pack_fp8x4(v[0], v[1], v[2], v[3]);
+    const int64_t item = (i * 4) / D;  // global item; d = 4 consecutive columns
+    const int d = (int)((i * 4) % D);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (item < N) v = *reinterpret_cast<const float4*>(E32 + item * D + d);
+    const int64_t t = item / kF8TI;
+    const int it = (int)(item % kF8TI);
+    unsigned char* dst = T8 + t * kF8TI * D + f8_off((int)D, it, d >> 4) + (d & 15);
+    *reinterpret_cast<int*>(dst) = pack_fp8x4(v.x * qs, v.y * qs, v.z * qs, v.w * qs);
   }
 }
 
@@ -1515,8 +1619,9 @@ static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
 
 static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   DecPlan p{};
-  if (dtype == HVAE_FP8) {  // k_dec_fp8: 128 users per block, 64-item tiles
-    p.upb = 128;
+  if (dtype == HVAE_FP8) {  // k_dec_fp8: 128 users per block (64 with the D split), 64-item tiles
+    p.ds = D > 384 ? 2 : 1;
+    p.upb = 128 / p.ds;
     const int64_t nub = cdiv(nb, p.upb), tiles = cdiv(N, kF8TI);
     int64_t s = cdiv(256, nub);
     s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 2));
@@ -1607,15 +1712,17 @@ static int launch_bf16_v2(const float* U, int64_t ldu, const void* E, const floa
 template <int D, bool WO>
 static int launch_fp8(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                       const DecPlan& p, DecOut o, hipStream_t st) {
-  constexpr int lds = f8_stages<D>() * f8_tile_bytes<D>();
+  constexpr int DS = D > 384 ? 2 : 1;
+  constexpr int lds = f8_stages<D>() * f8_tile_bytes<D>() + f8_xbytes<D>();
   static bool attr_set = false;
   if (!attr_set) {
-    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec_fp8<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec_fp8<D, DS, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = true;
   }
   const unsigned char* T8 = (const unsigned char*)E + f8_offset_bytes(N, D);
   const int* ke = (const int*)((const char*)E + f8_tail_offset(N, D));
-  k_dec_fp8<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, T8, ke, enorm, nb, N, p.splits, p.tiles_per_split, o);
+  k_dec_fp8<D, DS, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, T8, ke, enorm, nb, N, p.splits, p.tiles_per_split,
+                                                            o);
   HVAE_LAUNCH_CHECK("k_dec_fp8");
   return HVAE_OK;
 }
@@ -1643,6 +1750,7 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
       case 128: return launch_fp8<128, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 256: return launch_fp8<256, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 384: return launch_fp8<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      case 768: return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       default: break;
     }
   } else if (dtype == HVAE_BF16 && p.v2) {
@@ -1693,7 +1801,7 @@ using namespace hvae;
 extern "C" int hvae_decoder_supported(int dtype, int64_t D) {
   if (dtype == HVAE_BF16) return D == 64 || D == 128 || D == 256 || D == 384 || (D == 768 && !dec_use_v1());
   if (dtype == HVAE_F32) return D == 32 || D == 64 || D == 128 || D == 256 || D == 384;
-  if (dtype == HVAE_FP8) return D == 128 || D == 256 || D == 384;
+  if (dtype == HVAE_FP8) return D == 128 || D == 256 || D == 384 || D == 768;
   return 0;
 }
 
@@ -1719,7 +1827,8 @@ extern "C" int hvae_decoder_image(int dtype, const float* E32, int64_t N, int64_
   HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32 || dtype == HVAE_FP8, "hvae_decoder_image: bad dtype");
   hipStream_t st = as_stream(stream);
   if (dtype == HVAE_FP8) {
-    HVAE_REQUIRE(D % 64 == 0 && N * D * 2 < (1ll << 31), "hvae_decoder_image: fp8 needs D %% 64 == 0, N D < 2^30");
+    HVAE_REQUIRE((D == 128 || D == 256 || D == 384 || D == 768) && N * D * 2 < (1ll << 31),
+                 "hvae_decoder_image: fp8 needs D in {128, 256, 384, 768} and N D < 2^30");
     const int64_t ntiles = cdiv(N, kF8TI);
     unsigned* amax = (unsigned*)((char*)out + f8_tail_offset(N, D) + 128);  // scratch word of the tail
     HVAE_HIP(hipMemsetAsync(amax, 0, sizeof(unsigned), st));
@@ -1728,7 +1837,7 @@ extern "C" int hvae_decoder_image(int dtype, const float* E32, int64_t N, int64_
     k_build_image<<<(unsigned)std::min<int64_t>(cdiv(N * D, 256), 8192), 256, 0, st>>>(E32, N, D, (bf16_t*)out,
                                                                                       nullptr, 0);
     HVAE_LAUNCH_CHECK("k_build_image");
-    k_build_f8<<<(unsigned)std::min<int64_t>(cdiv(ntiles * 32 * D, 256), 8192), 256, 0, st>>>(
+    k_build_f8<<<(unsigned)std::min<int64_t>(cdiv(ntiles * 16 * D, 256), 8192), 256, 0, st>>>(
         E32, N, D, ntiles, amax, (unsigned char*)out + f8_offset_bytes(N, D), (int*)((char*)out + f8_tail_offset(N, D)));
     HVAE_LAUNCH_CHECK("k_build_f8");
     return HVAE_OK;

@@ -62,44 +62,40 @@ def _image(ops, E):
     return ops.decoder_image(E, _lib.HVAE_FP8)
 
 
-def test_fp8_image_layout(ops, hip_device):
-    """bf16 part == bf16(E); e4m3 tiles in fragment order == torch's e4m3 of E 2^ke; ke at the tail."""
-    N, D = 150, 128
+def _sw(D, it):
+    """hvae_decoder.hip f8_sw: XOR swizzle of the 16-B chunks of item row `it` of a tile."""
+    if D % 256 == 0:
+        return ((it & 1) << 1) | (((it >> 1) & 1) << 2) | (((it >> 3) & 1) << 3) | ((it >> 2) & 1)
+    return ((it >> 1) & 1) | ((((it >> 1) ^ (it >> 2)) & 1) << 1) | (((it >> 3) & 1) << 2)
+
+
+@pytest.mark.parametrize("N,D", [(150, 128), (70, 768), (65, 384)])
+def test_fp8_image_layout(ops, hip_device, N, D):
+    """bf16 part == bf16(E); e4m3 tiles [64][D] with swizzled chunks == torch's e4m3 of E 2^ke; ke at the tail."""
     E = torch.as_tensor(synth_embeddings(N, D, seed=4)) * 3.0
     img = _image(ops, E.to(hip_device))
     assert torch.equal(img.bf16.cpu(), E.bfloat16())
     off = (N * D * 2 + 255) // 256 * 256
     nt = (N + 63) // 64
     raw = img.buf.cpu()
-    tail = off + nt * 128 * D
+    tail = off + nt * 64 * D
     ke = int(raw[tail: tail + 4].view(torch.int32)[0])
     assert ke == int(_pow2_exp(E.abs().max()))
-    E8 = (E * 2.0 ** ke).to(torch.float8_e4m3fn)
-    tiles = raw[off: tail].view(nt, 128 * D)
-    zero = torch.zeros((), dtype=torch.float8_e4m3fn)
-    for t in range(nt):
-        b = tiles[t].view(torch.float8_e4m3fn)
-        for f in range(2 * (D // 64)):          # GEMM1 fragments
-            frag = b[f * 2048:(f + 1) * 2048].view(2, 64, 16)
-            for ln in (0, 5, 31, 32, 63):
-                for j in (0, 7, 16, 31):
-                    item = 64 * t + 32 * (f & 1) + (ln & 31)
-                    d = 64 * (f >> 1) + 32 * (ln >> 5) + j
-                    want = E8[item, d] if item < N else zero
-                    assert frag[j >> 4, ln, j & 15].view(torch.uint8) == want.view(torch.uint8), (t, f, ln, j)
-        for db in range(D // 32):               # GEMM2 fragments
-            frag = b[64 * D + db * 2048: 64 * D + (db + 1) * 2048].view(2, 64, 16)
-            for ln in (0, 9, 31, 32, 63):
-                h = ln >> 5
-                for j in range(32):
-                    it = 32 * (j >> 4) + (j & 3) + 8 * ((j & 15) >> 2) + 4 * h
-                    item = 64 * t + it
-                    want = E8[item, 32 * db + (ln & 31)] if item < N else zero
-                    assert frag[j >> 4, ln, j & 15].view(torch.uint8) == want.view(torch.uint8), (t, db, ln, j)
+    E8 = torch.zeros(nt * 64, D, dtype=torch.float8_e4m3fn)
+    E8[:N] = (E * 2.0 ** ke).to(torch.float8_e4m3fn)
+    want = torch.empty(nt * 64 * D, dtype=torch.uint8)
+    E8u = E8.view(torch.uint8)
+    for item in range(nt * 64):
+        t, it = divmod(item, 64)
+        for ch in range(D // 16):
+            o = t * 64 * D + it * D + 16 * (ch ^ _sw(D, it))
+            want[o: o + 16] = E8u[item, 16 * ch: 16 * ch + 16]
+    assert torch.equal(raw[off: tail], want)
 
 
 @pytest.mark.parametrize("nb,N,D", [(3, 50, 384), (64, 890, 384), (200, 12101, 384), (130, 1000, 128),
-                                    (300, 5000, 256), (520, 20011, 384)])
+                                    (300, 5000, 256), (520, 20011, 384), (64, 2000, 768), (300, 5001, 768),
+                                    (7, 100, 768)])
 def test_decoder_fp8(ops, hip_device, nb, N, D):
     E = torch.as_tensor(synth_embeddings(N, D, seed=N))
     g = torch.Generator().manual_seed(nb)
@@ -135,7 +131,8 @@ def test_decoder_fp8_large_norm_fixup(ops, hip_device):
     assert ((lse.double().cpu() - ref).abs() / ref.abs().clamp(min=1)).max() < 2e-2
 
 
-@pytest.mark.parametrize("nb,N,D", [(40, 700, 384), (64, 12101, 384), (5, 3000, 128), (300, 9000, 256)])
+@pytest.mark.parametrize("nb,N,D", [(40, 700, 384), (64, 12101, 384), (5, 3000, 128), (300, 9000, 256),
+                                    (130, 4000, 768)])
 def test_decoder_train_fused_fp8(ops, hip_device, nb, N, D):
     """Fused sweep + finalize == decoder_fwd + decoder_bwd (bitwise), and == autograd on the quantised scores."""
     X = synth_csr(nb, N, lam=5.0, seed=nb + N)
