@@ -800,15 +800,15 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   const int ke = *e_exp;
   const int sa = 127 - ke;        // A scale (E8 = E 2^ke)
 
-  // U: lane (col, h) holds u[dbase + 64 ks + 32 h + j], j < 32, as e4m3 of u 2^ku (ku from the whole row)
+  // U: lane (col, h) holds u[dbase + 64 ks + 32 h + j], j < 32, as e4m3 of u 2^ku (ku from the whole row).
+  // Lanes past nb read the last user's row (no per-load branches); their columns are never stored.
+  const float* urow = U + min(user, nb - 1) * ldu + 32 * h;
   float amax = 0.f, usq = 0.f;
-  if (user < nb) {
-#pragma unroll
-    for (int q4 = 0; q4 < D / 8; ++q4) {  // this lane half's 32-column groups of the whole row
-      const float4 a = *reinterpret_cast<const float4*>(U + user * ldu + 64 * (q4 >> 3) + 32 * h + 4 * (q4 & 7));
-      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
-      usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
-    }
+#pragma unroll 8
+  for (int q4 = 0; q4 < D / 8; ++q4) {  // this lane half's 32-column groups of the whole row
+    const float4 a = *reinterpret_cast<const float4*>(urow + 64 * (q4 >> 3) + 4 * (q4 & 7));
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+    usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
   }
   amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
   usq += __shfl_xor(usq, 32, 64);
@@ -819,18 +819,18 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   const float qu = ldexpf(1.f, ku);
   i32x8 uf[KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
+  for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
     for (int q4 = 0; q4 < 8; ++q4) {
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (user < nb) a = *reinterpret_cast<const float4*>(U + user * ldu + dbase + 64 * ks + 32 * h + 4 * q4);
+      const float4 a = *reinterpret_cast<const float4*>(urow + dbase + 64 * ks + 4 * q4);
       uf[ks][q4] = pack_fp8x4(a.x * qu, a.y * qu, a.z * qu, a.w * qu);
     }
+    __builtin_amdgcn_sched_barrier(0);  // one k-step's loads in flight at a time (registers)
+  }
 
   // LDS-DMA: tile bytes [(w PW + i) KiB, +1 KiB) into the same place of the ring slot
-  int voff[PW];
-#pragma unroll
-  for (int i = 0; i < PW; ++i) voff[i] = (w * PW + i) * 1024 + lane * 16;
+  // (one VGPR: the piece index moves the scalar soffset and M0, not the lane offset)
+  const int voff = w * PW * 1024 + lane * 16;
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned char*>(T8), (short)0, (int)(ntiles * TB), 0x00020000);
   const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
@@ -841,10 +841,11 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
     for (int i = 0; i < PW; ++i)
       if (i == 0)  // soff may be fresh from v_readfirstlane: 5 wait states before a buffer op reads it
         asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
+                     :: "s"(lb), "v"(voff), "s"(rsrc), "s"(soff) : "memory");
       else
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff[i]), "s"(rsrc), "s"(soff) : "memory");
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff), "s"(rsrc), "s"(soff + (uint32_t)(i * 1024))
+                     : "memory");
   };
   auto lds_fence = [] { asm volatile("" ::: "memory"); };
   auto barrier = [&] {
