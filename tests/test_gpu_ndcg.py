@@ -27,7 +27,9 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.timeout(900)
-def test_ndcg_parity_planted(hip_device, tmp_path):
+@pytest.mark.parametrize("precision", [None, "fp8"])
+def test_ndcg_parity_planted(hip_device, tmp_path, precision):
+    """precision None = the default bf16 decoder; "fp8" = the block-scaled e4m3 sweep (BASELINE configs[4])."""
     from src.ml.evaluate import evaluate_recommendation_model
     from src.ml.train import train_hybrid_vae
     fix = json.loads((HERE / "golden" / "ndcg_planted.json").read_text())
@@ -44,12 +46,12 @@ def test_ndcg_parity_planted(hip_device, tmp_path):
         np.random.seed(s)
         train_hybrid_vae(str(data), str(emb), str(out), latent_dim=c["latent"], hidden_dims=c["hidden"],
                          batch_size=c["batch"], epochs=c["epochs"], learning_rate=c["lr"], beta=c["beta"],
-                         dropout=c["dropout"], device="cuda", patience=20)
+                         dropout=c["dropout"], device="cuda", patience=20, precision=precision)
         np.random.seed(c["neg_seed"])
         res = evaluate_recommendation_model(str(out / "best_model.pth"), str(data), str(emb), k_values=[5, 10, 20],
                                             device="cuda", n_negatives=99)
         got.append(res[10]["ndcg"])
-        print(f"seed {s}: NDCG@10 {res[10]['ndcg']:.4f} HR@10 {res[10]['hit_ratio']:.4f}", flush=True)
+        print(f"[{precision or 'bf16'}] seed {s}: NDCG@10 {res[10]['ndcg']:.4f} HR@10 {res[10]['hit_ratio']:.4f}", flush=True)
     mean = float(np.mean(got))
-    print(f"NDCG@10 mean {mean:.4f} vs reference {fix['ndcg10_mean']:.4f} +- {fix['ndcg10_std']:.4f}")
+    print(f"[{precision or 'bf16'}] NDCG@10 mean {mean:.4f} vs reference {fix['ndcg10_mean']:.4f} +- {fix['ndcg10_std']:.4f}")
     assert abs(mean - fix["ndcg10_mean"]) < 0.004
