@@ -855,18 +855,13 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   };
 
   // GEMM1 A operand (ks, half): item row 32 half + col, chunks 4 (ks0 + ks) + 2 h + {0, 1}
-  const int swc = f8_sw(D, col);
-  auto rdA = [&](const unsigned char* buf, int ks, int half) {
-    const int ch = 4 * (dbase / 64 + ks) + 2 * h;
-    const unsigned char* row = buf + (32 * half + col) * D;
-    const uint4 x = *reinterpret_cast<const uint4*>(row + 16 * (ch ^ swc));
-    const uint4 y = *reinterpret_cast<const uint4*>(row + 16 * ((ch + 1) ^ swc));
-    i32x8 r;
-    r[0] = (int)x.x; r[1] = (int)x.y; r[2] = (int)x.z; r[3] = (int)x.w;
-    r[4] = (int)y.x; r[5] = (int)y.y; r[6] = (int)y.z; r[7] = (int)y.w;
-    return r;
-  };
   // GEMM2 A operand (d-block db): four transposed reads, read c = items f8_item_of(h, 8 c + q) (q = 0..7)
+  // The swizzle only permutes chunks within periods of PC chunks, so DS = 1 keeps each lane's in-period
+  // offsets in registers (8 + 16, or 16 + 32 for PC = 16) and every read is base + offset + immediate;
+  // the D split (register-bound) recomputes them per read.
+  constexpr int PC = D % 256 == 0 ? 16 : 8;  // swizzle period in chunks
+  constexpr int NA = PC / 4, NB = PC / 2;
+  const int swc = f8_sw(D, col);
   const int g1 = (lane >> 4) & 1, qq = (lane & 15) >> 1, pp = lane & 1;
   int trow[4], tsw[4];
 #pragma unroll
@@ -875,13 +870,49 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
     trow[c] = it * D + 8 * pp;
     tsw[c] = f8_sw(D, it);
   }
+  int offA[DS == 1 ? 2 : 1][DS == 1 ? NA : 1][2], offB[4][DS == 1 ? NB : 1];
+  if constexpr (DS == 1) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf)
+#pragma unroll
+      for (int k = 0; k < NA; ++k)
+#pragma unroll
+        for (int part = 0; part < 2; ++part)
+          offA[hf][k][part] = (32 * hf + col) * D + 16 * ((4 * k + 2 * h + part) ^ swc);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < NB; ++k) offB[c][k] = trow[c] + 16 * ((2 * k + g1) ^ tsw[c]);
+  }
+  auto rdA = [&](const unsigned char* buf, int ks, int half) {
+    uint4 x, y;
+    if constexpr (DS == 1) {
+      const unsigned char* b = buf + 16 * PC * (ks / NA);
+      x = *reinterpret_cast<const uint4*>(b + offA[half][ks % NA][0]);
+      y = *reinterpret_cast<const uint4*>(b + offA[half][ks % NA][1]);
+    } else {
+      const int ch = 4 * (dbase / 64 + ks) + 2 * h;
+      const unsigned char* row = buf + (32 * half + col) * D;
+      x = *reinterpret_cast<const uint4*>(row + 16 * (ch ^ swc));
+      y = *reinterpret_cast<const uint4*>(row + 16 * ((ch + 1) ^ swc));
+    }
+    i32x8 r;
+    r[0] = (int)x.x; r[1] = (int)x.y; r[2] = (int)x.z; r[3] = (int)x.w;
+    r[4] = (int)y.x; r[5] = (int)y.y; r[6] = (int)y.z; r[7] = (int)y.w;
+    return r;
+  };
   auto rdB = [&](const unsigned char* buf, int db) {
-    const int ch = 2 * (dbase / 32 + db) + g1;
     i32x8 r;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      auto* p = (__attribute__((address_space(3))) i32x2*)(void*)(buf + trow[c] + 16 * (ch ^ tsw[c]));
-      const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(p);
+      const unsigned char* a;
+      if constexpr (DS == 1) {
+        a = buf + 16 * PC * (db / NB) + offB[c][db % NB];
+      } else {
+        const int ch = 2 * (dbase / 32 + db) + g1;
+        a = buf + trow[c] + 16 * (ch ^ tsw[c]);
+      }
+      const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) i32x2*)(void*)a);
       r[2 * c] = v[0];
       r[2 * c + 1] = v[1];
     }

@@ -40,7 +40,8 @@ def main():
     if args.dtype == "fp32":
         E, enorm = E32, None
     else:
-        E = ops.decoder_image(E32)
+        from hvae import _lib
+        E = ops.decoder_image(E32, _lib.HVAE_FP8 if args.dtype == "fp8" else _lib.HVAE_BF16)
         enorm = ops.row_norm_max(E)
     if args.train:
         sys.path.insert(0, str(ROOT / "tests" / "golden"))
