@@ -354,12 +354,17 @@ int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v, const hva
  *   gradient rows of rg (their missed steps replayed first).
  * hvae_adam_lazy_catchup: bring rows to *cfg->step_dev completed steps: the
  *   rows listed by `rows` (item_of[0 : *n_unique]; before a batch's forward),
- *   or all N rows when rows == NULL (before anything else reads W1t, m or v). */
+ *   or all N rows when rows == NULL (before anything else reads W1t, m or v).
+ * hvae_adam_lazy_catchup_csr: the same for the rows the CSR batch x lists (duplicates
+ *   replayed once), without the W1-gradient plan: the plan can then run beside
+ *   the forward. Bitwise equal to hvae_adam_lazy_catchup on the plan's rows. */
 int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
                    int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense, int64_t dense_off,
                    int64_t n_dense, void* stream);
 int hvae_adam_lazy_catchup(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v,
                            int32_t* last_step, const hvae_rowgrad* rows, int64_t N, int64_t H, void* stream);
+int hvae_adam_lazy_catchup_csr(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v,
+                               int32_t* last_step, const hvae_csr_batch* x, int64_t H, void* stream);
 /* *counter += delta (device-side step/batch counters for graph replay). */
 int hvae_counter_add(int64_t* counter, int64_t delta, void* stream);
 /* *a += da and, if b != NULL, *b += db, in one launch (end of a train step). */

@@ -321,6 +321,48 @@ __global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* 
   }
 }
 
+// The same catch-up from the batch's CSR entries instead of the W1-gradient plan's unique-row list, so
+// that it does not wait for the plan (which then runs beside the forward on another stream). A row listed
+// by several entries is claimed once: the entry's thread moves last_step[j] from its value to `to` with an
+// atomicCAS, and only the winner's row is replayed; the replayed arithmetic is the same, so the result is
+// bitwise that of k_adam_catchup. One block per batch row (grid-stride): all its entries claim at once,
+// then every thread walks the claimed rows' float4 columns (no barrier between rows).
+__global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const float2* __restrict__ tab, float* p,
+                                                          float* m, float* v, int32_t* __restrict__ last_step,
+                                                          hvae_csr_batch x, int64_t H) {
+  __shared__ int s_j[256], s_from[256];
+  __shared__ int s_n;
+  const int to = (int)load_step(a.step_dev);
+  const int64_t H4 = H / 4;
+  const AdamK none{};
+  for (int64_t b = blockIdx.x; b < x.nb; b += gridDim.x) {
+    const int64_t r = batch_row(x.rows, x.rows_offset, b);
+    const int64_t e0 = x.row_ptr[r], e1 = x.row_ptr[r + 1];
+    for (int64_t g0 = e0; g0 < e1; g0 += 256) {
+      if (threadIdx.x == 0) s_n = 0;
+      __syncthreads();
+      const int64_t e = g0 + threadIdx.x;
+      if (e < e1) {
+        const int j = x.col_idx[e];
+        const int from = __hip_atomic_load(last_step + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (from < to && atomicCAS(last_step + j, from, to) == from) {
+          const int k = atomicAdd(&s_n, 1);
+          s_j[k] = j;
+          s_from[k] = from;
+        }
+      }
+      __syncthreads();
+      const int64_t work = (int64_t)s_n * H4;
+      for (int64_t idx = threadIdx.x; idx < work; idx += blockDim.x) {
+        const int k = (int)(idx / H4);
+        col_update(a, tab, p, m, v, (int64_t)s_j[k] * H4 + idx % H4, s_from[k], to, false, none,
+                   make_float4(0.f, 0.f, 0.f, 0.f));
+      }
+      __syncthreads();
+    }
+  }
+}
+
 // The step's update with lazy W1t. Blocks [0, nb_rows) take the gradient rows
 // (replay missed steps, then step t = *step + 1 with the clipped gradient);
 // blocks [nb_rows, nb_rows + nb_sweep) bring one of kLazySweep row ranges (rotating
@@ -548,6 +590,19 @@ extern "C" int hvae_adam_lazy_catchup(const hvae_adam* cfg, const float* tab, fl
                                                       rows ? rows->item_of : nullptr,
                                                       rows ? rows->n_unique : nullptr, N, H, rm);
   HVAE_LAUNCH_CHECK("k_adam_catchup");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_adam_lazy_catchup_csr(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v,
+                                          int32_t* last_step, const hvae_csr_batch* x, int64_t H, void* stream) {
+  HVAE_REQUIRE(cfg && cfg->step_dev && tab && p && m && v && last_step && H % 4 == 0 && x && x->row_ptr &&
+                   x->col_idx,
+               "hvae_adam_lazy_catchup_csr: bad args");
+  if (x->nb == 0) return HVAE_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>(x->nb, 16384);
+  ProbeScope probe("adam_catchup", as_stream(stream));
+  k_adam_catchup_csr<<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v, last_step, *x, H);
+  HVAE_LAUNCH_CHECK("k_adam_catchup_csr");
   return HVAE_OK;
 }
 

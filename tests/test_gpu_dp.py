@@ -55,7 +55,10 @@ def _worker_body(rank, world, port, q):
     gen = torch.Generator().manual_seed(100 + rank)
     losses = [fused.run_epoch(data, 32, True, ConstBeta(0.2), 0.3, generator=gen)["total_loss"] for _ in range(3)]
     torch.cuda.synchronize()
-    q.put((rank, losses, fused.flat.cpu(), fused.m.cpu(), fused.v.cpu(), int(fused.step_dev.item())))
+    # numpy arrays pickle by value: a torch CPU tensor would travel as a shared-memory fd, which the parent can
+    # only open while this process is alive (it may already have exited: EOFError in the parent)
+    q.put((rank, losses, fused.flat.cpu().numpy(), fused.m.cpu().numpy(), fused.v.cpu().numpy(),
+           int(fused.step_dev.item())))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -72,7 +75,8 @@ def test_dp_two_ranks_one_gpu(hip_device):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    (_, la, fa, ma, va, sa), (_, lb, fb, mb, vb, sb) = res
+    (_, la, fa, ma, va, sa), (_, lb, fb, mb, vb, sb) = [
+        (r, l_, torch.from_numpy(f), torch.from_numpy(m), torch.from_numpy(v), s_) for r, l_, f, m, v, s_ in res]
     assert sa == sb == 3 * ((300 + 31) // 32)
     assert torch.equal(fa, fb) and torch.equal(ma, mb) and torch.equal(va, vb)  # replicas identical
     assert torch.isfinite(fa).all()
