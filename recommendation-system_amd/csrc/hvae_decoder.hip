@@ -739,6 +739,9 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 constexpr int kF8TI = 64;  // items per tile
+#ifndef F8_G2_AHEAD
+#define F8_G2_AHEAD 2
+#endif
 
 template <int D>
 constexpr int f8_tile_bytes() { return 64 * D; }
@@ -938,13 +941,20 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   for (int d = 0; d < (WITH_O ? DB : 1); ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  // GEMM2 A operands in flight: DS = 1 keeps F8_G2_AHEAD d-blocks of transposed reads ahead (the D split has
+  // no registers for more than one). Measured at Syn-1M shape: 1, 2, 3, 4 ahead = 363, 359, 361, 359 us, so the
+  // operand latency is not what bounds the sweep (scripts/gpu_dec8_ab.sh)
+  constexpr int AH2 = DS == 1 ? F8_G2_AHEAD : 1;
   auto gemm2 = [&](const unsigned char* buf, const i32x8& pf, int sbp) {
     if constexpr (WITH_O) {
-      i32x8 a = rdB(buf, 0);
+      i32x8 a[AH2];
+#pragma unroll
+      for (int j = 0; j < AH2; ++j)
+        if (j < DB) a[j] = rdB(buf, j);
 #pragma unroll
       for (int db = 0; db < DB; ++db) {
-        const i32x8 c = a;
-        if (db + 1 < DB) a = rdB(buf, db + 1);
+        const i32x8 c = a[db % AH2];
+        if (db + AH2 < DB) a[db % AH2] = rdB(buf, db + AH2);
         o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
       }
     }
