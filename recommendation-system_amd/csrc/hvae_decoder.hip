@@ -974,10 +974,20 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
         c1[r] = it + 32 >= lim ? -INFINITY : c1[r];
       }
     }
-    float mx = fmaxf(c0[0], c1[0]);
+    // tree of v_max3 (depth 4 instead of a 31-long chain), then the other lane half through
+    // v_permlane32_swap (a VALU op; __shfl_xor is an LDS round trip): r[0] / r[1] = the value of lane
+    // (l & 31) / (l & 31) + 32, so their max is the column's in every lane
+    float t3[11];
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(c0[r], c1[r]));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    for (int i = 0; i < 5; ++i) t3[i] = fmaxf(fmaxf(c0[3 * i], c0[3 * i + 1]), c0[3 * i + 2]);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) t3[5 + i] = fmaxf(fmaxf(c1[3 * i], c1[3 * i + 1]), c1[3 * i + 2]);
+    t3[10] = fmaxf(c0[15], c1[15]);
+    const float u0 = fmaxf(fmaxf(t3[0], t3[1]), t3[2]), u1 = fmaxf(fmaxf(t3[3], t3[4]), t3[5]);
+    const float u2 = fmaxf(fmaxf(t3[6], t3[7]), t3[8]), u3 = fmaxf(t3[9], t3[10]);
+    float mx = fmaxf(fmaxf(u0, u1), fmaxf(u2, u3));
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    mx = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
     if (t == t_beg) {  // as k_dec2_bf16: p = exp(s - m) <= e^60, never rescaled; flagged if l ends tiny
       m = fmaxf(mx, bound - kOffsetSpan);
       mL = m * kLog2e;
@@ -1005,8 +1015,8 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
       // tile t + NS - 1 into the slot of tile t - 1 (every wave finished its GEMM2 before the barrier)
       issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
       if (wave_active) {
-        const int e = tile_prep(t, c0, c1);
-        const float cE = mL + (float)e;
+        int e = 0;
+        float cE = 0.f;
         float qv[32];
         int pk[8];
         float qsum = 0.f;
@@ -1020,7 +1030,15 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
           }
         };
         f32x16 n0, n1;
-        gemm1(lds + nxt * TB, n0, n1, [&](int g) { smax(32 * g / KS / 4 * 4, 32 * (g + 1) / KS / 4 * 4); });
+        // tile t's max and exponent under GEMM1(t+1)'s first MFMA pair, its exponentials under the others
+        gemm1(lds + nxt * TB, n0, n1, [&](int g) {
+          if (g == 0) {
+            e = tile_prep(t, c0, c1);
+            cE = mL + (float)e;
+          } else {
+            smax(4 * ((8 * (g - 1)) / (KS - 1)), 4 * ((8 * g) / (KS - 1)));
+          }
+        });
         lsum += ldexpf(qsum, e);
         i32x8 pf;
 #pragma unroll
