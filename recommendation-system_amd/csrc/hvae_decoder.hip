@@ -742,6 +742,9 @@ constexpr int kF8TI = 64;  // items per tile
 #ifndef F8_G2_AHEAD
 #define F8_G2_AHEAD 2
 #endif
+#ifndef F8_SPREAD
+#define F8_SPREAD 0
+#endif
 
 template <int D>
 constexpr int f8_tile_bytes() { return 64 * D; }
@@ -837,19 +840,21 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<unsigned char*>(T8), (short)0, (int)(ntiles * TB), 0x00020000);
   const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
-  auto issue = [&](int64_t t, int slot_i) {
+  auto issue_range = [&](int64_t t, int slot_i, int i0, int i1) {
     const uint32_t soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)TB));
     const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
 #pragma unroll
-    for (int i = 0; i < PW; ++i)
-      if (i == 0)  // soff may be fresh from v_readfirstlane: 5 wait states before a buffer op reads it
+    for (int i = i0; i < i1; ++i)
+      if (i == i0)  // soff may be fresh from v_readfirstlane: 5 wait states before a buffer op reads it
         asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                     :: "s"(lb), "v"(voff), "s"(rsrc), "s"(soff) : "memory");
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff), "s"(rsrc), "s"(soff + (uint32_t)(i * 1024))
+                     : "memory");
       else
         asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                      :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff), "s"(rsrc), "s"(soff + (uint32_t)(i * 1024))
                      : "memory");
   };
+  auto issue = [&](int64_t t, int slot_i) { issue_range(t, slot_i, 0, PW); };
   auto lds_fence = [] { asm volatile("" ::: "memory"); };
   auto barrier = [&] {
     lds_fence();
@@ -945,7 +950,7 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   // no registers for more than one). Measured at Syn-1M shape: 1, 2, 3, 4 ahead = 363, 359, 361, 359 us, so the
   // operand latency is not what bounds the sweep (scripts/gpu_dec8_ab.sh)
   constexpr int AH2 = DS == 1 ? F8_G2_AHEAD : 1;
-  auto gemm2 = [&](const unsigned char* buf, const i32x8& pf, int sbp) {
+  auto gemm2 = [&](const unsigned char* buf, const i32x8& pf, int sbp, auto&& after) {
     if constexpr (WITH_O) {
       i32x8 a[AH2];
 #pragma unroll
@@ -956,6 +961,7 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
         const i32x8 c = a[db % AH2];
         if (db + AH2 < DB) a[db % AH2] = rdB(buf, db + AH2);
         o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
+        after(db);
       }
     }
   };
@@ -1012,8 +1018,13 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
       wait_vmcnt<(NS - 3) * PW>();  // tile t + 1 has landed
       barrier();
       const int nxt = cur == NS - 1 ? 0 : cur + 1;
-      // tile t + NS - 1 into the slot of tile t - 1 (every wave finished its GEMM2 before the barrier)
-      issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
+      // tile t + NS - 1 into the slot of tile t - 1 (every wave finished its GEMM2 before the barrier):
+      // in one burst here, or (F8_SPREAD) its pieces spread over GEMM2(t)'s MFMAs (Syn-1M shape: 334 us burst,
+      // 349 us spread)
+      const int64_t t_dma = min(t + NS - 1, t_end - 1);
+      const int s_dma = cur == 0 ? NS - 1 : cur - 1;
+      constexpr bool spread = F8_SPREAD && WITH_O;
+      if (!spread || !wave_active) issue(t_dma, s_dma);
       if (wave_active) {
         int e = 0;
         float cE = 0.f;
@@ -1043,7 +1054,10 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
         i32x8 pf;
 #pragma unroll
         for (int i = 0; i < 8; ++i) pf[i] = pk[i];
-        gemm2(lds + cur * TB, pf, 127 + e);
+        gemm2(lds + cur * TB, pf, 127 + e, [&](int db) {
+          if constexpr (spread)
+            if (PW * db / DB < PW * (db + 1) / DB) issue_range(t_dma, s_dma, PW * db / DB, PW * (db + 1) / DB);
+        });
         c0 = n0;
         c1 = n1;
       }
@@ -1104,7 +1118,7 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
           pf[j4] = pack_fp8x4(q[0], q[1], q[2], q[3]);
         }
         lsum += ldexpf(qsum, e);
-        gemm2(lds + cur * TB, pf, 127 + e);
+        gemm2(lds + cur * TB, pf, 127 + e, [](int) {});
       }
       barrier();  // slot cur and the exchange buffer are free
       issue(min(t + 2, t_end - 1), cur);
