@@ -745,6 +745,9 @@ constexpr int kF8TI = 64;  // items per tile
 #ifndef F8_SPREAD
 #define F8_SPREAD 0
 #endif
+#ifndef F8_DS2_AHEAD
+#define F8_DS2_AHEAD 1  // d = 768 (200 K items): 1, 2, 3 ahead = 1713, 1724-1732, 1757 us
+#endif
 
 template <int D>
 constexpr int f8_tile_bytes() { return 64 * D; }
@@ -949,7 +952,7 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   // GEMM2 A operands in flight: DS = 1 keeps F8_G2_AHEAD d-blocks of transposed reads ahead (the D split has
   // no registers for more than one). Measured at Syn-1M shape: 1, 2, 3, 4 ahead = 363, 359, 361, 359 us, so the
   // operand latency is not what bounds the sweep (scripts/gpu_dec8_ab.sh)
-  constexpr int AH2 = DS == 1 ? F8_G2_AHEAD : 1;
+  constexpr int AH2 = DS == 1 ? F8_G2_AHEAD : F8_DS2_AHEAD;
   auto gemm2 = [&](const unsigned char* buf, const i32x8& pf, int sbp, auto&& after) {
     if constexpr (WITH_O) {
       i32x8 a[AH2];
