@@ -745,6 +745,9 @@ constexpr int kF8TI = 64;  // items per tile
 #ifndef F8_SPREAD
 #define F8_SPREAD 0
 #endif
+#ifndef F8_DS2_RING
+#define F8_DS2_RING 1  // D = 768: 3-slot ring with the softmax split over the wave pair (0: 2-slot sequence)
+#endif
 #ifndef F8_DS2_AHEAD
 #define F8_DS2_AHEAD 1  // d = 768 (200 K items): 1, 2, 3 ahead = 1713, 1724-1732, 1757 us
 #endif
@@ -752,10 +755,11 @@ constexpr int kF8TI = 64;  // items per tile
 template <int D>
 constexpr int f8_tile_bytes() { return 64 * D; }
 template <int D>
-constexpr int f8_xbytes() { return D > 384 ? 4 * 8192 : 0; }  // DS = 2: [4 waves][s0, s1][64 lanes][16] floats
+constexpr int f8_xbytes() { return D > 384 ? 4 * (F8_DS2_RING ? 4096 : 8192) : 0; }  // DS = 2 exchange, 4 waves
 template <int D>
 constexpr int f8_stages() {
-  return D > 384 ? 2 : ((160 * 1024) / f8_tile_bytes<D>() >= 6 ? 6 : (160 * 1024) / f8_tile_bytes<D>());
+  return D > 384 ? (F8_DS2_RING ? 3 : 2)
+                 : ((160 * 1024) / f8_tile_bytes<D>() >= 6 ? 6 : (160 * 1024) / f8_tile_bytes<D>());
 }
 // fp8 image: bf16 E [N][D] (exact fixups, score bound) | e4m3 tiles [ntiles][64][D] (swizzled) | int ke
 static inline int64_t f8_offset_bytes(int64_t N, int64_t D) { return et_offset_bytes(N, D); }
@@ -791,7 +795,8 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   constexpr int PW = TB / 4096;          // 1-KiB LDS-DMA pieces per wave per tile
   constexpr int NS = f8_stages<D>();
   constexpr int UPB = 128 / DS;          // users per block
-  static_assert(D % 64 == 0 && (DS == 1 ? (D <= 384 && NS >= 3) : (D == 768 && NS == 2)), "fp8 decoder shape");
+  static_assert(D % 64 == 0 && (DS == 1 ? (D <= 384 && NS >= 3) : (D == 768 && NS == (F8_DS2_RING ? 3 : 2))),
+                "fp8 decoder shape");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
@@ -1066,8 +1071,127 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
       }
       cur = nxt;
     }
+  } else if constexpr (F8_DS2_RING) {
+    // DS = 2, 3-slot ring: wave dh owns the softmax of items 32 dh .. 32 dh + 31. Per tile: the partial S^T of
+    // the partner's item half crosses through LDS (4 KiB per wave), the wave completes its own half, runs its
+    // 16 exponentials under GEMM1(t+1)'s MFMAs, and the packed P half and its block exponent cross back
+    // through the same buffer (the MFMA takes block b's scale from lane column + 32 b) before GEMM2(t).
+    // Three 48 KiB slots + 4 x 4 KiB exchange = 160 KiB.
+    float* xmine = reinterpret_cast<float*>(lds + NS * TB + w * 4096);
+    const float* xpart = reinterpret_cast<const float*>(lds + NS * TB + (w ^ 2) * 4096);
+    auto half_of = [&](const f32x16& a0, const f32x16& a1) -> const f32x16& { return dh == 0 ? a0 : a1; };
+    auto put16 = [&](const f32x16& sv) {
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4)
+        *reinterpret_cast<float4*>(xmine + r4 * 256 + lane * 4) =
+            make_float4(sv[4 * r4], sv[4 * r4 + 1], sv[4 * r4 + 2], sv[4 * r4 + 3]);
+    };
+    // own half's full S^T = d-half 0 partial + d-half 1 partial (the same order in both waves' halves)
+    auto complete = [&](const f32x16& own, f32x16& sm) {
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4) {
+        const float4 y = *reinterpret_cast<const float4*>(xpart + r4 * 256 + lane * 4);
+        const float yv[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sm[4 * r4 + k] = dh == 0 ? own[4 * r4 + k] + yv[k] : yv[k] + own[4 * r4 + k];
+      }
+    };
+    auto half_max = [&](int64_t t, f32x16& sm) {
+      if (t == ntiles - 1 && (N % kF8TI) != 0) {
+        const int lim = (int)(N - t * kF8TI) - 4 * h - 32 * dh;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sm[r] = ((r & 3) + 8 * (r >> 2) >= lim) ? -INFINITY : sm[r];
+      }
+      const float a0 = fmaxf(fmaxf(sm[0], sm[1]), sm[2]), a1 = fmaxf(fmaxf(sm[3], sm[4]), sm[5]);
+      const float a2 = fmaxf(fmaxf(sm[6], sm[7]), sm[8]), a3 = fmaxf(fmaxf(sm[9], sm[10]), sm[11]);
+      const float a4 = fmaxf(fmaxf(sm[12], sm[13]), fmaxf(sm[14], sm[15]));
+      float mx = fmaxf(fmaxf(fmaxf(a0, a1), a2), fmaxf(a3, a4));
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    };
+    f32x16 c0, c1;  // this wave's partial S^T of the current tile (both item halves)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) { c0[r] = 0.f; c1[r] = 0.f; }
+    constexpr int PRE = NS - 1;
+    if (t_beg < t_end) {
+#pragma unroll
+      for (int i = 0; i < PRE; ++i) issue(min(t_beg + i, t_end - 1), i);
+      wait_vmcnt<(PRE - 1) * PW>();
+    }
+    barrier();
+    if (t_beg < t_end && wave_active) gemm1(lds, c0, c1, [](int) {});
+    int cur = 0;
+    for (int64_t t = t_beg; t < t_end; ++t) {
+      wait_vmcnt<(NS - 3) * PW>();  // tile t + 1 has landed
+      barrier();                    // B1: iteration t - 1 is over everywhere (slot t - 1, exchange buffer)
+      const int nxt = cur == NS - 1 ? 0 : cur + 1;
+      issue(min(t + NS - 1, t_end - 1), cur == 0 ? NS - 1 : cur - 1);
+      if (wave_active) put16(half_of(c1, c0));  // the partner's item half of my D-half partial
+      barrier();                                // B2
+      f32x16 sm;
+      float mh = 0.f;
+      if (wave_active) {
+        complete(half_of(c0, c1), sm);
+        mh = half_max(t, sm);
+      }
+      if (t == t_beg) {  // the pair's common offset from the first tile's max over both halves
+        barrier();
+        if (wave_active) xmine[lane] = mh;
+        barrier();
+        if (wave_active) {
+          m = fmaxf(fmaxf(mh, xpart[lane]), bound - kOffsetSpan);
+          mL = m * kLog2e;
+        }
+      }
+      int e = 0;
+      int pk[4];
+      f32x16 n0, n1;
+      if (wave_active) {
+        e = max(-119, min(127, (int)ceilf(__builtin_fmaf(mh, kLog2e, -mL)) - 8));
+        const float cE = mL + (float)e;
+        float qv[16];
+        float qsum = 0.f;
+        gemm1(lds + nxt * TB, n0, n1, [&](int g) {
+#pragma unroll
+          for (int j = 4 * ((4 * g) / KS); j < 4 * ((4 * g + 4) / KS); ++j) {
+            qv[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(sm[j], kLog2e, -cE));
+            qsum += qv[j];
+            if ((j & 3) == 3) pk[j >> 2] = pack_fp8x4(qv[j - 3], qv[j - 2], qv[j - 1], qv[j]);
+          }
+        });
+        lsum += ldexpf(qsum, e);
+      }
+      barrier();  // B3: the partner has read my partial
+      if (wave_active) {
+        reinterpret_cast<int4*>(xmine)[lane] = make_int4(pk[0], pk[1], pk[2], pk[3]);
+        reinterpret_cast<int*>(xmine)[256 + lane] = e;
+      }
+      barrier();  // B4
+      if (wave_active) {
+        const int4 y = reinterpret_cast<const int4*>(xpart)[lane];
+        const int ey = reinterpret_cast<const int*>(xpart)[256 + lane];
+        i32x8 pf;
+        if (dh == 0) {
+          pf[0] = pk[0]; pf[1] = pk[1]; pf[2] = pk[2]; pf[3] = pk[3];
+          pf[4] = y.x; pf[5] = y.y; pf[6] = y.z; pf[7] = y.w;
+        } else {
+          pf[0] = y.x; pf[1] = y.y; pf[2] = y.z; pf[3] = y.w;
+          pf[4] = pk[0]; pf[5] = pk[1]; pf[6] = pk[2]; pf[7] = pk[3];
+        }
+        gemm2(lds + cur * TB, pf, 127 + (h == dh ? e : ey), [](int) {});  // lane half h: block h's scale
+        c0 = n0;
+        c1 = n1;
+      }
+      cur = nxt;
+    }
+    // the user's l = l(items 0-31) + l(items 32-63), the same sum in both waves
+    const float lw = lsum + __shfl_xor(lsum, 32, 64);
+    barrier();
+    if (wave_active) xmine[lane] = lw;
+    barrier();
+    if (wave_active) lsum = dh == 0 ? lw + xpart[lane] : xpart[lane] + lw;
   } else {
-    // DS = 2: two slots; tile t + 1's LDS-DMA runs under all of tile t
+    // DS = 2, two slots: tile t + 1's LDS-DMA runs under all of tile t
     float* xbuf = reinterpret_cast<float*>(lds + NS * TB);  // [4 w][2 s][64 lane][16]
     auto xput = [&](const f32x16& s0, const f32x16& s1) {
       float* xb = xbuf + w * 2048;
@@ -1130,7 +1254,7 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   }
 
   if (!wave_active) return;
-  const float ltot = lsum + __shfl_xor(lsum, 32, 64);
+  const float ltot = (DS == 2 && F8_DS2_RING) ? lsum : lsum + __shfl_xor(lsum, 32, 64);
   if (user >= nb) return;
   if (h == 0 && dh == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
   if (out.direct) {
