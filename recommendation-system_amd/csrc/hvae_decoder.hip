@@ -745,6 +745,9 @@ constexpr int kF8TI = 64;  // items per tile
 #ifndef F8_SPREAD
 #define F8_SPREAD 0
 #endif
+#ifndef F8_G1_AHEAD
+#define F8_G1_AHEAD 1  // GEMM1 operand k-steps in flight (Syn-1M shape: 1 = 335 us, 2 = 344 us)
+#endif
 #ifndef F8_DS2_RING
 #define F8_DS2_RING 1  // D = 768: 3-slot ring with the softmax split over the wave pair (0: 2-slot sequence)
 #endif
@@ -938,11 +941,16 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   auto gemm1 = [&](const unsigned char* buf, f32x16& s0, f32x16& s1, auto&& fill) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
-    i32x8 a0 = rdA(buf, 0, 0), a1 = rdA(buf, 0, 1);
+    // A operands of G1A k-steps in flight (DS = 1; the D split has no registers for a second)
+    constexpr int G1A = DS == 1 ? F8_G1_AHEAD : 1;
+    i32x8 ra0[G1A], ra1[G1A];
+#pragma unroll
+    for (int j = 0; j < G1A; ++j)
+      if (j < KS) { ra0[j] = rdA(buf, j, 0); ra1[j] = rdA(buf, j, 1); }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) {
-      const i32x8 c0 = a0, c1 = a1;
-      if (ks + 1 < KS) { a0 = rdA(buf, ks + 1, 0); a1 = rdA(buf, ks + 1, 1); }
+      const i32x8 c0 = ra0[ks % G1A], c1 = ra1[ks % G1A];
+      if (ks + G1A < KS) { ra0[ks % G1A] = rdA(buf, ks + G1A, 0); ra1[ks % G1A] = rdA(buf, ks + G1A, 1); }
       s0 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c0, uf[ks], s0, 0, 0, 0, sa, 0, sbu);
       s1 = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c1, uf[ks], s1, 0, 0, 0, sa, 0, sbu);
       fill(ks);
