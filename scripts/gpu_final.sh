@@ -5,8 +5,8 @@ R=$GRAFT_REPO_ROOT
 mkdir -p gpurun_out/final
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/final/pytest.log 2>&1
 timeout -k 10 300 python bench.py > gpurun_out/final/bench.log 2>&1
-timeout -k 10 300 python bench.py --workload syn1m --steps 60 --warmup 5 --probe-steps 5 --no-cpu-baseline > gpurun_out/final/bench_syn1m.log 2>&1
-timeout -k 10 300 python bench.py --workload syn1m --precision fp8 --steps 60 --warmup 5 --probe-steps 5 --no-cpu-baseline > gpurun_out/final/bench_syn1m_fp8.log 2>&1
+timeout -k 10 300 python bench.py --workload syn1m --steps 200 --warmup 10 --probe-steps 5 --no-cpu-baseline > gpurun_out/final/bench_syn1m.log 2>&1
+timeout -k 10 300 python bench.py --workload syn1m --precision fp8 --steps 200 --warmup 10 --probe-steps 5 --no-cpu-baseline > gpurun_out/final/bench_syn1m_fp8.log 2>&1
 timeout -k 10 400 python -u bench.py --workload syn10m --steps 20 --warmup 3 --probe-steps 2 --no-cpu-baseline > gpurun_out/final/bench_syn10m.log 2>&1
 timeout -k 10 400 python -u bench.py --workload syn10m --precision fp8 --steps 20 --warmup 3 --probe-steps 2 --no-cpu-baseline > gpurun_out/final/bench_syn10m_fp8.log 2>&1
 cd /tmp && export TMPDIR=/tmp
