@@ -1,3 +1,4 @@
+# Data-parallel rehearsal on one GPU: GPU tests, then a 2-rank bench.py (gloo transport, both ranks on the one MI355X).
 set -e
 mkdir -p gpurun_out
 timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest.log 2>&1

@@ -1,3 +1,4 @@
+# PMC passes (one counter group per run) for the bf16 decoder sweep at the Syn-1M shape.
 set -e
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/pmc2

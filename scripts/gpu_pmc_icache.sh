@@ -1,3 +1,4 @@
+# Instruction-fetch PMC passes over the default bench (the latency-bound All_Beauty step).
 set -e
 R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out/pmc3

@@ -1,3 +1,4 @@
+# rocprofv3 kernel-trace stats of the Syn-1M bench.
 set -e
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp
