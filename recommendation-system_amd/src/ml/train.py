@@ -239,7 +239,11 @@ def _build_matrix(df: pd.DataFrame, user_to_idx: dict, item_to_idx: dict, shape:
 
 def _get_device(device: str | None = None) -> torch.device:
     if device:
-        return torch.device(device)
+        dev = torch.device(device)
+        if dev.type != "cuda":  # the reference's cpu / mps choices parse, then fail here, before any data loads
+            raise RuntimeError(f"device {device!r}: the MI355X HybridVAE path runs on a HIP device only; "
+                               "there is no CPU fallback.")
+        return dev
     if torch.cuda.is_available():
         return torch.device("cuda")
     raise RuntimeError("The MI355X HybridVAE path needs a HIP device (torch.cuda on ROCm); none is visible. "

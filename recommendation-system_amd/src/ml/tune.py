@@ -44,7 +44,11 @@ DEFAULT_SEARCH_SPACE = {
 
 def _get_device(device: str | None = None) -> torch.device:
     if device:
-        return torch.device(device)
+        dev = torch.device(device)
+        if dev.type != "cuda":  # the reference's cpu / mps choices parse, then fail here, before any data loads
+            raise RuntimeError(f"device {device!r}: the MI355X HybridVAE path runs on a HIP device only; "
+                               "there is no CPU fallback.")
+        return dev
     if torch.cuda.is_available():
         return torch.device("cuda")
     raise RuntimeError("The MI355X HybridVAE path needs a HIP device (torch.cuda on ROCm); none is visible. "
@@ -182,7 +186,8 @@ def main() -> None:
     parser.add_argument("--epochs", type=int, default=10, help="Max epochs per config")
     parser.add_argument("--patience", type=int, default=3, help="Early stopping patience")
     parser.add_argument("--batch-size", type=int, default=512, help="Batch size")
-    parser.add_argument("--device", choices=["cuda"], help="Device (a HIP device; there is no CPU fallback)")
+    parser.add_argument("--device", choices=["cuda", "mps", "cpu"],
+                        help="Device (reference flag; only a HIP device runs: cpu / mps raise, there is no CPU fallback)")
     parser.add_argument("--latent-dims", type=int, nargs="+", default=[32, 64, 128])
     parser.add_argument("--dropouts", type=float, nargs="+", default=[0.3, 0.5])
     parser.add_argument("--betas", type=float, nargs="+", default=[0.1, 0.2, 0.3])
