@@ -11,6 +11,7 @@
 // (device-scope ticket) sums the partials in split order 0..S-1 and applies
 // the epilogue -- deterministic, and no second launch.
 #include <algorithm>
+#include <cstdlib>
 
 #include "hvae_common.h"
 
@@ -384,11 +385,23 @@ __global__ void k_colsum_final(const float* __restrict__ part, int64_t P, int64_
 }
 
 // Tile choice: 32x32 for the batch-sized GEMMs (short K, few 64x64 tiles: spread the
-// output over more CUs); 64x64 when that already gives >= 64 tiles or K is long
-// (then split-K into register-staged ranges fills the machine instead).
+// output over more CUs); 64x64 when that already gives >= 512 tiles (two blocks per CU)
+// or K is long (then split-K into register-staged ranges fills the machine instead).
+// At B = 4096 (scripts/bench_gemm.py, MI355X) the 512 threshold moved 4096x128x384 from
+// 21.2 to 14.2 us and 4096x256x512 from 26.2 to 24.3 us against the old 64, while
+// 4096x512x256 keeps its 64x64 tiles (23.9 us; 27.6 with 32x32).
+// HVAE_GEMM_TILE64_MIN (A/B knob, read once): the 64x64-tile count from which 64x64 tiles are used.
+static int64_t tile64_min() {
+  static const int64_t v = [] {
+    const char* e = std::getenv("HVAE_GEMM_TILE64_MIN");
+    return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)512;
+  }();
+  return v;
+}
+
 static int gemm_tile(int64_t M, int64_t N, int64_t K) {
   if (K > 4 * (int64_t)GBK * kRegStages) return 64;
-  return cdiv(M, 64) * cdiv(N, 64) >= 64 ? 64 : 32;
+  return cdiv(M, 64) * cdiv(N, 64) >= tile64_min() ? 64 : 32;
 }
 
 static int gemm_splits(int64_t M, int64_t N, int64_t K) {
