@@ -1,16 +1,17 @@
 #!/usr/bin/env python3
 """HybridVAE train throughput (users/sec) on MI355X -- the BASELINE.json metric.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload all_beauty|appliances|syn1m]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload syn10m|syn1m|all_beauty|appliances]
 
 One "step" = one fused train step (encoder -> reparam/KL -> projection ->
 streaming decoder + multinomial loss -> backward -> clip 5.0 -> Adam) over
 one batch of users of a synthetic interaction matrix shaped like the named
-workload (default: BASELINE.json configs[1], All_Beauty 22,363 x 12,101,
-d=384, latent 128, hidden [512], batch 64, bf16 decoder MFMA). Inputs (CSR,
-weights, frozen E) are resident in HBM before the timed region. N > 1 runs
-one process per GPU (torchrun), user-batch data parallel with the gradient
-exchange over RCCL (weak scaling: B users per GPU per step).
+workload. Default: the north-star config (BASELINE.json configs[3]) on one
+GPU -- a 1.25 M-user shard (10 M users / 8 GPUs) of the 10M x 1M synthetic,
+d = 768, latent 128, hidden [512], 4096 users per GPU per step, bf16 decoder
+MFMA. Inputs (CSR, weights, frozen E) are resident in HBM before the timed
+region. N > 1 runs one process per GPU (torchrun), user-batch data parallel
+with the gradient exchange over RCCL (weak scaling: B users per GPU per step).
 
 Prints ONE JSON line on rank 0, with a live roofline for the dominant kernel
 (HIP events around its launches on the stream it runs on) and the CPU
@@ -72,52 +73,143 @@ def make_data(w: dict, rank: int, world: int):
     return X, E, users
 
 
-def mean_unique_items(X, users, B: int, gen_seed: int = 0, samples: int = 32) -> float:
-    """Mean count of distinct items in a batch of B users drawn from `users` (W1t rows with a gradient)."""
+def batch_stats(X, users, B: int, gen_seed: int = 0, samples: int = 32) -> tuple[float, float]:
+    """Mean distinct items (W1t rows with a gradient) and mean stored entries of a batch of B users."""
     rng = np.random.default_rng(gen_seed)
-    tot = 0
+    tot = nnz = 0
     for _ in range(samples):
         rows = rng.choice(users, size=min(B, len(users)), replace=False)
-        tot += len(np.unique(X[rows].indices))
-    return tot / samples
+        sub = X[rows]
+        tot += len(np.unique(sub.indices))
+        nnz += sub.nnz
+    return tot / samples, nnz / samples
 
 
-def cpu_baseline(w: dict, X, E, seconds: float) -> dict:
+def host_cores() -> tuple[int, str]:
+    """CPUs this process may run on (affinity, capped by a cgroup CPU quota) and the CPU model."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:  # cgroup v2 quota ("max 100000" = unlimited)
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            n = max(1, min(n, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return n, model
+
+
+def cpu_baseline(w: dict, X, E, seconds: float, threads: int | None = None) -> dict:
     """The pinned CPU restatement of the reference trainer on this host's cores.
 
     Per batch: the reference loader's per-row densification (UserInteractionDataset
     .__getitem__ + collate, src/ml/train.py:45-47) then one train step
-    (fwd, loss, backward, clip 5.0, Adam) -- the work of one GPU step.
+    (fwd, loss, backward, clip 5.0, Adam; src/ml/train.py:81-103) -- the work of
+    one GPU step. The loader and the step are timed separately: "value" is the
+    two in series (the reference's num_workers=0 DataLoader), "step_only" the
+    step alone.
     """
     from oracle import ref_cpu as R
-    threads = min(16, os.cpu_count() or 1)
+    cores, model = host_cores()
+    threads = threads or cores
     torch.set_num_threads(threads)
     B = w.get("cpu_batch", w["batch"])
     p = R.init_params(w["items"], E, w["latent"], w["hidden"], seed=0)
     state = {}
     rng = np.random.default_rng(0)
     order = rng.permutation(X.shape[0])
+    t_load = t_step = 0.0
 
-    def one(i):
+    def one(i, timed):
+        nonlocal t_load, t_step
+        t0 = time.perf_counter()
         rows = order[(i * B) % (len(order) - B):][:B]
         x = torch.stack([torch.FloatTensor(X[int(u)].toarray().flatten()) for u in rows])
+        t1 = time.perf_counter()
         enc = [(torch.rand(B, h) >= w["dropout"]).float() / (1 - w["dropout"]) for h in w["hidden"]]
         proj = (torch.rand(B, w["d"]) >= w["dropout"]).float() / (1 - w["dropout"])
         eps = torch.randn(B, w["latent"])
         R.train_step(p, state, x, w["beta"], lr=w["lr"], enc_masks=enc, proj_mask=proj, eps=eps)
+        t2 = time.perf_counter()
+        if timed:
+            t_load += t1 - t0
+            t_step += t2 - t1
 
-    for i in range(2):
-        one(i)
+    warm = 1 if B * w["items"] > 1e8 else 2  # the Syn-10M shape takes seconds per step
+    for i in range(warm):
+        one(i, False)
     n, t0 = 0, time.perf_counter()
     while True:
-        one(n + 2)
+        one(n + warm, True)
         n += 1
         el = time.perf_counter() - t0
         if (el >= seconds and n >= 3) or n >= 5000:
             break
-    return {"value": round(n * B / el, 2), "unit": "users/s", "cores": threads, "kind": "port",
+    return {"value": round(n * B / (t_load + t_step), 2), "unit": "users/s", "cores": threads, "kind": "port",
+            "step_only": round(n * B / t_step, 2), "loader_only": round(n * B / t_load, 2),
+            "cpu_model": model, "host_cpus_usable": cores,
             "sample": f"{n} steps x {B} users of the same synthetic workload (per-row densifying loader + "
-                      f"fwd/bwd/clip/Adam), {el:.1f} s, torch fp32 on CPU"}
+                      f"fwd/bwd/clip/Adam in series), {el:.1f} s, torch fp32 on {threads} CPU threads"}
+
+
+# kernel families the library's probe can bracket (ProbeScope names in csrc/)
+FAMILIES = ("decoder_sweep", "decoder_finalize", "gemm", "adam_rows", "adam_catchup", "encoder_fwd", "ln_bwd",
+            "rowgrad_plan", "rowgrad_apply", "clip")
+
+
+def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int, kernels: dict) -> dict:
+    """Algorithmic work per launch and the bound each family is measured against.
+
+    decoder_sweep: 4 B N D flop (S = U E^T and O = P E; no dE, E is frozen), MFMA-bound when those flops take
+      longer at peak than reading E once (2 B, 1 B or 4 B per element) takes at 8 TB/s, HBM-bound otherwise.
+    gemm: the exact-fp32 MFMA GEMMs of the step: heads, projection forward, and their data and weight
+      gradients, 6 B (2 L H + d L + d^2) flop per step, split evenly over the launches per step.
+    adam_rows (lazy exact Adam): p, m, v (24 B per element) of the batch's unique W1t rows and of the 1/8 of
+      W1t rows the rotating g = 0 sweep brings up to date (plus 8 B per swept row), and p, m, v, g (28 B) of
+      the small dense parameters; with HVAE_DENSE_ADAM=1 all N rows.
+    encoder_fwd: the gathered W1t rows (nnz H 4 B) + h, xhat (B H 8 B) written.
+    decoder_finalize: split partials read (splits B (D + 2) 4 B), the batch's fp32 E rows (nnz D 4 B), dU written.
+    """
+    N, H, D, Lt = w["items"], w["hidden"][0], w["d"], w["latent"]
+    uniq, nnz = batch_stats(X, users, B, gen_seed=rank)
+    out = {}
+
+    def put(name, bound, alg, peak, unit, **extra):
+        t, n = kernels[name]
+        if t <= 0 or n <= 0:
+            return
+        ach = alg / t / (1e12 if unit == "TFLOP/s" else 1e9)
+        out[name] = {"bound": bound, "achieved": ach, "peak": peak, "unit": unit, "alg_per_launch": alg,
+                     "avg_launch_us": t * 1e6, **extra}
+
+    dec_flops = 4.0 * B * N * D
+    dec_bytes = {"bf16": 2.0, "fp8": 1.0, "fp32": 4.0}[precision] * N * D + 8.0 * B * D
+    dec_peak = {"bf16": PEAK_BF16_TFLOPS, "fp8": PEAK_FP8_TFLOPS, "fp32": PEAK_F32_TFLOPS}[precision]
+    if dec_flops / (dec_peak * 1e12) >= dec_bytes / (PEAK_HBM_GBS * 1e9):
+        put("decoder_sweep", "mfma", dec_flops, dec_peak, "TFLOP/s")
+    else:
+        put("decoder_sweep", "hbm", dec_bytes, PEAK_HBM_GBS, "GB/s",
+            tflops=round(dec_flops / kernels["decoder_sweep"][0] / 1e12, 3) if kernels["decoder_sweep"][0] else None)
+    n_gemm = max(kernels["gemm"][1], 1)
+    gemm_flops = 6.0 * B * (2 * Lt * H + (D * Lt + D * D if Lt != D else 0))
+    for k in range(1, len(w["hidden"])):
+        gemm_flops += 6.0 * B * w["hidden"][k] * w["hidden"][k - 1]
+    put("gemm", "mfma", gemm_flops / n_gemm, PEAK_F32_TFLOPS, "TFLOP/s")
+    n_small = fused.layout.n_small
+    if fused.lazy_adam:
+        swept = -(-N // 8)
+        adam_bytes = 24.0 * H * (uniq + swept) + 8.0 * swept + 28.0 * n_small
+    else:
+        adam_bytes = 24.0 * N * H + 4.0 * N + 28.0 * n_small
+    put("adam_rows", "hbm", adam_bytes, PEAK_HBM_GBS, "GB/s")
+    put("encoder_fwd", "hbm", 4.0 * nnz * H + 8.0 * B * H, PEAK_HBM_GBS, "GB/s")
+    return out
 
 
 def main():
@@ -125,7 +217,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--workload", default="all_beauty", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="syn10m", choices=sorted(WORKLOADS))
     ap.add_argument("--batch-size", type=int, default=None)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "fp32"])
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -194,11 +286,12 @@ def main():
     ms = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
-    # ---- live per-kernel timing: libhvae brackets each launch of the armed kernel with a hipEvent pair
-    # recorded on the stream the kernel runs on (eager steps of the same workload, after the timed region)
+    # ---- live per-kernel timing: libhvae brackets each launch of the armed kernel family with a hipEvent pair
+    # recorded on the stream it runs on (eager steps of the same workload, after the timed region)
     import ctypes as C
     from hvae._lib import check, lib
-    N, H, D = w["items"], w["hidden"][0], w["d"]
+    from hvae.provenance import kernel_source_digest
+    N, H, D, Lt = w["items"], w["hidden"][0], w["d"], w["latent"]
     fused.use_graphs = False
 
     def probe(name):
@@ -210,54 +303,33 @@ def main():
         check(lib().hvae_probe_arm(None, 0), "probe_disarm")
         return avg.value * 1e-6, n.value // args.probe_steps
 
-    kernels = {name: probe(name) for name in ("adam_rows", "decoder_sweep", "decoder_finalize", "encoder_fwd",
-                                             "gemm", "ln_bwd")}
+    kernels = {name: probe(name) for name in FAMILIES}
     fused.use_graphs = True
-    # Algorithmic bytes / flops per launch:
-    #  adam_rows: the lazy exact Adam (hvae_adam_lazy) reads+writes p, m, v (24 B per element) of the batch's
-    #    unique W1t rows and of the 1/8 of W1t rows its rotating g = 0 sweep brings up to date (plus 4 B of
-    #    slot lookup and 4 B of step stamp per swept row), and p, m, v, g (28 B) of the dense small params;
-    #    with HVAE_DENSE_ADAM=1 (dense torch semantics every step) all N rows.
-    #  decoder_sweep: 4 B N D flops (S = U E^T, O = P E); bytes = E read once (bf16 2 B, fp8 1 B, fp32 4 B per
-    #    element) + U read + O written.
-    uniq = mean_unique_items(X, users, B, gen_seed=rank)
-    n_small = fused.layout.n_small
-    if fused.lazy_adam:
-        swept = -(-N // 8)
-        adam_bytes = 24.0 * H * (uniq + swept) + 8.0 * swept + 28.0 * n_small
-    else:
-        adam_bytes = 24.0 * N * H + 4.0 * N + 28.0 * n_small
-    dec_flops = 4.0 * B * N * D
-    dec_bytes = {"bf16": 2.0, "fp8": 1.0, "fp32": 4.0}[args.precision] * N * D + 8.0 * B * D
-    dec_peak = {"bf16": PEAK_BF16_TFLOPS, "fp8": PEAK_FP8_TFLOPS, "fp32": PEAK_F32_TFLOPS}[args.precision]
-    t_adam, t_dec = kernels["adam_rows"][0], kernels["decoder_sweep"][0]
-    roof = {
-        "adam_rows": {"bound": "hbm", "achieved": adam_bytes / t_adam / 1e9, "peak": PEAK_HBM_GBS,
-                      "unit": "GB/s", "alg_per_launch": adam_bytes, "avg_launch_us": t_adam * 1e6},
-    }
-    # the decoder is MFMA-bound when its flops take longer at peak than its bytes do (large batches),
-    # HBM-bound otherwise (All_Beauty's B = 64: 128 flop per byte of E, under the ~310 ridge)
-    if dec_flops / (dec_peak * 1e12) >= dec_bytes / (PEAK_HBM_GBS * 1e9):
-        roof["decoder_sweep"] = {"bound": "mfma", "achieved": dec_flops / t_dec / 1e12, "peak": dec_peak,
-                                 "unit": "TFLOP/s", "alg_per_launch": dec_flops, "avg_launch_us": t_dec * 1e6}
-    else:
-        roof["decoder_sweep"] = {"bound": "hbm", "achieved": dec_bytes / t_dec / 1e9, "peak": PEAK_HBM_GBS,
-                                 "unit": "GB/s", "alg_per_launch": dec_bytes, "avg_launch_us": t_dec * 1e6,
-                                 "tflops": dec_flops / t_dec / 1e12}
-    dom = max(roof, key=lambda k: kernels[k][0])
+    roof = roofline_models(w, args.precision, B, fused, X, users, rank, kernels)
+    # the dominant kernel family: the largest per-step total (average launch x launches per step) among the
+    # families with an algorithmic model
+    dom = max(roof, key=lambda k: kernels[k][0] * max(kernels[k][1], 1))
     r = roof[dom]
-    traffic = None
+    traffic, stale = None, None
     pmc = ROOT / "profiles" / (f"pmc_{args.workload}.json" if args.precision == "bf16"
                                else f"pmc_{args.workload}_{args.precision}.json")
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get(dom, {}).get("hbm_bytes_per_launch")
+            doc = json.loads(pmc.read_text())
+            if doc.get("src_sha") == kernel_source_digest():
+                traffic = doc.get(dom, {}).get("hbm_bytes_per_launch")
+            else:  # measured on other kernel sources: refuse it
+                stale = {"pmc_src_sha": doc.get("src_sha"), "tree_src_sha": kernel_source_digest()}
         except (ValueError, OSError):
             traffic = None
     roofline = {"bound": r["bound"], "achieved": round(r["achieved"], 2), "peak": r["peak"], "unit": r["unit"],
                 "frac": round(r["achieved"] / r["peak"], 4), "traffic": traffic, "kernel": dom,
-                "avg_launch_us": round(r["avg_launch_us"], 2)}
-    launch_us = {k: {"avg_us": round(v[0] * 1e6, 2), "launches_per_step": v[1]} for k, v in kernels.items()}
+                "avg_launch_us": round(r["avg_launch_us"], 2),
+                "alg_per_launch": r["alg_per_launch"]}
+    if stale:
+        roofline["traffic_stale"] = stale
+    launch_us = {k: {"avg_us": round(v[0] * 1e6, 2), "launches_per_step": v[1],
+                     "us_per_step": round(v[0] * 1e6 * v[1], 2)} for k, v in kernels.items()}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -283,6 +355,7 @@ def main():
             "roofline": roofline,
             "kernels": {k: {kk: (round(vv, 3) if isinstance(vv, float) else vv) for kk, vv in v.items()}
                         for k, v in roof.items()},
+            "src_sha": kernel_source_digest(),
             "launch_us": launch_us,
             "cpu_baseline": cpu,
         }

@@ -34,7 +34,13 @@ def per_kernel(d, counter):
 def main():
     wl, fdir, wdir = sys.argv[1:4]
     fetch, write = per_kernel(fdir, "FETCH_SIZE"), per_kernel(wdir, "WRITE_SIZE")
-    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes); FETCH_SIZE x2 (gfx950)"}
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "recommendation-system_amd"))
+    from hvae.provenance import kernel_source_digest
+    import subprocess
+    head = subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip()
+    out = {"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes); FETCH_SIZE x2 (gfx950)",
+           # bench.py reports this file's traffic only while the kernel sources hash to src_sha
+           "src_sha": kernel_source_digest(), "measured_at_commit": head or None}
     for spec in sys.argv[4:]:
         rx, name = spec.split("=")
         fv = [v for k, vs in fetch.items() if re.search(rx, k) for v in vs]
