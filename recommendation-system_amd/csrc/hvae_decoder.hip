@@ -348,6 +348,11 @@ constexpr float kLog2e = 1.4426950408889634f;
 #ifndef DEC2_G2_AHEAD
 #define DEC2_G2_AHEAD 1
 #endif
+// Timing ablations of the sweep (A/B builds only, results invalid): 1 = no LDS-DMA in the loop and no
+// vmcnt waits, 2 = DMA issued but never waited for, 3 = no exponentials, 4 = no DS = 2 partial-S exchange
+#ifndef DEC2_ABL
+#define DEC2_ABL 0
+#endif
 // a split's ltot below e^-60 means its max term lost precision (see k_dec2_bf16)
 constexpr float kMinL = 8.75651e-27f;
 
@@ -599,13 +604,14 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   float bound = 0.f;
   if (t_beg < t_end && wave_active) {
     s_cur = gemm1(lds, [](int) {});
-    if (DS == 2) xput((int)(t_beg & 1), s_cur);
+    if (DS == 2 && DEC2_ABL != 4) xput((int)(t_beg & 1), s_cur);
   }
   bound = sqrtf(usq) * emax * 1.02f;
 
   for (int64_t t = t_beg; t < t_end; ++t) {
     const bool more = t + 1 < t_end;
-    if (NS >= 3) wait_vmcnt<(NS >= 3 ? NS - 3 : 0) * PW>();
+    if (DEC2_ABL == 1 || DEC2_ABL == 2) {
+    } else if (NS >= 3) wait_vmcnt<(NS >= 3 ? NS - 3 : 0) * PW>();
     else wait_vmcnt<0>();
     lds_fence();
     __builtin_amdgcn_s_barrier();
@@ -618,15 +624,15 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
     // transposed reads, 580 -> 610 us; after GEMM2's issue, 589 -> 597 us).
     const int64_t t_dma = min(t + NS - 1, t_end - 1);
     const int s_dma = cur == 0 ? NS - 1 : cur - 1;
-    if (NS >= 3 && (!kSpread || !wave_active)) issue(t_dma, s_dma);  // idle waves still load their share
-    if constexpr (DS == 2 && XB == 1) {  // single exchange buffer: everyone has read S(t) before S(t+1) lands
+    if (DEC2_ABL != 1 && NS >= 3 && (!kSpread || !wave_active)) issue(t_dma, s_dma);  // idle waves load too
+    if constexpr (DS == 2 && XB == 1 && DEC2_ABL != 4) {  // single exchange buffer: everyone has read S(t) before S(t+1) lands
       if (wave_active) xadd((int)(t & 1), s_cur);
       lds_fence();
       __builtin_amdgcn_s_barrier();
       lds_fence();
     }
     if (wave_active) {
-      if (DS == 2 && XB == 2) xadd((int)(t & 1), s_cur);
+      if (DS == 2 && XB == 2 && DEC2_ABL != 4) xadd((int)(t & 1), s_cur);
       if (t == ntiles - 1 && (N % kBfTI) != 0) {  // rows past N (read as 0) leave the softmax
         const int lim = (int)(N - t * kBfTI) - 4 * h;  // rows of this lane's half at or past it are tail
 #pragma unroll
@@ -651,7 +657,8 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
       auto smax_rows = [&](int r0, int r1) {
 #pragma unroll
         for (int r = r0; r < r1; ++r) {
-          pv[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_cur[r], kLog2e, -mL));
+          pv[r] = DEC2_ABL == 3 ? __builtin_fmaf(s_cur[r], kLog2e, -mL)
+                                : __builtin_amdgcn_exp2f(__builtin_fmaf(s_cur[r], kLog2e, -mL));
           lsum += pv[r];
           if (r & 1) pk[r >> 1] = pack_bf16x2(pv[r - 1], pv[r]);
         }
@@ -662,9 +669,10 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
       constexpr int NG = KS / 2;
       f32x16 s_nx = gemm1(lds + nxt * TB, [&](int g) {
         smax_rows(16 * g / NG, 16 * (g + 1) / NG);
-        if (kSpread && PW * g / NG < PW * (g + 1) / NG) issue_range(t_dma, s_dma, PW * g / NG, PW * (g + 1) / NG);
+        if (DEC2_ABL != 1 && kSpread && PW * g / NG < PW * (g + 1) / NG)
+          issue_range(t_dma, s_dma, PW * g / NG, PW * (g + 1) / NG);
       });
-      if (DS == 2 && more) xput((int)((t + 1) & 1), s_nx);
+      if (DS == 2 && more && DEC2_ABL != 4) xput((int)((t + 1) & 1), s_nx);
       bf16x8 pf[2];
       pf[0] = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
       pf[1] = __builtin_bit_cast(bf16x8, make_uint4(pk[4], pk[5], pk[6], pk[7]));
@@ -679,6 +687,7 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
     }
     cur = nxt;
   }
+  if (DEC2_ABL == 2) wait_vmcnt<0>();
 
   if (!wave_active) return;
   const float ltot = lsum + __shfl_xor(lsum, 32, 64);

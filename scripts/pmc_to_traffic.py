@@ -1,6 +1,8 @@
 """Turn FETCH_SIZE / WRITE_SIZE passes into profiles/pmc_<workload>.json (HBM bytes per launch).
 
-    python scripts/pmc_to_traffic.py <workload> <fetch_dir> <write_dir> kernel_regex=name [...]
+    python scripts/pmc_to_traffic.py <workload> <fetch_dir> <write_dir> kernel_regex=name [...] [src_sha=<hex>]
+
+src_sha: the kernel-source digest of the tree the passes ran on (bench.py prints it; default: this tree's).
 
 FETCH_SIZE and WRITE_SIZE are in KiB. On gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane)
 coalesced streaming reads, global_load and LDS-DMA alike (MI355X_MICROARCH.md, HBM), so it is doubled;
@@ -43,6 +45,9 @@ def main():
            "src_sha": kernel_source_digest(), "measured_at_commit": head or None}
     for spec in sys.argv[4:]:
         rx, name = spec.split("=")
+        if rx == "src_sha":
+            out["src_sha"] = name
+            continue
         fv = [v for k, vs in fetch.items() if re.search(rx, k) for v in vs]
         wv = [v for k, vs in write.items() if re.search(rx, k) for v in vs]
         if not fv or not wv:

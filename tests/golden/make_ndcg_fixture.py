@@ -1,7 +1,9 @@
 """G7: NDCG@K statistical fixture from the reference's own `make train-best` / `make evaluate` path.
 
-Run in the build container (where /root/reference exists), in the background (~20 min on 6 threads):
-    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_ndcg_fixture.py [n_seeds]
+Run in the build container (where /root/reference exists), in the background (~7 min per seed on 6 threads):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_ndcg_fixture.py [n_seeds] [first_seed] [threads]
+Seeds already in ndcg_planted.json are kept: a later run with first_seed > 0 appends its seeds, so the
+fixture grows one seed at a time (each seed's run is written as soon as it finishes).
 
 The All_Beauty data cannot be fetched here, so the offline stand-in is an
 All_Beauty-shaped planted-cluster dataset (gen.synth_planted: 22,363 users x 12,101 items,
@@ -25,20 +27,36 @@ import numpy as np
 
 HERE = Path(__file__).resolve().parent
 sys.path.insert(0, str(HERE))
-from gen import PLANTED_CONFIG, write_planted_artifacts  # noqa: E402
+from gen import PLANTED_CONFIG, digest, synth_planted, write_planted_artifacts  # noqa: E402
 from make_golden import import_reference  # noqa: E402
 
 
 def main():
     import torch
     n_seeds = int(sys.argv[1]) if len(sys.argv) > 1 else 3
-    torch.set_num_threads(6)
+    first = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+    torch.set_num_threads(int(sys.argv[3]) if len(sys.argv) > 3 else 6)
     _, train_m, eval_m = import_reference()
     c = PLANTED_CONFIG
-    runs = []
+    path = HERE / "ndcg_planted.json"
+    old = json.loads(path.read_text()) if (first > 0 and path.exists()) else {"runs": []}
+    runs = [r for r in old["runs"] if r["seed"] < first]
+    tr, va, te, E, _, _ = synth_planted(**c)
+    data_digest = digest(tr["user_id"].str[1:].astype(np.int64).values, tr["asin"].str[1:].astype(np.int64).values,
+                         va["asin"].str[1:].astype(np.int64).values, te["asin"].str[1:].astype(np.int64).values, E)
+    assert old.get("data_digest", data_digest) == data_digest, "planted dataset changed since the kept seeds"
+
+    def save():
+        nd = np.array([r["metrics"]["10"]["ndcg"] for r in runs])
+        fix = {"config": c, "torch": torch.__version__, "runs": runs,
+               "ndcg10_mean": float(nd.mean()), "ndcg10_std": float(nd.std(ddof=1)) if len(nd) > 1 else 0.0,
+               "data_digest": data_digest}
+        path.write_text(json.dumps(fix, indent=1))
+        return fix
+
     with tempfile.TemporaryDirectory() as td:
         data, emb = write_planted_artifacts(td)
-        for s in range(n_seeds):
+        for s in range(first, first + n_seeds):
             out = Path(td) / f"models_{s}"
             torch.manual_seed(s)
             np.random.seed(s)
@@ -56,11 +74,8 @@ def main():
                          "metrics": {str(k): v for k, v in res.items()},
                          "val_losses": hist["val_losses"], "train_losses": hist["train_losses"]})
             print(json.dumps(runs[-1]), flush=True)
-    nd = np.array([r["metrics"]["10"]["ndcg"] for r in runs])
-    fix = {"config": c, "torch": torch.__version__, "runs": runs,
-           "ndcg10_mean": float(nd.mean()), "ndcg10_std": float(nd.std(ddof=1)) if len(nd) > 1 else 0.0}
-    (HERE / "ndcg_planted.json").write_text(json.dumps(fix, indent=1))
-    print("ndcg@10", fix["ndcg10_mean"], "+-", fix["ndcg10_std"])
+            fix = save()
+    print("ndcg@10", fix["ndcg10_mean"], "+-", fix["ndcg10_std"], "over", len(runs), "seeds")
 
 
 if __name__ == "__main__":
