@@ -725,6 +725,341 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   }
 }
 
+// ------------------------------------------------------- bf16, version 3 ---
+// D = 768 (Syn-10M), the version-2 D split with the softmax owned by halves. Version 2 at D = 768 adds the
+// pair's whole partial S^T tiles through LDS and both waves of a user group run the full softmax: its loop
+// issues ~330 non-MFMA instructions per 48 MFMAs at one wave per SIMD, and MFMA is busy 40 % of the time
+// (profiles/r02_pmc_dec2_d768.txt). Here wave (ug, dh) owns items 16 dh .. 16 dh + 15 of every tile:
+//   * it sends the partner only the half of its partial S^T the partner owns (2 KiB), completes its own half
+//     (8 values per lane), runs only those 8 exponentials (under GEMM1(t + 1)'s MFMAs) and sends its packed
+//     P half back (1 KiB): P of the 32 items = [P half of dh = 0 | P half of dh = 1], the B operands of
+//     GEMM2's two k-steps;
+//   * GEMM2(t) first runs the k-step of its own P half (12 MFMAs) while the partner's half is read, then the
+//     other (12 MFMAs), so no barrier is followed by an MFMA that waits on LDS.
+// Two barriers per tile: A publishes tile t + 1 and the partial S^T halves of t + 1; B publishes P(t).
+// The image, the LDS-DMA ring (three 48-KiB slots) and GEMM1 / GEMM2 operand reads are version 2's.
+#ifndef DEC3_G1_AHEAD
+#define DEC3_G1_AHEAD 2  // GEMM1 A operand k-groups (MFMA pairs) in flight
+#endif
+#ifndef DEC3_G2_AHEAD
+#define DEC3_G2_AHEAD 2  // GEMM2 A operand d-blocks in flight
+#endif
+__host__ __device__ constexpr int d3_lds_bytes(int D) { return 3 * ((D / 128) * 8192) + 4 * 2048 + 4 * 1024; }
+
+template <int D, bool WITH_O>
+__global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, int64_t ldu,
+                                                   const bf16_t* __restrict__ E, const float* __restrict__ e_maxnorm,
+                                                   int64_t nb, int64_t N, int splits, int64_t tiles_per_split,
+                                                   DecOut out) {
+  constexpr int DW = D / 2;             // dims owned by one wave
+  constexpr int KS = DW / 16;           // GEMM1 k-steps
+  constexpr int NG = KS / 2;            // GEMM1 MFMA pairs
+  constexpr int DB = DW / 32;           // GEMM2 d-blocks
+  constexpr int NSEG = D / 128;
+  constexpr int TB = NSEG * 8192;
+  constexpr int PW = NSEG * 8 / 4;      // 1-KiB LDS-DMA pieces per wave per tile
+  constexpr int NS = 3;
+  static_assert(D % 128 == 0 && KS % 2 == 0 && NG >= 12 && PW <= NG && d3_lds_bytes(D) <= 160 * 1024,
+                "k_dec3_bf16 shape");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  float* xs = reinterpret_cast<float*>(lds + NS * TB);                 // [4 w][2 r4][64 lane][4]: partner halves
+  uint32_t* xp = reinterpret_cast<uint32_t*>(lds + NS * TB + 4 * 2048);  // [4 w][64 lane][4]: packed P halves
+  float* xm = reinterpret_cast<float*>(xp);                            // [4 w][32]: max / sum exchange (aliases xp)
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ug = w & 1, dh = w >> 1, pw = w ^ 2;  // partner wave: same users, other D half
+  const int split = blockIdx.x % splits;
+  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 64 + ug * 32;
+  const int64_t user = u0 + col;
+  const bool wave_active = u0 < nb;
+  const int64_t ntiles = (N + kBfTI - 1) / kBfTI;
+  const int64_t t_beg = (int64_t)split * tiles_per_split;
+  const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
+  const int dbase = dh * DW;
+  const float emax = *e_maxnorm;  // before any LDS-DMA is in flight (the compiler's wait would drain them)
+
+  // U fragments (B operand of GEMM1): lane holds U[user][dbase + 16 ks + 8 h + j]; |u| over the whole row
+  uint4 uf[KS];
+  float usq = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (user < nb) {
+      a = *reinterpret_cast<const float4*>(U + user * ldu + dbase + 16 * ks + 8 * h);
+      b = *reinterpret_cast<const float4*>(U + user * ldu + dbase + 16 * ks + 8 * h + 4);
+    }
+    usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+    uf[ks] = make_uint4(pack_bf16x2(a.x, a.y), pack_bf16x2(a.z, a.w), pack_bf16x2(b.x, b.y), pack_bf16x2(b.z, b.w));
+    __builtin_amdgcn_sched_barrier(0);  // a few k-steps' loads in flight, not all 48 (register peak)
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (user < nb) {
+      const float4 a = *reinterpret_cast<const float4*>(U + user * ldu + (DW - dbase) + 16 * ks + 8 * h);
+      const float4 b = *reinterpret_cast<const float4*>(U + user * ldu + (DW - dbase) + 16 * ks + 8 * h + 4);
+      usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  usq += __shfl_xor(usq, 32, 64);
+  const float bound = sqrtf(usq) * emax * 1.02f;
+
+  // LDS-DMA into version 2's image. Piece p (1 KiB) of a tile holds rows 8 ((p >> 1) & 3) + ((lane >> 2) & 7),
+  // chunk group 2 (p & 1) + (lane >> 5) of segment p >> 3; the chunk XOR (row >> 2) & 3 depends on p only
+  // through bit 1, so two lane offsets serve every piece and the rest of the source offset is scalar.
+  int vlane[2];
+#pragma unroll
+  for (int pb = 0; pb < 2; ++pb) {
+    const int row = 8 * pb + ((lane >> 2) & 7);
+    vlane[pb] = ((lane >> 2) & 7) * (D * 2) + 64 * (lane >> 5) + 16 * ((lane & 3) ^ ((row >> 2) & 3));
+  }
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(E), (short)0, (int)(N * D * 2), 0x00020000);
+  const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
+  auto issue_range = [&](int64_t t, int slot_i, int i0, int i1) {
+    const uint32_t soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(kBfTI * D * 2)));
+    const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const int p = w * PW + i;  // wave-uniform
+      const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
+      const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
+      if (i == i0)  // soff may be fresh from v_readfirstlane: 5 wait states before a buffer op reads it
+        asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+      else
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+    }
+  };
+  auto lds_fence = [] { asm volatile("" ::: "memory"); };
+  auto barrier = [&] {  // this wave's LDS writes complete, then the workgroup barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    lds_fence();
+  };
+
+  // operand addressing (version 2): GEMM1 row reads by ks parity, GEMM2 transposed reads by j
+  const int g1 = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
+  static_assert((DW / 32) % 4 == 0, "a D half starts at a 128-column segment boundary");
+  const int cseg = (dbase / 128) << 13;  // the wave's first segment (uniform), so every other term is immediate
+  const int laneA0 = ((col >> 3) << 11) + ((col & 7) << 6) + (((0 + h) ^ ((col >> 2) & 3)) << 4);
+  const int laneA1 = ((col >> 3) << 11) + ((col & 7) << 6) + (((2 + h) ^ ((col >> 2) & 3)) << 4);
+  const int laneT0 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((0 + h) & 3)) << 4) + 8 * (pp & 1);
+  const int laneT1 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((2 + h) & 3)) << 4) + 8 * (pp & 1);
+
+  // GEMM1 partial over this wave's dims: S^T[32 items][32 users] = E_tile U^T; fill(g) after MFMA pair g
+  auto gemm1 = [&](const unsigned char* buf, auto&& fill) {
+    f32x16 s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+    const unsigned char* b0 = buf + cseg + laneA0;
+    const unsigned char* b1 = buf + cseg + laneA1;
+    auto rdA = [&](int ks) {
+      const int grp = ks >> 1;
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(((ks & 1) ? b1 : b0) + ((grp >> 2) << 13) +
+                                                                         ((grp & 3) << 9)));
+    };
+    constexpr int AH = DEC3_G1_AHEAD;
+    bf16x8 a[2 * AH];
+#pragma unroll
+    for (int j = 0; j < 2 * AH; ++j) a[j] = rdA(j);
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      const bf16x8 c0 = a[(2 * g) % (2 * AH)], c1 = a[(2 * g + 1) % (2 * AH)];
+      if (2 * g + 2 * AH < KS) {
+        a[(2 * g) % (2 * AH)] = rdA(2 * g + 2 * AH);
+        a[(2 * g + 1) % (2 * AH)] = rdA(2 * g + 2 * AH + 1);
+      }
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c0, __builtin_bit_cast(bf16x8, uf[2 * g]), s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c1, __builtin_bit_cast(bf16x8, uf[2 * g + 1]), s, 0, 0, 0);
+      fill(g);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    return s;
+  };
+  f32x16 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  // one k-step (items 16 kh .. 16 kh + 15) of GEMM2 over all d-blocks: O^T[DW][32 users] += E^T P^T
+  auto gemm2_half = [&](const unsigned char* buf, int kh, const bf16x8& pf, auto&& fill) {
+    if constexpr (WITH_O) {
+      const unsigned char* t0 = buf + cseg + laneT0 + (kh << 12);
+      const unsigned char* t1 = buf + cseg + laneT1 + (kh << 12);
+      auto rdT = [&](int db, int j) {
+        auto* p = (__attribute__((address_space(3))) s16x4*)(void*)((j ? t1 : t0) + (j << 11) + ((db >> 2) << 13) +
+                                                                     ((db & 3) << 9));
+        return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
+      };
+      // the transposed reads of a d-block go out BH d-blocks before its MFMA (one ahead left each MFMA
+      // waiting on the LDS latency right after the previous one issued)
+      constexpr int BH = DEC3_G2_AHEAD;
+      s16x4 n[BH][2];
+#pragma unroll
+      for (int j = 0; j < BH; ++j) { n[j][0] = rdT(j, 0); n[j][1] = rdT(j, 1); }
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        const s16x4 c0 = n[db % BH][0], c1 = n[db % BH][1];
+        if (db + BH < DB) { n[db % BH][0] = rdT(db + BH, 0); n[db % BH][1] = rdT(db + BH, 1); }
+        const s16x8 a = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pf, o[db], 0, 0, 0);
+        fill(db);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+  // this wave's half of a partial S^T tile: rows 8 dh .. 8 dh + 7 of the accumulator (items 16 dh ..);
+  // the partner's half goes to LDS as [r4][lane] float4
+  // (the halves are picked by value selects on the wave-uniform dh: a runtime index into the accumulator
+  // vector -- which the compiler folds such a select into -- moves it through indexed-register mode)
+  auto half_of = [&](const f32x16& s, int which, int r) {
+    float a = s[r], b = s[8 + r];
+    asm volatile("" : "+v"(a), "+v"(b));  // opaque: keeps the select from folding into an indexed extract
+    return which ? b : a;
+  };
+  auto put_half = [&](const f32x16& s) {
+    float* dst = xs + w * 512;
+#pragma unroll
+    for (int r4 = 0; r4 < 2; ++r4)
+      *reinterpret_cast<float4*>(dst + r4 * 256 + lane * 4) =
+          make_float4(half_of(s, 1 - dh, 4 * r4), half_of(s, 1 - dh, 4 * r4 + 1), half_of(s, 1 - dh, 4 * r4 + 2),
+                      half_of(s, 1 - dh, 4 * r4 + 3));
+  };
+
+  float m = 0.f, mL = 0.f, lsum = 0.f;
+  float sm[8];   // this wave's half of S^T(t): own partial, completed in GEMM1(t + 1)'s first gaps
+  float4 y0 = make_float4(0.f, 0.f, 0.f, 0.f), y1 = y0;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) sm[r] = 0.f;
+  f32x16 s_nx;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) s_nx[r] = 0.f;
+  if (t_beg < t_end) {
+    issue_range(t_beg, 0, 0, PW);
+    issue_range(min(t_beg + 1, t_end - 1), 1, 0, PW);
+    wait_vmcnt<PW>();
+  }
+  barrier();
+  if (t_beg < t_end) {
+    // first tile: whole S^T half, the pair's common fixed offset m from its max (version 2's rule), then the
+    // partner halves are zeroed so that the loop's completion step is the same for every tile
+    s_nx = gemm1(lds, [](int) {});
+    put_half(s_nx);
+    barrier();
+    float mh = -INFINITY;
+    {
+      const float* src = xs + pw * 512;
+      y0 = *reinterpret_cast<const float4*>(src + lane * 4);
+      y1 = *reinterpret_cast<const float4*>(src + 256 + lane * 4);
+      const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+#pragma unroll
+      for (int r = 0; r < 8; ++r) sm[r] = dh == 0 ? half_of(s_nx, dh, r) + yv[r] : yv[r] + half_of(s_nx, dh, r);
+      if (t_beg == ntiles - 1 && (N % kBfTI) != 0) {
+        const int lim = (int)(N - t_beg * kBfTI) - 4 * h - 16 * dh;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) sm[r] = ((r & 3) + 8 * (r >> 2) >= lim) ? -INFINITY : sm[r];
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) mh = fmaxf(mh, sm[r]);
+      mh = fmaxf(mh, __shfl_xor(mh, 32, 64));
+      if (h == 0) xm[w * 32 + col] = mh;
+    }
+    barrier();
+    {
+      m = fmaxf(fmaxf(mh, xm[pw * 32 + col]), bound - kOffsetSpan);
+      mL = m * kLog2e;
+      float* dst = xs + w * 512;
+      *reinterpret_cast<float4*>(dst + lane * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(dst + 256 + lane * 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    barrier();  // the max exchange is read (xm aliases the P buffers) and the zeroed halves are published
+  }
+
+  int cur = 0;
+  for (int64_t t = t_beg; t < t_end; ++t) {
+    // [A(t)]: tile t + 1 has landed; the partner's partial half of S^T(t) is published
+    wait_vmcnt<0>();
+    barrier();
+    const int nxt = cur == NS - 1 ? 0 : cur + 1;
+    const int64_t t_dma = min(t + 2, t_end - 1);
+    const int s_dma = cur == 0 ? NS - 1 : cur - 1;
+    {
+      // every wave runs the same body (a wave past nb computes on zero rows): a branch around it splits the
+      // loop-carried O accumulators between register classes
+      // GEMM1(t + 1) (on a stale slot after the last tile: one code path, result unused); in its gaps: the
+      // completion of S^T(t)'s own half, the tail mask, the 8 exponentials of tile t, the LDS-DMA of t + 2
+      float pv[8];
+      uint32_t pk[4];
+      const bool tail = t == ntiles - 1 && (N % kBfTI) != 0;  // wave-uniform
+      f32x16 s_new = gemm1(lds + nxt * TB, [&](int g) {
+        if (g == 0) {
+          const float* src = xs + pw * 512;
+          y0 = *reinterpret_cast<const float4*>(src + lane * 4);
+          y1 = *reinterpret_cast<const float4*>(src + 256 + lane * 4);
+        } else if (g == 1) {
+          const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+#pragma unroll
+          for (int r = 0; r < 8; ++r) sm[r] = dh == 0 ? sm[r] + yv[r] : yv[r] + sm[r];
+          if (__builtin_expect(tail, 0)) {  // rows past N (read as 0) leave the softmax
+            const int lim = (int)(N - t * kBfTI) - 4 * h - 16 * dh;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) sm[r] = ((r & 3) + 8 * (r >> 2) >= lim) ? -INFINITY : sm[r];
+          }
+        } else if (g >= 2 && g < 10) {
+          const int r = g - 2;
+          pv[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sm[r], kLog2e, -mL));
+          lsum += pv[r];
+          if (r & 1) pk[r >> 1] = pack_bf16x2(pv[r - 1], pv[r]);
+        }
+        if (g < PW) issue_range(t_dma, s_dma, g, g + 1);
+      });
+      // P(t) own half out; [B(t)]; the partner's partial half of S^T(t + 1) out; GEMM2(t), own half first
+      *reinterpret_cast<uint4*>(xp + (w * 64 + lane) * 4) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      barrier();
+      put_half(s_new);
+      const bf16x8 pown = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+      uint4 po = make_uint4(0u, 0u, 0u, 0u);
+      gemm2_half(lds + cur * TB, dh, pown, [&](int db) {
+        if (db == 0) po = *reinterpret_cast<const uint4*>(xp + (pw * 64 + lane) * 4);
+      });
+      gemm2_half(lds + cur * TB, 1 - dh, __builtin_bit_cast(bf16x8, po), [](int) {});
+#pragma unroll
+      for (int r = 0; r < 8; ++r) sm[r] = half_of(s_new, dh, r);
+    }
+    cur = nxt;
+  }
+  wait_vmcnt<0>();  // the last tile's LDS-DMA (a duplicate, never read) lands before the ring is released
+
+  // l = (own items) + (partner's items), the same sum in both waves
+  lsum += __shfl_xor(lsum, 32, 64);
+  barrier();  // every wave is past its last read of the P buffers (xm aliases them)
+  if (h == 0) xm[w * 32 + col] = lsum;
+  barrier();
+  if (!wave_active || t_beg >= t_end || user >= nb) return;
+  const float lo = xm[pw * 32 + col];
+  const float ltot = dh == 0 ? lsum + lo : lo + lsum;
+  if (h == 0 && dh == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
+  const int64_t row = out.direct ? user : (int64_t)split * nb + user;
+  if (h == 0 && dh == 0) {
+    if (out.direct) out.lse[user] = m + logf(ltot);
+    else { out.m[row] = m; out.l[row] = ltot; }
+  }
+  if (WITH_O) {
+    const float sc = out.direct ? 1.0f / ltot : 1.0f;
+#pragma unroll
+    for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
+        *reinterpret_cast<float4*>(out.O + row * D + dd) =
+            make_float4(o[d][4 * g4] * sc, o[d][4 * g4 + 1] * sc, o[d][4 * g4 + 2] * sc, o[d][4 * g4 + 3] * sc);
+      }
+  }
+}
+
 // ------------------------------------------------------------------- fp8 ---
 // The same sweep on the block-scaled fp8 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, OCP e4m3 operands,
 // twice the bf16 rate; BASELINE configs[4]). Both products carry exact power-of-two scales:
@@ -1796,6 +2131,7 @@ struct DecPlan {
   int64_t blocks;
   size_t lds;
   int v2;    // bf16 version-2 sweep (k_dec2_bf16)
+  int v3;    // bf16 version-3 sweep (k_dec3_bf16, D = 768)
   int ds;    // its D split (1 or 2)
   int nw;    // its waves per block (4, or 8 with ds = 2)
   int64_t upb;
@@ -1812,10 +2148,7 @@ static bool dec_use_v1() {
   static const int v = env_int("HVAE_DEC_V1", 0);
   return v != 0;
 }
-static int dec_forced_splits() {
-  static const int v = env_int("HVAE_DEC_SPLITS", 0);
-  return v;
-}
+static int dec_forced_splits() { return env_int("HVAE_DEC_SPLITS", 0); }  // read at every plan (A/B)
 
 static int dec_forced_ds() {
   static const int v = env_int("HVAE_DEC_DS", 0);
@@ -1828,6 +2161,8 @@ static int dec_forced_nw() {
 }
 
 static bool v2_supported(int64_t D) { return D == 64 || D == 128 || D == 256 || D == 384 || D == 768; }
+// HVAE_DEC_V3=0 keeps the version-2 sweep at D = 768 (A/B; read at every plan, so a test can switch it)
+static bool v3_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V3", 1) != 0; }
 
 static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
   s = std::max<int64_t>(1, std::min<int64_t>(s, std::min<int64_t>(tiles, kMaxSplits)));
@@ -1853,11 +2188,12 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   }
   const bool bf = dtype == HVAE_BF16;
   p.v2 = bf && !dec_use_v1() && v2_supported(D);
+  p.v3 = p.v2 && v3_supported(D);
   p.ds = p.v2 && (D > 384 || nb <= 64) ? 2 : 1;
   if (p.v2 && D <= 384 && (dec_forced_ds() == 1 || dec_forced_ds() == 2)) p.ds = dec_forced_ds();
   p.nw = p.v2 && p.ds == 2 && nb > 64 && D <= 384 ? 8 : 4;
   if (p.v2 && p.ds == 2 && D <= 384 && (dec_forced_nw() == 4 || dec_forced_nw() == 8)) p.nw = dec_forced_nw();
-  p.upb = bf ? (p.v2 ? 32 * p.nw / p.ds : kBfUsersPerBlock) : kF32UsersPerBlock;
+  p.upb = bf ? (p.v3 ? 64 : p.v2 ? 32 * p.nw / p.ds : kBfUsersPerBlock) : kF32UsersPerBlock;
   const int64_t ti = bf ? kBfTI : kF32TI;
   const int64_t target = bf ? 256 : 512;
   const int64_t nub = cdiv(nb, p.upb), tiles = cdiv(N, ti);
@@ -1928,6 +2264,22 @@ static int launch_bf16_v2(const float* U, int64_t ldu, const void* E, const floa
 }
 
 template <int D, bool WO>
+static int launch_bf16_v3(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                          const DecPlan& p, DecOut o, hipStream_t st) {
+  constexpr int lds = d3_lds_bytes(D);
+  static_assert(lds <= 160 * 1024, "k_dec3_bf16 LDS");
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec3_bf16<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr_set = true;
+  }
+  k_dec3_bf16<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N, p.splits,
+                                                          p.tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec3_bf16");
+  return HVAE_OK;
+}
+
+template <int D, bool WO>
 static int launch_fp8(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                       const DecPlan& p, DecOut o, hipStream_t st) {
   constexpr int DS = D > 384 ? 2 : 1;
@@ -1971,6 +2323,8 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
       case 768: return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       default: break;
     }
+  } else if (dtype == HVAE_BF16 && p.v3 && D == 768) {
+    return launch_bf16_v3<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
   } else if (dtype == HVAE_BF16 && p.v2) {
     if (p.ds == 1) {
       switch (D) {

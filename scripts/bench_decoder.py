@@ -31,6 +31,10 @@ def main():
     ap.add_argument("--train", action="store_true", help="time hvae_decoder_train (sweep + finalize with the CSR "
                                                           "batch's sparse terms) instead of hvae_decoder_fwd")
     ap.add_argument("--probe", default="decoder_sweep", choices=["decoder_sweep", "decoder_finalize"])
+    ap.add_argument("--ab", nargs="*", default=[], help="A/B arms in one process: each arm a comma list of "
+                    "ENV=VAL settings read by the library at plan time (e.g. HVAE_DEC_V3=0), timed in "
+                    "interleaved rounds")
+    ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -50,20 +54,33 @@ def main():
         step = lambda: ops.decoder_train(x, U, E, enorm, E32, 1.0 / args.nb)  # noqa: E731
     else:
         step = lambda: ops.decoder_fwd(U, E, enorm)  # noqa: E731
-    step()  # warm-up (and kernel attributes)
-    torch.cuda.synchronize()
-    check(lib().hvae_probe_arm(args.probe.encode(), 4 * args.reps), "probe_arm")
-    for _ in range(args.reps):
-        step()
-    torch.cuda.synchronize()
-    avg, n = C.c_double(), C.c_int()
-    check(lib().hvae_probe_collect(C.byref(avg), C.byref(n)), "probe_collect")
-    check(lib().hvae_probe_arm(None, 0), "probe_disarm")
-    us = avg.value
-    flops = 4.0 * args.nb * args.N * args.D
-    print(json.dumps({"nb": args.nb, "N": args.N, "D": args.D, "dtype": args.dtype, "probe": args.probe,
-                      "launches": n.value,
-                      "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 1)}), flush=True)
+    import os
+
+    def timed(label):
+        step()  # warm-up (and kernel attributes)
+        torch.cuda.synchronize()
+        check(lib().hvae_probe_arm(args.probe.encode(), 4 * args.reps), "probe_arm")
+        for _ in range(args.reps):
+            step()
+        torch.cuda.synchronize()
+        avg, n = C.c_double(), C.c_int()
+        check(lib().hvae_probe_collect(C.byref(avg), C.byref(n)), "probe_collect")
+        check(lib().hvae_probe_arm(None, 0), "probe_disarm")
+        us = avg.value
+        flops = 4.0 * args.nb * args.N * args.D
+        print(json.dumps({"nb": args.nb, "N": args.N, "D": args.D, "dtype": args.dtype, "probe": args.probe,
+                          "arm": label, "launches": n.value,
+                          "avg_us": round(us, 2), "tflops": round(flops / us / 1e6, 1)}), flush=True)
+
+    if not args.ab:
+        timed("")
+        return
+    for _ in range(args.rounds):
+        for arm in args.ab:
+            for kv in arm.split(","):
+                k, v = kv.split("=")
+                os.environ[k] = v
+            timed(arm)
 
 
 if __name__ == "__main__":

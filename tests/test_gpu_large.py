@@ -1,0 +1,193 @@
+"""Parity at the BASELINE configs' full shapes, through the C ABI (hvae_decoder_train).
+
+configs[2]  Syn-1M: 4096 users x 100,000 items, d = 384 (bf16 and fp8);
+configs[3]  Syn-10M, one GPU's step: 4096 users x 1,000,000 items, d = 768 (bf16) -- the 1.5 GB bf16 image
+            puts the 32-bit buffer extent N d 2 = 1.536e9 of the LDS-DMA resource to the test;
+configs[4]  the same shape on the fp8 sweep.
+At these sizes the float64 reference of the scores (the reference's u E^T, src/ml/model.py:198, and its
+log-softmax loss, :281) runs on a seeded sample of 64 users of each batch (first and last included), on the
+device, over all N items, with the decoder operands rounded as the kernel rounds them (bf16; or e4m3 with
+the kernel's power-of-two scales). Checked per sampled user: lse, O = softmax(S) E, the loss row
+n_b lse_b - u_b . sum_j x_bj E_j and d(u) = (n_b O_b - sum_j x_bj E_j) / B (fp32 E and u for the sparse terms,
+as hvae_decoder.hip's finalize).
+
+Also: 64 users x 1M items (256 item splits: the grouped split merge), users whose |u| forces the flagged
+exact recompute at d = 768, version 3 of the d = 768 sweep against version 2 (HVAE_DEC_V3=0), and one fused
+Syn-1M-shaped train step whose exact lazy Adam stays bitwise equal to the dense update over 3 replays.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gen import synth_csr
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops(hip_device):
+    from hvae import ops
+    return ops
+
+
+def _maxrel(a, b):
+    a = a.detach().double()
+    b = b.detach().double().to(a.device)
+    return float((a - b).abs().max() / max(b.abs().max().item(), 1e-30))
+
+
+def _pow2_exp(amax: torch.Tensor) -> torch.Tensor:
+    _, e = torch.frexp(amax)
+    return torch.where(amax > 0, torch.clamp(8 - e, max=127), torch.zeros_like(e))
+
+
+def _q8(x: torch.Tensor, k: torch.Tensor) -> torch.Tensor:
+    s = torch.ldexp(torch.ones_like(x), k.to(x.dtype).expand_as(x))
+    return (x * s).to(torch.float8_e4m3fn).float() / s
+
+
+def _inputs(dev, nb, N, D, seed, unorm=4.0):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    E = torch.randn(N, D, device=dev, generator=g)
+    E /= E.norm(dim=1, keepdim=True)
+    U = torch.randn(nb, D, device=dev, generator=g)
+    U *= unorm / U.norm(dim=1, keepdim=True)  # |u| of trained projections (bench_decoder.py)
+    return E, U
+
+
+def _reference(Ur, Er, U32, E32, x, idx, scale):
+    """float64 lse, O, loss rows, d(u) for users idx (rows of x), items chunked so S stays ~0.5 GB."""
+    Ur, Er = Ur[idx].double(), Er.double()
+    N = Er.shape[0]
+    m = torch.full((len(idx),), -float("inf"), dtype=torch.float64, device=Ur.device)
+    chunk = 1 << 20
+    for c0 in range(0, N, chunk):
+        m = torch.maximum(m, (Ur @ Er[c0:c0 + chunk].t()).amax(1))
+    l = torch.zeros_like(m)
+    O = torch.zeros(len(idx), Er.shape[1], dtype=torch.float64, device=Ur.device)
+    Oa = torch.zeros_like(O)  # softmax(S) |E|: the scale of O's e4m3 rounding envelope
+    for c0 in range(0, N, chunk):
+        p = torch.exp(Ur @ Er[c0:c0 + chunk].t() - m[:, None])
+        l += p.sum(1)
+        O += p @ Er[c0:c0 + chunk]
+        Oa += p @ Er[c0:c0 + chunk].abs()
+    lse = m + torch.log(l)
+    O /= l[:, None]
+    Oa /= l[:, None]
+    xs = torch.as_tensor(x[idx.cpu().numpy()].toarray(), dtype=torch.float64, device=Ur.device)
+    n = xs.sum(1)
+    xE = xs @ E32.double()
+    rr = n * lse - (U32[idx].double() * xE).sum(1)
+    dU = scale * (n[:, None] * O - xE)
+    return lse, O, rr, dU, Oa
+
+
+def _sample(nb, k=64, seed=0):
+    rng = np.random.default_rng(seed)
+    idx = np.unique(np.concatenate([[0, nb - 1], rng.choice(nb, size=min(k, nb) - 2, replace=False)]))
+    return torch.as_tensor(idx)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("nb,N,D", [(4096, 100_000, 384), (4096, 1_000_000, 768), (64, 1_000_000, 768)])
+def test_decoder_train_full_shape(ops, hip_device, dtype, nb, N, D):
+    from hvae import _lib
+    E, U = _inputs(hip_device, nb, N, D, seed=N + D + nb)
+    X = synth_csr(nb, N, lam=15.0, seed=D)
+    xd = ops.csr_from_scipy(X, hip_device)
+    img = ops.decoder_image(E, _lib.HVAE_FP8 if dtype == "fp8" else _lib.HVAE_BF16)
+    enorm = ops.row_norm_max(img)
+    lse, O, rr, dU = ops.decoder_train(xd, U, img, enorm, E, 1.0 / nb, want_o=True)
+    torch.cuda.synchronize()
+    assert torch.isfinite(lse).all() and torch.isfinite(O).all() and torch.isfinite(dU).all()
+    idx = _sample(nb).to(hip_device)
+    if dtype == "bf16":
+        Ur, Er = U.bfloat16().float(), img.bf16.float()
+    else:
+        ke = _pow2_exp(E.abs().max())
+        Ur, Er = _q8(U, _pow2_exp(U.abs().amax(1, keepdim=True))), _q8(E, ke)
+    lse_r, O_r, rr_r, dU_r, Oa_r = _reference(Ur, Er, U, E, X, idx, 1.0 / nb)
+    emax = Er.abs().max().item()
+    del Er
+    # lse: fp32 sums of N exponentials of exact-offset scores; O: P rounded to bf16 / e4m3 in GEMM2
+    assert (lse[idx].double() - lse_r).abs().max() < 2e-4 * lse_r.abs().max().clamp(min=1)
+    if dtype == "bf16":
+        assert _maxrel(O[idx], O_r) < 1e-2
+    else:  # e4m3 P: every element inside the rounding envelope of test_gpu_fp8.py
+        env = 2.0 ** -4 * Oa_r + 2.0 ** -11 * emax
+        assert bool(((O[idx].double() - O_r).abs() <= env).all())
+    assert _maxrel(rr[idx], rr_r) < 1e-4
+    assert _maxrel(dU[idx], dU_r) < (2e-2 if dtype == "bf16" else 1e-1)
+
+
+@pytest.mark.timeout(300)
+def test_decoder_d768_v3_matches_v2(ops, hip_device, monkeypatch):
+    """Version 3 (item-half softmax ownership) against version 2 (whole-tile softmax in both waves) of the
+    d = 768 bf16 sweep: both round the same bf16 operands; only fp32 summation order differs."""
+    nb, N, D = 700, 50_001, 768
+    E, U = _inputs(hip_device, nb, N, D, seed=11)
+    X = synth_csr(nb, N, lam=15.0, seed=3)
+    xd = ops.csr_from_scipy(X, hip_device)
+    img = ops.decoder_image(E)
+    enorm = ops.row_norm_max(img)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("HVAE_DEC_V3", v)
+        out[v] = ops.decoder_train(xd, U, img, enorm, E, 1.0 / nb, want_o=True)
+    (l3, o3, r3, d3), (l2, o2, r2, d2) = out["1"], out["0"]
+    assert (l3 - l2).abs().max() < 1e-4
+    assert _maxrel(o3, o2) < 5e-3 and _maxrel(r3, r2) < 1e-5 and _maxrel(d3, d2) < 5e-3
+
+
+@pytest.mark.timeout(300)
+def test_decoder_d768_large_norm_fixup(ops, hip_device):
+    """|u| up to 1500 at d = 768: the fixed offset underflows, the users are flagged and recomputed exactly."""
+    N, D = 4000, 768
+    E, _ = _inputs(hip_device, 1, N, D, seed=5)
+    g = torch.Generator(device=hip_device).manual_seed(1)
+    U = torch.randn(8, D, device=hip_device, generator=g)
+    U = U / U.norm(dim=1, keepdim=True) * torch.tensor([1, 10, 50, 100, 200, 400, 800, 1500.0],
+                                                       device=hip_device)[:, None]
+    img = ops.decoder_image(E)
+    lse, O = ops.decoder_fwd(U, img, ops.row_norm_max(img))
+    S = U.bfloat16().double() @ img.bf16.double().t()
+    ref = torch.logsumexp(S, 1)
+    assert torch.isfinite(lse).all() and torch.isfinite(O).all()
+    assert ((lse.double() - ref).abs() / ref.abs().clamp(min=1)).max() < 2e-3
+    assert _maxrel(O, torch.softmax(S, 1) @ img.bf16.double()) < 1e-2
+
+
+@pytest.mark.timeout(600)
+def test_fused_step_syn1m_shape_lazy_adam_bitwise(hip_device, monkeypatch):
+    """One Syn-1M-shaped configuration (B = 4096, N = 100,000, d = 384, latent 128, hidden [512]): three
+    graph-replayed train steps have finite losses, and the exact lazy Adam leaves parameters and both moments
+    bitwise equal to the dense every-row update (src/ml/train.py:92, torch.optim.Adam)."""
+    from hvae.executor import ConstBeta, FusedTrainer
+    from src.ml.model import HybridVAE
+    n_users, N, D, B = 3 * 4096 + 17, 100_000, 384, 4096
+    X = synth_csr(n_users, N, lam=15.0, seed=21)
+    g = np.random.default_rng(22)
+    E = g.standard_normal((N, D)).astype(np.float32)
+    E /= np.linalg.norm(E, axis=1, keepdims=True)
+    outs = []
+    for lazy in ("0", "1"):
+        monkeypatch.setenv("HVAE_DENSE_ADAM", "0" if lazy == "1" else "1")
+        torch.manual_seed(0)
+        model = HybridVAE(N, E, latent_dim=128, hidden_dims=[512], dropout=0.3, beta=0.2).to(hip_device)
+        fused = FusedTrainer(model, hip_device, precision="bf16", seed=99, use_graphs=True)
+        assert fused.lazy_adam == (lazy == "1")
+        data = fused.device_data(X, list(range(n_users)))
+        gen = torch.Generator().manual_seed(7)
+        r = fused.run_epoch(data, B, True, ConstBeta(0.2), 0.3, generator=gen, max_batches=3)
+        fused.flush()
+        torch.cuda.synchronize()
+        outs.append((r, fused.flat.clone(), fused.m.clone(), fused.v.clone()))
+        del model, fused, data
+        torch.cuda.empty_cache()
+    (ra, fa, ma, va), (rb, fb, mb, vb) = outs
+    assert all(np.isfinite(v) for v in ra.values())
+    assert ra == rb
+    assert torch.equal(fa, fb) and torch.equal(ma, mb) and torch.equal(va, vb)
