@@ -30,6 +30,7 @@
 //     and b+8 share one), keeping the split's E slice L2-resident; a merge
 //     kernel combines the (m, l, O) partials.
 #include <algorithm>
+#include <type_traits>
 
 #include "hvae_common.h"
 
@@ -738,6 +739,19 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
 //     other (12 MFMAs), so no barrier is followed by an MFMA that waits on LDS.
 // Two barriers per tile: A publishes tile t + 1 and the partial S^T halves of t + 1; B publishes P(t).
 // The image, the LDS-DMA ring (three 48-KiB slots) and GEMM1 / GEMM2 operand reads are version 2's.
+// timing ablations (A/B builds only, results invalid): 1 = no LDS-DMA / vmcnt waits in the loop,
+// 2 = no barriers in the loop, 3 = both, 4 = no half-S / P exchange through LDS
+#ifndef DEC3_ABL
+#define DEC3_ABL 0
+#endif
+// where a tile's LDS-DMA pieces go: 0 = one per GEMM1 MFMA pair, 1 = one per two GEMM2 MFMAs,
+// 2 = half in each
+#ifndef DEC3_DMA
+#define DEC3_DMA 0
+#endif
+#ifndef DEC3_DMA_PRE
+#define DEC3_DMA_PRE 0  // (DEC3_DMA 0) pieces issued before GEMM1's first MFMA (0, 3, 6 = 11.07, 11.13, 11.19 ms)
+#endif
 #ifndef DEC3_G1_AHEAD
 #define DEC3_G1_AHEAD 2  // GEMM1 A operand k-groups (MFMA pairs) in flight
 #endif
@@ -817,15 +831,17 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(E), (short)0, (int)(N * D * 2), 0x00020000);
   const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
-  auto issue_range = [&](int64_t t, int slot_i, int i0, int i1) {
-    const uint32_t soff = (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(kBfTI * D * 2)));
+  static_assert(PW % 2 == 0, "piece parity is compile-time");
+  // pieces [i0, i1) of tile t into ring slot slot_i; soff = the tile's byte offset, wave-uniform (readfirstlane).
+  // fresh: soff was just produced by v_readfirstlane (5 wait states before a buffer op reads it)
+  auto issue_pieces = [&](uint32_t soff, int slot_i, int i0, int i1, bool fresh) {
     const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
-      const int p = w * PW + i;  // wave-uniform
-      const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
-      const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
-      if (i == i0)  // soff may be fresh from v_readfirstlane: 5 wait states before a buffer op reads it
+      const int p = w * PW + i;  // wave-uniform; bits 0 and 1 of p are those of i (PW is even)
+      const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (i & 1));
+      const int vo = vlane[(i >> 1) & 1];
+      if (fresh && i == i0)
         asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                      :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
       else
@@ -833,6 +849,10 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
                      :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
     }
   };
+  auto tile_soff = [&](int64_t t) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(kBfTI * D * 2)));
+  };
+  auto issue_range = [&](int64_t t, int slot_i, int i0, int i1) { issue_pieces(tile_soff(t), slot_i, i0, i1, true); };
   auto lds_fence = [] { asm volatile("" ::: "memory"); };
   auto barrier = [&] {  // this wave's LDS writes complete, then the workgroup barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -850,7 +870,7 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
   const int laneT1 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((2 + h) & 3)) << 4) + 8 * (pp & 1);
 
   // GEMM1 partial over this wave's dims: S^T[32 items][32 users] = E_tile U^T; fill(g) after MFMA pair g
-  auto gemm1 = [&](const unsigned char* buf, auto&& fill) {
+  auto gemm1 = [&](const unsigned char* buf, auto&& pre, auto&& fill) {
     f32x16 s;
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
@@ -865,6 +885,8 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
     bf16x8 a[2 * AH];
 #pragma unroll
     for (int j = 0; j < 2 * AH; ++j) a[j] = rdA(j);
+    pre();  // under the first operand reads' latency
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
       const bf16x8 c0 = a[(2 * g) % (2 * AH)], c1 = a[(2 * g + 1) % (2 * AH)];
@@ -946,7 +968,7 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
   if (t_beg < t_end) {
     // first tile: whole S^T half, the pair's common fixed offset m from its max (version 2's rule), then the
     // partner halves are zeroed so that the loop's completion step is the same for every tile
-    s_nx = gemm1(lds, [](int) {});
+    s_nx = gemm1(lds, [] {}, [](int) {});
     put_half(s_nx);
     barrier();
     float mh = -INFINITY;
@@ -978,14 +1000,20 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
     barrier();  // the max exchange is read (xm aliases the P buffers) and the zeroed halves are published
   }
 
+  // the loop is instantiated per D half (dh) so that every register pick of a half is static
+  auto sweep = [&](auto dh_c) {
+  constexpr int DHC = decltype(dh_c)::value;
   int cur = 0;
   for (int64_t t = t_beg; t < t_end; ++t) {
     // [A(t)]: tile t + 1 has landed; the partner's partial half of S^T(t) is published
-    wait_vmcnt<0>();
-    barrier();
+    if (DEC3_ABL != 1 && DEC3_ABL != 3) wait_vmcnt<0>();
+    if (DEC3_ABL != 2 && DEC3_ABL != 3) barrier();
     const int nxt = cur == NS - 1 ? 0 : cur + 1;
     const int64_t t_dma = min(t + 2, t_end - 1);
     const int s_dma = cur == 0 ? NS - 1 : cur - 1;
+    const uint32_t soff_dma = tile_soff(t_dma);  // well before the first piece reads it
+    constexpr int P1 = DEC3_DMA == 0 ? PW : DEC3_DMA == 1 ? 0 : PW / 2;  // pieces under GEMM1, the rest GEMM2
+    constexpr bool kDma = DEC3_ABL != 1 && DEC3_ABL != 3;
     {
       // every wave runs the same body (a wave past nb computes on zero rows): a branch around it splits the
       // loop-carried O accumulators between register classes
@@ -994,15 +1022,17 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
       float pv[8];
       uint32_t pk[4];
       const bool tail = t == ntiles - 1 && (N % kBfTI) != 0;  // wave-uniform
-      f32x16 s_new = gemm1(lds + nxt * TB, [&](int g) {
-        if (g == 0) {
+      f32x16 s_new = gemm1(lds + nxt * TB, [&] {
+        if (kDma && DEC3_DMA == 0) issue_pieces(soff_dma, s_dma, 0, DEC3_DMA_PRE, true);
+      }, [&](int g) {
+        if (g == 0 && DEC3_ABL != 4) {
           const float* src = xs + pw * 512;
           y0 = *reinterpret_cast<const float4*>(src + lane * 4);
           y1 = *reinterpret_cast<const float4*>(src + 256 + lane * 4);
         } else if (g == 1) {
           const float yv[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
 #pragma unroll
-          for (int r = 0; r < 8; ++r) sm[r] = dh == 0 ? sm[r] + yv[r] : yv[r] + sm[r];
+          for (int r = 0; r < 8; ++r) sm[r] = DHC == 0 ? sm[r] + yv[r] : yv[r] + sm[r];
           if (__builtin_expect(tail, 0)) {  // rows past N (read as 0) leave the softmax
             const int lim = (int)(N - t * kBfTI) - 4 * h - 16 * dh;
 #pragma unroll
@@ -1014,23 +1044,41 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
           lsum += pv[r];
           if (r & 1) pk[r >> 1] = pack_bf16x2(pv[r - 1], pv[r]);
         }
-        if (g < PW) issue_range(t_dma, s_dma, g, g + 1);
+        constexpr int PRE = DEC3_DMA == 0 ? DEC3_DMA_PRE : 0;
+        if (kDma && g < P1 - PRE) issue_pieces(soff_dma, s_dma, PRE + g, PRE + g + 1, PRE == 0 && g == 0);
       });
       // P(t) own half out; [B(t)]; the partner's partial half of S^T(t + 1) out; GEMM2(t), own half first
-      *reinterpret_cast<uint4*>(xp + (w * 64 + lane) * 4) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-      barrier();
-      put_half(s_new);
+      if (DEC3_ABL != 4) *reinterpret_cast<uint4*>(xp + (w * 64 + lane) * 4) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
+      if (DEC3_ABL != 2 && DEC3_ABL != 3) barrier();
+      if (DEC3_ABL != 4) {
+        float* dst = xs + w * 512;  // the partner's half of the new partial (static registers)
+#pragma unroll
+        for (int r4 = 0; r4 < 2; ++r4) {
+          const int r = 8 * (1 - DHC) + 4 * r4;
+          *reinterpret_cast<float4*>(dst + r4 * 256 + lane * 4) =
+              make_float4(s_new[r], s_new[r + 1], s_new[r + 2], s_new[r + 3]);
+        }
+      }
       const bf16x8 pown = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
       uint4 po = make_uint4(0u, 0u, 0u, 0u);
-      gemm2_half(lds + cur * TB, dh, pown, [&](int db) {
-        if (db == 0) po = *reinterpret_cast<const uint4*>(xp + (pw * 64 + lane) * 4);
+      gemm2_half(lds + cur * TB, DHC, pown, [&](int db) {
+        if (db == 0 && DEC3_ABL != 4) po = *reinterpret_cast<const uint4*>(xp + (pw * 64 + lane) * 4);
+        if (kDma && P1 + db / 2 < PW && (db & 1) == 0)
+          issue_pieces(soff_dma, s_dma, P1 + db / 2, P1 + db / 2 + 1, false);
       });
-      gemm2_half(lds + cur * TB, 1 - dh, __builtin_bit_cast(bf16x8, po), [](int) {});
+      gemm2_half(lds + cur * TB, 1 - DHC, __builtin_bit_cast(bf16x8, po), [&](int db) {
+        const int i = P1 + (DB + db) / 2;
+        if (kDma && i < PW && (db & 1) == 0) issue_pieces(soff_dma, s_dma, i, i + 1, false);
+      });
 #pragma unroll
-      for (int r = 0; r < 8; ++r) sm[r] = half_of(s_new, dh, r);
+      for (int r = 0; r < 8; ++r) sm[r] = s_new[8 * DHC + r];
     }
     cur = nxt;
   }
+  };
+  if (dh == 0) sweep(std::integral_constant<int, 0>{});
+  else sweep(std::integral_constant<int, 1>{});
+
   wait_vmcnt<0>();  // the last tile's LDS-DMA (a duplicate, never read) lands before the ring is released
 
   // l = (own items) + (partner's items), the same sum in both waves
