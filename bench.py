@@ -69,8 +69,7 @@ def make_data(w: dict, rank: int, world: int):
         X = synth_csr(w["users"] // 8, w["items"], lam=w["lam"], seed=1000 + rank)
         return X, E, np.arange(X.shape[0])
     X = synth_csr(w["users"], w["items"], lam=w["lam"], seed=0)
-    users = np.arange(rank, w["users"], world)  # each rank owns a disjoint user shard
-    return X, E, users
+    return X, E, np.arange(X.shape[0])  # every rank holds every user and takes its slice of each global batch
 
 
 def batch_stats(X, users, B: int, gen_seed: int = 0, samples: int = 32) -> tuple[float, float]:
@@ -256,8 +255,9 @@ def main():
     fused = FusedTrainer(model, device, lr=w["lr"], precision=args.precision, seed=1234, use_graphs=True,
                          process_group=group)
     data = fused.device_data(X, users)
+    data.dp_global = world > 1 and not w.get("shard_gen")  # per-rank generated shards are already disjoint
     B = w["batch"]
-    n_per_epoch = len(users) // B
+    n_per_epoch = len(users) // (B * (world if data.dp_global else 1))
     beta = ConstBeta(w["beta"])
     gen = torch.Generator(device=device).manual_seed(rank)  # epoch orders drawn on the GPU
 

@@ -370,6 +370,15 @@ int hvae_counter_add(int64_t* counter, int64_t delta, void* stream);
 /* *a += da and, if b != NULL, *b += db, in one launch (end of a train step). */
 int hvae_counters_add(int64_t* a, int64_t da, int64_t* b, int64_t db, void* stream);
 
+/* ------------------------------------------------------- data parallel -- */
+/* No reference counterpart (the reference trainer is single-device). One rank's share of a
+ * data-parallel step: its batch x compacted into row_ptr_out[0..nb] (int32 offsets from 0; [nb] = nnz),
+ * col_out[0..cap) and vals_out[0..cap) = scale * vals. Ranks all-gather these packets with their da [nb, H]
+ * and rebuild the union batch's first-layer row gradient with hvae_w1_rowgrad (hvae/dist.py). Entries at
+ * or past cap are dropped (size cap from the host CSR: the batch's largest possible nnz). */
+int hvae_csr_batch_pack(const hvae_csr_batch* x, float scale, int32_t* row_ptr_out, int32_t* col_out,
+                        float* vals_out, int64_t cap, void* stream);
+
 /* ------------------------------------------------------------ eval (K16) -- */
 /* scores[r, c] = U[user_row[r], :] . E32[cand[r, c], :]   (fp32)
  * The 99-negative protocol of RecommendationEvaluator.evaluate_user_with_negatives

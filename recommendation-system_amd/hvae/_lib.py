@@ -130,6 +130,7 @@ SIGNATURES = {
     "hvae_rank_first": (cint, [vp, i64, i64, vp, vp]),
     "hvae_topk": (cint, [vp, i64, i64, i64, P(CsrBatch), i64, vp, vp, vp]),
     "hvae_cast_bf16": (cint, [vp, vp, i64, vp]),
+    "hvae_csr_batch_pack": (cint, [P(CsrBatch), f32, vp, vp, vp, i64, vp]),
 }
 
 _lib = None

@@ -1,38 +1,32 @@
 """User-batch data parallelism for the fused trainer (one process per GPU, RCCL over xGMI).
 
-The reference is single-device (no collectives anywhere). The
-MI355X build shards users across ranks; parameters, Adam state and the frozen
-embeddings are replicated (E is never communicated). After each rank's
-forward/backward:
+The reference is single-device (no collectives anywhere). The MI355X build shards users across
+ranks; parameters, Adam state and the frozen embeddings are replicated (E is never communicated), and one
+data-parallel step is one step of the single-GPU trainer over the UNION of the ranks' batches:
 
-  * the small dense gradients (every parameter except the first-layer
-    weight, ~0.3-0.8 M floats) are all-reduced with ReduceOp.AVG;
-  * the first-layer weight gradient is row-sparse (only the items of each
-    rank's batch): every rank all-gathers the (item id, gradient row) lists
-    of all ranks and merges them with the same deterministic counting-sort
-    kernel that builds the local rows (hvae_w1_rowgrad), weighting each rank
-    by 1/world. A dense all-reduce of the [N, H] gradient would move N*H*4
-    bytes per step instead.
+  * sharding (dp_shard): every rank draws the same seeded permutation of all users; global batch g is users
+    [g W B, (g + 1) W B) of it and rank r takes the r-th B of them, so the union of a step is exactly the
+    global batch one GPU would take at batch size W B. The last, partial global batch is split over the ranks
+    as evenly as possible (a rank may get none). Every rank therefore runs the same number of steps, with
+    the same collectives (pre-sharded data, as bench.py's per-rank shards, must have equal sizes).
+  * exchange (one step, two all-gathers): rank r's packet is [its dense small-parameter gradient * w_r | its
+    batch compacted as CSR (row offsets, item ids, values * w_r)] plus its da [B, H], the gradient of the
+    first hidden layer's pre-activation, with w_r = B_r / (sum of the ranks' B_r) (1 / W for full batches).
+    The first-layer weight gradient is linear in (x, da): every rank rebuilds it for the union batch from the
+    gathered packets with the same deterministic row-gradient kernels, in rank-major batch order -- the order
+    one GPU would use for the union batch. Per rank B H + 2 nnz + B words move instead of (distinct items)
+    x H (Syn-10M: ~9 MB instead of ~160 MB), and nothing is padded to an epoch maximum.
+  * the dense small gradients are summed in rank order; every rank then clips and steps Adam on identical
+    gradients, so the replicas stay bit-identical.
 
-The row lists are exchanged at a fixed size M per epoch: every rank counts the
-unique items of each of its batches on the host when the epoch order is drawn,
-and one all-reduce(MAX) per epoch gives the largest list of any rank and batch.
-Entries past a rank's own count carry weight 0.
-
-A step then makes ONE collective: each rank packs [dense gradients | row count |
-item ids | gradient rows] into one fp32 buffer at the end of its forward/backward
-graph, a single all_gather_into_tensor moves it (per-collective latency, not
-bytes, dominates at these sizes on xGMI), and the update graph averages the
-dense parts in rank order and merges the row lists. So a step has no host
-synchronisation: two captured graphs with one collective between them.
-
-Then every rank clips and steps Adam on identical gradients, so the replicas
-stay bit-identical. The merge function is injectable so that the collective
-protocol can be tested with gloo on CPU (tests/test_dist_gloo.py); with the
-gloo backend, device tensors are staged through host memory.
+In the fused trainer a step is two captured graphs (forward/backward + pack; unpack + union row gradient +
+clip + Adam) with the two collectives launched eagerly between them. pack_fn / merge_fn are injectable so
+that the protocol runs with gloo on CPU (tests/test_dist_gloo.py); with the gloo backend device tensors are
+staged through host memory.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable
 
 import numpy as np
@@ -40,49 +34,83 @@ import torch
 import torch.distributed as dist
 
 
-def batch_unique_counts(indptr: np.ndarray, indices: np.ndarray, order: np.ndarray, B: int,
-                        drop_last: bool = False) -> np.ndarray:
-    """Unique items of each batch of `order` (users, batch size B): the host twin of the plan kernels."""
+def init_from_env(backend: str | None = None):
+    """torchrun's environment (WORLD_SIZE, RANK, LOCAL_RANK, MASTER_*) -> one process per GPU: select GPU
+    LOCAL_RANK and join the process group (RCCL -- backend "nccl" on ROCm -- unless HVAE_DIST_BACKEND names
+    another) before any other GPU work. Returns the group, or None for a single process."""
+    if int(os.environ.get("WORLD_SIZE", "1")) <= 1:
+        return None
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(torch.cuda.device_count(), 1)
+    dev = torch.device("cuda", local % ndev)  # more ranks than GPUs: a one-GPU rehearsal (gloo)
+    torch.cuda.set_device(dev)
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        be = backend or os.environ.get("HVAE_DIST_BACKEND", "nccl")
+        if be == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(be)
+    return dist.group.WORLD
+
+
+def is_main(group) -> bool:
+    return group is None or dist.get_rank(group) == 0
+
+
+def all_reduce_host(values, group, device, op=dist.ReduceOp.SUM) -> np.ndarray:
+    """Host numbers reduced over the ranks (a device tensor for RCCL, a CPU one for gloo)."""
+    t = torch.as_tensor(np.asarray(values, dtype=np.float64),
+                        device=device if dist.get_backend(group) == "nccl" else "cpu")
+    dist.all_reduce(t, op=op, group=group)
+    return t.cpu().numpy()
+
+
+def broadcast_seed(group, device) -> int:
+    """A seed drawn from rank 0's numpy global RNG, the same on every rank."""
+    s = np.array([np.random.randint(0, 2 ** 31 - 1) if dist.get_rank(group) == 0 else 0], dtype=np.float64)
+    t = torch.as_tensor(s, device=device if dist.get_backend(group) == "nccl" else "cpu")
+    dist.broadcast(t, 0, group=group)
+    return int(t.cpu().item())
+
+
+def dp_shard(order: np.ndarray, B: int, world: int, rank: int):
+    """This rank's users for one epoch of `order` (a permutation of all users, identical on every rank).
+
+    Returns (users, n_full, tail_counts): the rank's users in step order (n_full full batches of B, then its
+    tail), the number of full global batches, and every rank's share of the last partial global batch.
+    """
+    order = np.asarray(order)
+    WB = world * B
     n = len(order)
-    nb = n // B if drop_last else -(-n // B)
-    out = np.zeros(nb, dtype=np.int64)
-    for b in range(nb):
-        us = order[b * B:(b + 1) * B]
-        parts = [indices[indptr[u]:indptr[u + 1]] for u in us]
-        out[b] = len(np.unique(np.concatenate(parts))) if parts else 0
-    return out
+    n_full = n // WB
+    T = n - n_full * WB
+    counts = [T // world + (1 if r < T % world else 0) for r in range(world)]
+    full = order[: n_full * WB].reshape(n_full, world, B)[:, rank, :].reshape(-1)
+    start = n_full * WB + sum(counts[:rank])
+    return np.concatenate([full, order[start:start + counts[rank]]]), n_full, counts
 
 
 class DPExchange:
-    def __init__(self, group, device: torch.device, n_items: int, H: int,
-                 merge_fn: Callable | None = None, make_merged: Callable | None = None):
+    def __init__(self, group, device: torch.device, n_items: int, H: int, n_small: int,
+                 pack_fn: Callable | None = None, merge_fn: Callable | None = None,
+                 make_merged: Callable | None = None):
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = device
         self.backend = dist.get_backend(group)
-        self.n_items, self.H = n_items, H
+        self.n_items, self.H, self.ns = n_items, H, n_small
+        self.pack_fn = pack_fn or _hip_pack
         self.merge_fn = merge_fn or _hip_merge
         self.make_merged = make_merged or _hip_make_merged
-        self.M = 0
-        self._merged = None
-        self._buf = None
-        self._pk = None
+        self.B = self.cap = 0
+        self._plans: dict = {}
+        self._merged: dict = {}
 
-    # -- collectives (gloo cannot take device tensors for every op: stage through host) --
+    # ----------------------------------------------------------- collectives ---
     def _stage(self, t: torch.Tensor) -> torch.Tensor:
         return t.cpu() if (self.backend == "gloo" and t.device.type != "cpu") else t
-
-    def all_reduce_dense(self, g: torch.Tensor) -> None:
-        if self.world == 1:
-            return
-        x = self._stage(g)
-        op = dist.ReduceOp.AVG if self.backend == "nccl" else dist.ReduceOp.SUM
-        dist.all_reduce(x, op=op, group=self.group)
-        if op != dist.ReduceOp.AVG:
-            x.div_(self.world)
-        if x is not g:
-            g.copy_(x)
 
     def _all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
         o, i = self._stage(out), self._stage(inp)
@@ -90,94 +118,82 @@ class DPExchange:
         if o is not out:
             out.copy_(o)
 
-    # -- one-collective step: pack (graph 1) -> all-gather (eager) -> unpack + merge (graph 2) --
-    def _packed(self, n_small: int):
-        """(send [L], recv [W, L]) for the epoch's M; L = n_small + 1 + M + M * H (fp32 words)."""
-        M, W, H = self.M, self.world, self.H
-        L = n_small + 1 + M + M * H
-        if self._pk is None or self._pk[0].numel() != L:
-            self._pk = (torch.zeros(L, dtype=torch.float32, device=self.device),
-                        torch.zeros(W, L, dtype=torch.float32, device=self.device))
-        return self._pk
+    def all_reduce(self, values, op=dist.ReduceOp.SUM) -> np.ndarray:
+        """Host values reduced over the ranks (epoch bookkeeping, not per step)."""
+        t = torch.as_tensor(np.asarray(values, dtype=np.float64),
+                            device=self.device if self.backend == "nccl" else "cpu")  # RCCL takes device tensors
+        if self.world > 1:
+            dist.all_reduce(t, op=op, group=self.group)
+        return t.cpu().numpy()
 
-    def pack(self, g_small: torch.Tensor, n_unique: torch.Tensor, item_of: torch.Tensor, rows: torch.Tensor) -> None:
-        """Device copies of this rank's step gradients into the send buffer (capturable)."""
-        M, ns = self.M, g_small.numel()
-        assert M > 0, "plan_epoch() first"
-        assert item_of.numel() >= M and rows.shape[0] >= M, "row-gradient buffers shorter than the exchange size"
-        send, _ = self._packed(ns)
-        send[:ns].copy_(g_small.reshape(-1))
-        send[ns:ns + 1].view(torch.int32).copy_(n_unique.reshape(1).to(torch.int32))
-        send[ns + 1:ns + 1 + M].view(torch.int32).copy_(item_of[:M])
-        send[ns + 1 + M:].view(M, self.H).copy_(rows[:M])
+    # ------------------------------------------------------------- buffers ---
+    def plan(self, B: int, cap: int) -> None:
+        """Select the buffers of a step of B users per rank whose packed batch holds at most cap entries (the
+        same B and cap on every rank). Each (B, cap) keeps its own buffers for the life of the exchange, so a
+        graph captured against them stays valid when the epoch's short last step switches B and back."""
+        key = (B, cap)
+        if key not in self._plans:
+            W, H, ns, dev = self.world, self.H, self.ns, self.device
+            L = ns + (B + 1) + 2 * cap  # fp32 words: [g_small | row offsets | items | values]
+            j = torch.arange(B, dtype=torch.int32, device=dev)
+            if W * cap not in self._merged:  # the union batch's row gradient, per packet cap
+                self._merged[W * cap] = self.make_merged(self.n_items, H, W * cap, dev)
+            self._plans[key] = dict(
+                L=L, off_rp=ns, off_col=ns + B + 1,
+                send=torch.zeros(L, dtype=torch.float32, device=dev),
+                recv=torch.zeros(W, L, dtype=torch.float32, device=dev),
+                send_da=torch.zeros(B, H, dtype=torch.float32, device=dev),
+                recv_da=torch.zeros(W * B, H, dtype=torch.float32, device=dev),
+                rp_u=torch.zeros(W * (B + 1), dtype=torch.int64, device=dev),
+                base=(torch.arange(W, dtype=torch.int64, device=dev) * L + ns + B + 1)[:, None],
+                rows_u=(torch.arange(W, dtype=torch.int32, device=dev)[:, None] * (B + 1) + j[None, :]).reshape(-1),
+                merged=self._merged[W * cap])
+        for k, v in self._plans[key].items():
+            setattr(self, k, v)
+        self.B, self.cap = B, cap
 
-    def communicate(self, n_small: int) -> None:
-        """The step's one collective (eager, between the two graphs)."""
-        send, recv = self._packed(n_small)
-        if self.world == 1:
-            recv[0].copy_(send)
+    # ---------------------------------------------------------------- step ---
+    def pack(self, g_small: torch.Tensor, x, nb: int, da: torch.Tensor | None, weight: float) -> None:
+        """Device-only (graph-capturable): this rank's packet. x: its batch (CsrBatch of nb rows, or None
+        when the rank has no users in this step); da: its [nb, H] pre-activation gradient."""
+        ns = self.ns
+        torch.mul(g_small.reshape(-1), weight, out=self.send[:ns])
+        if x is None or nb == 0:
+            self.send[ns:].zero_()
+            self.send_da.zero_()
             return
-        self._all_gather(recv.reshape(-1), send)
+        flat = self.send
+        self.pack_fn(self, x, weight, flat[self.off_rp:self.off_rp + nb + 1].view(torch.int32),
+                     flat[self.off_col:self.off_col + self.cap].view(torch.int32),
+                     flat[self.off_col + self.cap:], self.cap)
+        if nb < self.B:  # a short tail: rows past nb are empty
+            flat[self.off_rp + nb + 1:self.off_rp + self.B + 1].view(torch.int32).copy_(
+                flat[self.off_rp + nb:self.off_rp + nb + 1].view(torch.int32).expand(self.B - nb))
+            self.send_da[nb:].zero_()
+        if da is not None and da.data_ptr() != self.send_da.data_ptr():
+            self.send_da[:nb].copy_(da[:nb])
+
+    def communicate(self) -> None:
+        """The step's collectives (eager, between the two graphs)."""
+        if self.world == 1:
+            self.recv[0].copy_(self.send)
+            self.recv_da.copy_(self.send_da)
+            return
+        self._all_gather(self.recv.reshape(-1), self.send)
+        self._all_gather(self.recv_da, self.send_da)
 
     def unpack_merge(self, g_small: torch.Tensor):
-        """Dense gradients <- mean over ranks (summed in rank order); row lists -> merged row gradient."""
-        M, W, H, ns = self.M, self.world, self.H, g_small.numel()
-        _, recv = self._packed(ns)
-        torch.sum(recv[:, :ns], dim=0, out=g_small.reshape(-1))
-        g_small.div_(W)
-        b = self._buf
-        b["n"].copy_(recv[:, ns].contiguous().view(torch.int32))
-        b["items"].view(W, M).copy_(recv[:, ns + 1:ns + 1 + M].contiguous().view(torch.int32))
-        b["rows"].view(W, M, H).copy_(recv[:, ns + 1 + M:].reshape(W, M, H))
-        return self.merge()
-
-    def plan_epoch(self, counts_per_batch: np.ndarray) -> int:
-        """One host collective per epoch: the largest row list of any rank and batch. (Re)allocates the
-        exchange and merge buffers when it grows, so that nothing is allocated inside a captured step."""
-        m = torch.tensor([int(counts_per_batch.max()) if len(counts_per_batch) else 1], dtype=torch.int64,
-                         device=self.device if self.backend == "nccl" else "cpu")  # RCCL takes device tensors only
-        if self.world > 1:
-            dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
-        M = max(int(m.item()), 1)
-        if M > self.M:
-            self.M = M
-            W, H, dev = self.world, self.H, self.device
-            self._buf = {
-                "n": torch.zeros(W, dtype=torch.int32, device=dev),
-                "items": torch.zeros(W * M, dtype=torch.int32, device=dev),
-                "rows": torch.zeros(W * M, H, dtype=torch.float32, device=dev),
-                "w": torch.zeros(W * M, dtype=torch.float32, device=dev),
-                "rp": torch.arange(W * M + 1, dtype=torch.int64, device=dev),
-                "j": torch.arange(M, dtype=torch.int32, device=dev),
-            }
-            self._merged = self.make_merged(self.n_items, H, W * M, dev)
-            self._pk = None
-        return self.M
-
-    def exchange(self, n_unique: torch.Tensor, item_of: torch.Tensor, rows: torch.Tensor) -> None:
-        """The collectives of a step: all-gather every rank's row list at the epoch's fixed size M."""
-        M = self.M
-        assert M > 0, "plan_epoch() first"
-        assert item_of.numel() >= M and rows.shape[0] >= M, "row-gradient buffers shorter than the exchange size"
-        b = self._buf
-        self._all_gather(b["n"], n_unique.reshape(1).to(torch.int32))
-        self._all_gather(b["items"], item_of[:M].contiguous())
-        self._all_gather(b["rows"], rows[:M].contiguous())
-
-    def merge(self):
-        """Device-only (graph-capturable) half: weights 1/W for each rank's own entries, 0 past its count
-        (those point at item 0), then the deterministic merge into the merged row gradient."""
-        W = self.world
-        b = self._buf
-        valid = (b["j"][None, :] < b["n"][:, None]).reshape(-1)  # rank-major [W*M]
-        torch.div(valid.to(torch.float32), W, out=b["w"])
-        b["items"].masked_fill_(~valid, 0)
-        self.merge_fn(self, b["items"], b["rows"], b["w"], self._merged, b["rp"])
-        return self._merged
-
-    def merged_rows(self, n_unique, item_of, rows):
-        self.exchange(n_unique, item_of, rows)
-        return self.merge()
+        """Device-only (graph-capturable): dense gradients <- rank-order sum of the weighted packets; the union
+        batch's first-layer row gradient <- the row-gradient kernels over the gathered (x, da)."""
+        W, B, ns = self.world, self.B, self.ns
+        torch.sum(self.recv[:, :ns], dim=0, out=g_small.reshape(-1))
+        rp = self.rp_u.view(W, B + 1)
+        rp.copy_(self.recv[:, self.off_rp:self.off_rp + B + 1].view(torch.int32))
+        rp.add_(self.base)
+        flat = self.recv.reshape(-1)
+        self.merge_fn(self, self.rp_u, flat.view(torch.int32), flat[self.cap:], self.rows_u, W * B, self.recv_da,
+                      self.merged)
+        return self.merged
 
 
 def _hip_make_merged(n_items, H, cap, device):
@@ -185,8 +201,13 @@ def _hip_make_merged(n_items, H, cap, device):
     return ops.RowGradBuffers(n_items, H, cap, device)
 
 
-def _hip_merge(ex: DPExchange, items, grows, weights, out, rp):
-    """Sum the gathered rows per item in (rank, slot) order with hvae_w1_rowgrad."""
+def _hip_pack(ex: DPExchange, x, weight, rp_out, col_out, val_out, cap):
+    from ._lib import check, lib, ptr
+    check(lib().hvae_csr_batch_pack(x, float(weight), ptr(rp_out), ptr(col_out), ptr(val_out), cap,
+                                    torch.cuda.current_stream(ex.device).cuda_stream), "hvae_csr_batch_pack")
+
+
+def _hip_merge(ex: DPExchange, row_ptr, col_idx, vals, rows, nb, da, out):
+    """hvae_w1_rowgrad over the union batch: rows rank-major, each rank's rows in its batch order."""
     from . import ops
-    csr = ops.Csr(rp, items.to(torch.int32), weights, ex.n_items)
-    ops.w1_rowgrad(csr, grows, out)
+    ops.w1_rowgrad(ops.Csr(row_ptr, col_idx, vals, ex.n_items, rows=rows, nb=nb), da, out)

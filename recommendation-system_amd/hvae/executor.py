@@ -122,6 +122,7 @@ class DeviceData:
     host_indptr: np.ndarray = field(default=None)   # host CSR (data-parallel exchange sizing)
     host_indices: np.ndarray = field(default=None)
     users_host: np.ndarray = field(default=None)
+    dp_global: bool = False   # data parallel: every rank holds every user (hvae/dist.py dp_shard)
 
     @staticmethod
     def from_scipy(mat, users, device) -> "DeviceData":
@@ -148,8 +149,27 @@ class DeviceData:
         return max(int(top.sum()), 1)
 
 
+def _sampler_order(n: int, generator: torch.Generator | None, device) -> torch.Tensor:
+    """The order DataLoader(shuffle=True) draws (torch RandomSampler.__iter__): with no generator, a fresh CPU
+    generator seeded from the global RNG; with a CPU generator, randperm from it and a second draw the sampler
+    makes when its iterator finishes; a device generator (benchmarks) draws on the device."""
+    if generator is None:
+        seed = int(torch.empty((), dtype=torch.int64).random_().item())
+        g = torch.Generator()
+        g.manual_seed(seed)
+        return torch.randperm(n, generator=g)
+    if generator.device.type != "cpu":
+        return torch.randperm(n, generator=generator, device=generator.device)
+    order = torch.randperm(n, generator=generator)
+    torch.randperm(n, generator=generator)  # RandomSampler's trailing (empty-slice) draw
+    return order
+
+
 class _StepBuffers:
-    """Activations / gradients for one batch size (graph-static pointers)."""
+    """Activations / gradients for one batch size (graph-static pointers).
+
+    cap: entries of the batch's first-layer row gradient (single GPU); with data parallelism the union
+    batch's (world x the per-rank packet cap), which the clip workspace must cover."""
 
     def __init__(self, ex: "FusedTrainer", B: int, cap: int, train: bool):
         dev, lay = ex.device, ex.layout
@@ -177,7 +197,9 @@ class _StepBuffers:
         self.dh = [f(B, hd) for hd in H]
         self.da = [f(B, hd) for hd in H]
         self.loss3 = f(3)
-        self.rg = ops.RowGradBuffers(lay.n_items, H[0], cap, dev) if train else None
+        # the local row gradient (single GPU); data parallel steps build the union's in the exchange
+        self.rg = ops.RowGradBuffers(lay.n_items, H[0], cap, dev) if (train and ex.dp is None) else None
+        self.cap = cap
         L_ = lib()
         need = [
             L_.hvae_decoder_workspace(ex.dec_dtype, B, lay.n_items, d),
@@ -199,6 +221,7 @@ class _StepBuffers:
         # side-stream GEMMs: their split-K slabs must not alias the main stream's
         self.ws2 = torch.empty_like(self.ws) if ex.two_streams else None
         self.graph = None
+        self.graph_data = None  # the DeviceData a captured graph reads (held, compared by identity)
 
 
 class FusedTrainer:
@@ -281,15 +304,23 @@ class FusedTrainer:
         self._bufs: dict[tuple, _StepBuffers] = {}
         self._views()
         self.dp = None
+        self.dp_epoch = 0
+        self._dp_caps: dict = {}
         if process_group is not None and torch.distributed.get_world_size(process_group) > 1:
             from .dist import DPExchange
-            self.dp = DPExchange(process_group, device, lay.n_items, lay.hidden[0])
+            self.dp = DPExchange(process_group, device, lay.n_items, lay.hidden[0], lay.n_small)
             # replicas start from rank 0's parameters (identical seeds make this a no-op, but be explicit)
-            torch.distributed.broadcast(self.flat, 0, group=process_group)
-            seed_t = torch.tensor([self.seed], dtype=torch.int64, device=device)
+            on_dev = torch.distributed.get_backend(process_group) == "nccl"
+            flat = self.flat if on_dev else self.flat.cpu()
+            torch.distributed.broadcast(flat, 0, group=process_group)
+            if flat is not self.flat:
+                self.flat.copy_(flat)
+            seed_t = torch.tensor([self.seed], dtype=torch.int64, device=device if on_dev else "cpu")
             torch.distributed.broadcast(seed_t, 0, group=process_group)
-            # per-rank dropout streams must differ (each rank sees different users)
-            self.seed = int(seed_t.item()) + 7919 * torch.distributed.get_rank(process_group)
+            # the epoch order is drawn from rank 0's seed on every rank (dp_shard); per-rank dropout streams must
+            # differ (each rank sees different users)
+            self.dp_seed = int(seed_t.item())
+            self.seed = self.dp_seed + 7919 * torch.distributed.get_rank(process_group)
 
     # ------------------------------------------------------------ state ---
     def _adopt_parameters(self):
@@ -349,7 +380,7 @@ class FusedTrainer:
     def _buffers(self, B: int, cap: int, train: bool) -> _StepBuffers:
         key = (B, train)
         b = self._bufs.get(key)
-        if b is None or (train and b.rg.cap < cap):
+        if b is None or (train and b.cap < cap):
             b = _StepBuffers(self, B, cap, train)
             self._bufs[key] = b
         return b
@@ -359,29 +390,36 @@ class FusedTrainer:
                         data.n_items)
 
     def _launch(self, bf: _StepBuffers, csr: CsrBatch, train: bool, beta: float, p_drop: float,
-                ext: dict | None = None, advance: int = 0):
+                ext: dict | None = None, advance: int = 0, weight: float = 1.0):
         """Enqueue one full step on the current stream (captured into a graph by the caller).
 
-        advance > 0 also moves the device batch offset (rows_offset) by that many users.
+        advance > 0 also moves the device batch offset (rows_offset) by that many users. Data parallel:
+        the step's exchange runs between the forward/backward and the update; weight = this rank's share of
+        the union batch.
         """
+        if train and self.dp is not None:
+            self._launch_fwd_bwd(bf, csr, train, beta, p_drop, ext)
+            self._launch_pack(bf, csr, weight)
+            self._launch_exchange()
+            self._launch_dp_update(bf, advance)
+            return
         self._launch_fwd_bwd(bf, csr, train, beta, p_drop, ext)
         if train:
-            if self.dp is None:
-                self._launch_update(bf.rg, bf, advance)
-            else:
-                self._launch_pack(bf)
-                self._launch_exchange(bf)
-                self._launch_dp_update(bf, advance)
+            self._launch_update(bf.rg, bf, advance)
         elif advance:
             self._advance(advance)
 
-    def _launch_pack(self, bf: _StepBuffers):
-        """End of a data-parallel forward/backward: this rank's gradients into the exchange buffer."""
-        self.dp.pack(self.g_small, bf.rg.n_unique, bf.rg.item_of, bf.rg.rows)
+    def _launch_pack(self, bf: _StepBuffers | None, csr: CsrBatch | None, weight: float):
+        """End of a data-parallel forward/backward: this rank's packet (weighted small gradients, its batch
+        as compact CSR, its first-layer pre-activation gradient). bf None: no users in this step."""
+        if bf is None:
+            self.dp.pack(self.g_small.zero_(), None, 0, None, 0.0)
+            return
+        self.dp.pack(self.g_small, C.byref(csr), bf.B, bf.da[0], weight)
 
-    def _launch_exchange(self, bf: _StepBuffers):
-        """The step's one collective (eager, between the two graphs): all-gather of the packed gradients."""
-        self.dp.communicate(self.g_small.numel())
+    def _launch_exchange(self):
+        """The step's collectives (eager, between the two graphs)."""
+        self.dp.communicate()
 
     def _launch_dp_update(self, bf: _StepBuffers, advance: int):
         merged = self.dp.unpack_merge(self.g_small)
@@ -426,7 +464,16 @@ class FusedTrainer:
                                    st2 if side_ else st), "gemm")
 
         ev_plan = None
-        if train and self.plan_stream is not None and B >= self.plan_side_min_batch:
+        dp = self.dp is not None
+        if train and dp:
+            # data parallel: no local row gradient (the exchange builds the union's); the batch's W1t rows
+            # replay their deferred steps, found from the CSR entries, before the forward reads them
+            if self.lazy_adam:
+                cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
+                check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
+                                                    ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
+                      "adam_lazy_catchup_csr")
+        elif train and self.plan_stream is not None and B >= self.plan_side_min_batch:
             # the batch's W1t rows replay their deferred steps (found from the CSR) before the forward reads
             # them, while the row-gradient plan runs on the plan stream
             if self.lazy_adam:
@@ -540,7 +587,8 @@ class FusedTrainer:
                           (B, H[k - 1], H[k], ptr(bf.da[k]), H[k], ptr(W), H[k - 1], ptr(bf.dh[k - 1]), H[k - 1]))
         if ev_plan is not None:
             main.wait_event(ev_plan)
-        check(L_.hvae_w1_rowgrad_apply(ptr(bf.da[0]), H[0], bf.rg.ref, st), "w1_rowgrad_apply")
+        if not dp:
+            check(L_.hvae_w1_rowgrad_apply(ptr(bf.da[0]), H[0], bf.rg.ref, st), "w1_rowgrad_apply")
         self._fork(side, main)  # join: every gradient is complete on the main stream
 
     def _launch_update(self, rg, bf: _StepBuffers, advance: int = 0):
@@ -602,16 +650,25 @@ class FusedTrainer:
 
     # -------------------------------------------------------- public API ---
     def step_batch(self, data: DeviceData, rows: torch.Tensor | None, B: int, beta: float, p_drop: float,
-                   train: bool = True, ext: dict | None = None) -> torch.Tensor:
-        """One eager step over `rows` (int32 device user ids, or None: rows 0..B-1). Returns loss3."""
+                   train: bool = True, ext: dict | None = None, weight: float | None = None) -> torch.Tensor:
+        """One eager step over `rows` (int32 device user ids, or None: rows 0..B-1). Returns loss3.
+
+        Data parallel (train): every rank calls it together with its own rows; weight = this rank's share of
+        the union batch (default 1 / world: equal batches)."""
         cap = int(data.row_ptr[-1].item()) if rows is None else data.max_batch_nnz(B)
+        dp = self.dp if train else None
+        if dp is not None:
+            cap = int(dp.all_reduce([cap], op=torch.distributed.ReduceOp.MAX)[0])
+            dp.plan(B, cap)
+            cap *= dp.world
         bf = self._buffers(B, cap, train)
         csr = self._csr(data, B, rows, None)
         if train:
             self._check_steps(1)
         else:
             self.flush()
-        self._launch(bf, csr, train, beta, p_drop, ext)
+        self._launch(bf, csr, train, beta, p_drop, ext,
+                     weight=(1.0 / dp.world if weight is None else weight) if dp is not None else 1.0)
         if train:
             self.host_step += 1
             self.flush()
@@ -628,14 +685,13 @@ class FusedTrainer:
         n = int(data.users.numel())
         if n == 0:
             return {"total_loss": float("nan"), "recon_loss": float("nan"), "kl_loss": float("nan")}
+        if train and self.dp is not None:
+            return self._run_epoch_dp(data, batch_size, shuffle, beta_fn, p_drop, drop_last, generator,
+                                      max_batches)
         if shuffle:
-            # a device generator draws the order on the GPU (no host stall at the epoch boundary); the
-            # default CPU generator keeps DataLoader(shuffle=True)'s exact order
-            order = torch.randperm(n, generator=generator,
-                                   device=generator.device if generator is not None else "cpu")
+            order = _sampler_order(n, generator, self.device)
             data.perm.copy_(data.users[order.to(self.device)])
         else:
-            order = None
             data.perm.copy_(data.users)
         accum = self.accum_train if train else self.accum_val
         accum.zero_()
@@ -652,38 +708,19 @@ class FusedTrainer:
         n_batches = n_full + (1 if tail else 0)
         const_beta = getattr(beta_fn, "constant", None)
         B = batch_size
-        dp = self.dp if train else None
-        M = 0
-        if dp is not None:  # fixed exchange size for the epoch: one host all-reduce, no per-step sync
-            from .dist import batch_unique_counts
-            users_h = data.users_host if order is None else data.users_host[order.cpu().numpy()]
-            counts = batch_unique_counts(data.host_indptr, data.host_indices,
-                                         users_h[: n_full * B + (tail if tail else 0)], B)
-            M = dp.plan_epoch(counts)
         for bi in range(n_full):
             beta = beta_fn(bi)
-            bf = self._buffers(B, max(data.max_batch_nnz(B), M), train)
+            bf = self._buffers(B, data.max_batch_nnz(B), train)
             if self.use_graphs and const_beta is not None:
-                key = (id(data), beta, p_drop, M)
-                if bf.graph is None or bf.graph_key != key:
-                    if bi == 0 and bf.graph is None:
-                        # first use: run eagerly (loads kernels, sets attributes), capture afterwards
-                        self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
-                        if train:
-                            self.host_step += 1
-                        continue
-                    self._capture(bf, data, train, beta, p_drop, key)
-                bf.graph.replay()
-                if dp is not None:  # collectives between the two graphs of a data-parallel step
-                    self._launch_exchange(bf)
-                    bf.graph_up.replay()
+                if not self._replay(bf, data, train, beta, p_drop, bi, (beta, p_drop)):
+                    continue
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
             if train:
                 self.host_step += 1
         if tail:
             beta = beta_fn(n_full)
-            bf = self._buffers(tail, max(data.max_batch_nnz(tail), M), train)
+            bf = self._buffers(tail, data.max_batch_nnz(tail), train)
             self._launch(bf, self._csr(data, tail, data.perm, self.boff), train, beta, p_drop, advance=tail)
             if train:
                 self.host_step += 1
@@ -691,8 +728,108 @@ class FusedTrainer:
         sums = accum.cpu().tolist()  # the one host sync of the epoch
         return {"total_loss": sums[0] / n_batches, "recon_loss": sums[1] / n_batches, "kl_loss": sums[2] / n_batches}
 
+    def _replay(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float, bi: int,
+                key) -> bool:
+        """Run one full batch through its captured graph(s), capturing them first if needed. The first use of
+        a buffer set runs eagerly instead (loads kernels, sets attributes) and returns False (already stepped).
+        A graph holds the DeviceData it reads (compared by identity, so a freed dataset's address reused by a
+        new one never replays a stale graph)."""
+        if bf.graph is None or bf.graph_key != key or bf.graph_data is not data:
+            if bi == 0 and bf.graph is None:
+                self._launch(bf, self._csr(data, bf.B, data.perm, self.boff), train, beta, p_drop, advance=bf.B,
+                             weight=key[-1] if self.dp is not None and train else 1.0)
+                if train:
+                    self.host_step += 1
+                return False
+            self._capture(bf, data, train, beta, p_drop, key)
+        bf.graph.replay()
+        if bf.graph_up is not None:  # data parallel: the collectives between the two graphs of a step
+            self._launch_exchange()
+            bf.graph_up.replay()
+        return True
+
+    # ------------------------------------------------------ data parallel ---
+    def _dp_cap(self, data: DeviceData, B: int) -> int:
+        """Entries of the largest batch of B users any rank can draw (agreed once per dataset and B)."""
+        key = (id(data), B)
+        hit = self._dp_caps.get(key)
+        if hit is None or hit[0] is not data:
+            cap = int(self.dp.all_reduce([data.max_batch_nnz(B)], op=torch.distributed.ReduceOp.MAX)[0])
+            self._dp_caps[key] = hit = (data, max(cap, 1))
+        return hit[1]
+
+    def _run_epoch_dp(self, data: DeviceData, B: int, shuffle: bool, beta_fn, p_drop: float, drop_last: bool,
+                      generator, max_batches) -> dict:
+        """A data-parallel training epoch (hvae/dist.py). data.dp_global: every rank holds every user and takes
+        its slice of each global batch of a permutation drawn from the shared seed; otherwise the ranks'
+        datasets are their own shards, which must have equal sizes."""
+        from .dist import dp_shard
+        dp, W, r = self.dp, self.dp.world, self.dp.rank
+        users = data.users_host
+        n = len(users)
+        if data.dp_global:
+            rng = np.random.default_rng([self.dp_seed, self.dp_epoch])
+            order = users[rng.permutation(n)] if shuffle else users
+            mine, n_full, counts = dp_shard(order, B, W, r)
+        else:
+            sizes = dp.all_reduce([n, -n], op=torch.distributed.ReduceOp.MAX)
+            if int(sizes[0]) != n or int(-sizes[1]) != n:
+                raise ValueError("data-parallel shards of unequal sizes: give every rank the whole dataset "
+                                 "(DeviceData.dp_global) or equal shards")
+            if shuffle:
+                mine = users[_sampler_order(n, generator, self.device).cpu().numpy()]
+            else:
+                mine = users
+            n_full, t = divmod(n, B)
+            counts = [t] * W
+        self.dp_epoch += 1
+        if drop_last:
+            counts = [0] * W
+        if max_batches is not None:
+            n_full, counts = min(n_full, max_batches), [0] * W
+        data.perm[:len(mine)].copy_(torch.as_tensor(np.asarray(mine, dtype=np.int32)).to(self.device))
+        self.accum_train.zero_()
+        self.boff.zero_()
+        n_steps = n_full + (1 if sum(counts) else 0)
+        self._check_steps(n_steps + 1)
+        const_beta = getattr(beta_fn, "constant", None)
+        cap = self._dp_cap(data, B)
+        if n_full:
+            dp.plan(B, cap)
+        for bi in range(n_full):
+            beta = beta_fn(bi)
+            bf = self._buffers(B, W * cap, True)
+            if self.use_graphs and const_beta is not None:
+                if not self._replay(bf, data, True, beta, p_drop, bi, (beta, p_drop, cap, 1.0 / W)):
+                    continue
+            else:
+                self._launch(bf, self._csr(data, B, data.perm, self.boff), True, beta, p_drop, advance=B,
+                             weight=1.0 / W)
+            self.host_step += 1
+        sums = self.accum_train.cpu().numpy() / W  # the union batch's loss = mean of equal shares
+        if sum(counts):  # the last, partial global batch: eager, every rank takes part (possibly with no users)
+            T, c, Bt = sum(counts), counts[r], max(counts)
+            beta = beta_fn(n_full)
+            dp.plan(Bt, cap)
+            bf = self._buffers(Bt, W * cap, True)
+            if c:
+                bfc = self._buffers(c, W * cap, True)
+                csr = self._csr(data, c, data.perm, self.boff)
+                self.accum_train.zero_()
+                self._launch_fwd_bwd(bfc, csr, True, beta, p_drop, None)
+                self._launch_pack(bfc, csr, c / T)
+                sums = sums + self.accum_train.cpu().numpy() * (c / T)
+            else:
+                self._launch_pack(None, None, 0.0)
+            self._launch_exchange()
+            self._launch_dp_update(bf, c)
+            self.host_step += 1
+        self.flush()
+        tot = dp.all_reduce(sums)  # the union batches' losses summed over the steps
+        return {"total_loss": tot[0] / n_steps, "recon_loss": tot[1] / n_steps, "kl_loss": tot[2] / n_steps}
+
     def _capture(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float, key):
-        """One graph per step (single GPU); data-parallel: forward/backward, then merge + clip + Adam,
+        """One graph per step (single GPU); data-parallel: forward/backward + pack, then merge + clip + Adam,
         with the collectives launched eagerly in between (they stay out of the graphs)."""
         csr = self._csr(data, bf.B, data.perm, self.boff)
         bf.csr_keepalive = csr
@@ -705,13 +842,14 @@ class FusedTrainer:
         else:
             with torch.cuda.graph(g):
                 self._launch_fwd_bwd(bf, csr, train, beta, p_drop, None)
-                self._launch_pack(bf)
+                self._launch_pack(bf, csr, key[-1])
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2):
                 self._launch_dp_update(bf, bf.B)
             bf.graph_up = g2
         bf.graph = g
         bf.graph_key = key
+        bf.graph_data = data
 
     def sync_state_to_model(self):
         """Parameters are views of the flat buffer already; nothing to copy."""

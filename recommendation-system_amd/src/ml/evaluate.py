@@ -23,6 +23,7 @@ import torch
 from scipy.sparse import csr_matrix
 
 from hvae import ops
+from hvae.dist import all_reduce_host, broadcast_seed, init_from_env, is_main
 
 from ..config import config
 from ..preprocessing.embeddings import load_embeddings
@@ -96,12 +97,23 @@ def _build_input_matrix(train_df: pd.DataFrame, val_df: pd.DataFrame, user_to_id
     return csr_matrix((np.ones(len(combined)), (rows, cols)), shape=shape)
 
 
-def _aggregate_metrics(all_metrics: dict, k_values: list[int]) -> dict[int, dict[str, float]]:
-    return {
-        k: {m: float(np.mean(all_metrics[k][m])) if len(all_metrics[k][m]) else 0.0
-            for m in ["recall", "ndcg", "hit_ratio"]}
-        for k in k_values
-    }
+_METRICS = ["recall", "ndcg", "hit_ratio"]
+
+
+def _aggregate_metrics(all_metrics: dict, k_values: list[int], group=None, device=None) -> dict[int, dict[str, float]]:
+    """Means of the per-row metrics (reference: evaluate.py:90-98). With a process group every rank holds a
+    shard of the rows: the sums and the row count are all-reduced, so every rank returns the global means."""
+    if group is None:
+        return {
+            k: {m: float(np.mean(all_metrics[k][m])) if len(all_metrics[k][m]) else 0.0 for m in _METRICS}
+            for k in k_values
+        }
+    sums = [float(np.sum(all_metrics[k][m])) for k in k_values for m in _METRICS]
+    n = len(all_metrics[k_values[0]]["recall"]) if k_values else 0
+    tot = all_reduce_host(sums + [n], group, device)
+    cnt = tot[-1]
+    it = iter(tot[:-1])
+    return {k: {m: (float(next(it)) / cnt if cnt else 0.0) for m in _METRICS} for k in k_values}
 
 
 # =============================================================================
@@ -113,7 +125,11 @@ class RecommendationEvaluator:
     """Leave-one-out evaluator (reference: evaluate.py:106-265), batched on the device."""
 
     def __init__(self, model: HybridVAE, interaction_matrix: csr_matrix, user_to_idx: dict[str, int],
-                 item_to_idx: dict[str, int], device: torch.device, batch_size: int = 1024):
+                 item_to_idx: dict[str, int], device: torch.device, batch_size: int = 1024, process_group=None):
+        """process_group: the dataset protocols shard their rows over its ranks (rank r scores rows r, r + W,
+        ...) and all-reduce the metric sums; the 99-negative protocol first seeds numpy identically on every
+        rank (from rank 0's global RNG) so that all ranks draw the same negatives for every row."""
+        self.group = process_group
         self.model = model.to(device)
         self.model.eval()
         self.device = device
@@ -210,6 +226,8 @@ class RecommendationEvaluator:
         """99-negative protocol over every known (user, item) test row (reference: evaluate.py:187-215)."""
         k_values = k_values or [5, 10, 20]
         logger.info(f"Evaluating with negative sampling ({n_negatives} negatives)...")
+        if self.group is not None:  # every rank draws every row's negatives from the same stream
+            np.random.seed(broadcast_seed(self.group, self.device))
         users, tests, negs = [], [], []
         for user_id, item_id in zip(test_df["user_id"].tolist(), test_df["asin"].tolist()):
             if user_id not in self.user_to_idx or item_id not in self.item_to_idx:
@@ -219,14 +237,22 @@ class RecommendationEvaluator:
             tests.append(t)
             negs.append(self._sample_negatives(u, t, n_negatives))
         all_metrics = {k: {"recall": [], "ndcg": [], "hit_ratio": []} for k in k_values}
-        if users:
-            rank = self._ranks(np.array(users), np.array(tests), negs)
+        sl = self._shard(len(users))
+        if len(users[sl]):
+            rank = self._ranks(np.array(users[sl]), np.array(tests[sl]), negs[sl])
             m = metrics_from_rank(rank, k_values)
             for k in k_values:
                 for name in ("recall", "ndcg", "hit_ratio"):
                     all_metrics[k][name] = list(m[k][name])
         logger.info(f"Evaluated {len(users)} users")
-        return _aggregate_metrics(all_metrics, k_values)
+        return _aggregate_metrics(all_metrics, k_values, self.group, self.device)
+
+    def _shard(self, n: int) -> slice:
+        """This rank's rows of a dataset protocol (all rows without a process group)."""
+        if self.group is None:
+            return slice(0, n)
+        import torch.distributed as dist
+        return slice(dist.get_rank(self.group), n, dist.get_world_size(self.group))
 
     def evaluate_user(self, user_id: str, test_items: list[str], k_values: list[int] | None = None):
         k_values = k_values or [5, 10, 20]
@@ -255,6 +281,8 @@ class RecommendationEvaluator:
             rels.append(rel)
         all_metrics = {k: {"recall": [], "ndcg": [], "hit_ratio": []} for k in k_values}
         K = max(k_values)
+        sl = self._shard(len(users))
+        users, rels = users[sl], rels[sl]
         for s in range(0, len(users), self.batch_size):
             idx, _ = self._topk(np.array(users[s:s + self.batch_size]), K, True)
             for r, rel in enumerate(rels[s:s + self.batch_size]):
@@ -263,7 +291,7 @@ class RecommendationEvaluator:
                     all_metrics[k]["ndcg"].append(ndcg_at_k(idx[r], rel, k))
                     all_metrics[k]["hit_ratio"].append(hit_ratio_at_k(idx[r], rel, k))
         logger.info(f"Evaluated {len(users)} users")
-        return _aggregate_metrics(all_metrics, k_values)
+        return _aggregate_metrics(all_metrics, k_values, self.group, self.device)
 
 
 # =============================================================================
@@ -288,26 +316,30 @@ def evaluate_recommendation_model(model_path: str, data_dir: str, embeddings_pat
                                   k_values: list[int] | None = None, device: str | None = None,
                                   n_negatives: int | None = None) -> dict:
     k_values = k_values or [5, 10, 20]
+    group = init_from_env() if (device is None or str(device).startswith("cuda")) else None  # torchrun: shard rows
     device = _get_device(device)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
     full_matrix, train_df, val_df, mappings = load_training_data(data_dir)
     user_to_idx, item_to_idx = mappings["user_to_idx"], mappings["item_to_idx"]
     input_matrix = _build_input_matrix(train_df, val_df, user_to_idx, item_to_idx, full_matrix.shape)
     test_df = pd.read_csv(Path(data_dir) / "test.csv")
     embeddings, _, _ = load_embeddings(embeddings_path)
     model = load_model_from_checkpoint(model_path, embeddings, device)
-    evaluator = RecommendationEvaluator(model, input_matrix, user_to_idx, item_to_idx, device)
+    evaluator = RecommendationEvaluator(model, input_matrix, user_to_idx, item_to_idx, device, process_group=group)
     if n_negatives is not None:
         protocol = f"NEGATIVE SAMPLING ({n_negatives} negatives)"
         results = evaluator.evaluate_dataset_with_negatives(test_df, n_negatives, k_values)
     else:
         protocol = "FULL RANKING (all items)"
         results = evaluator.evaluate_dataset(test_df, k_values)
-    logger.info(f"\n{'=' * 70}\nHYBRID VAE EVALUATION RESULTS\nProtocol: {protocol}\n{'=' * 70}")
-    print(f"\n{'-' * 70}\n{'K':<5} | {'Recall':>12} | {'NDCG':>12} | {'Hit Ratio':>12}\n{'-' * 70}")
-    for k in k_values:
-        m = results[k]
-        print(f"@{k:<4} | {m['recall']:>12.4f} | {m['ndcg']:>12.4f} | {m['hit_ratio']:>12.4f}")
-    print("-" * 70)
+    if is_main(group):
+        logger.info(f"\n{'=' * 70}\nHYBRID VAE EVALUATION RESULTS\nProtocol: {protocol}\n{'=' * 70}")
+        print(f"\n{'-' * 70}\n{'K':<5} | {'Recall':>12} | {'NDCG':>12} | {'Hit Ratio':>12}\n{'-' * 70}")
+        for k in k_values:
+            m = results[k]
+            print(f"@{k:<4} | {m['recall']:>12.4f} | {m['ndcg']:>12.4f} | {m['hit_ratio']:>12.4f}")
+        print("-" * 70)
     return results
 
 
@@ -324,7 +356,7 @@ def main() -> None:
     n_negatives = args.n_negatives if args.n_negatives > 0 else None
     results = evaluate_recommendation_model(model_path=args.model, data_dir=args.data, embeddings_path=args.embeddings,
                                             k_values=args.k_values, device=args.device, n_negatives=n_negatives)
-    if args.output:
+    if args.output and is_main(init_from_env()):
         with open(args.output, "w") as f:
             json.dump(results, f, indent=2)
         logger.info(f"Results saved to {args.output}")

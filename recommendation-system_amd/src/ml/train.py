@@ -24,6 +24,7 @@ from scipy.sparse import csr_matrix
 from torch.utils.data import DataLoader, Dataset, RandomSampler
 
 from hvae import ops
+from hvae.dist import init_from_env, is_main
 from hvae.executor import ConstBeta, DeviceData, FusedTrainer
 
 from ..config import config
@@ -132,14 +133,16 @@ class VAETrainer:
     """Trainer for HybridVAE (reference: train.py:55-145)."""
 
     def __init__(self, model: HybridVAE, device: torch.device, lr: float = 0.001, weight_decay: float = 0.0,
-                 precision: str | None = None):
+                 precision: str | None = None, process_group=None):
+        """process_group: user-batch data parallelism over its ranks (hvae/dist.py): every rank holds the
+        whole dataset and takes its slice of each global batch of batch_size x world users."""
         device = torch.device(device)
         if device.type == "cuda" and device.index is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.model = model.to(device)
         self.device = device
         self.fused = FusedTrainer(self.model, device, lr=lr, weight_decay=weight_decay,
-                                  precision=precision or (config.PRECISION or None))
+                                  precision=precision or (config.PRECISION or None), process_group=process_group)
         self.optimizer = HipAdam(model.parameters(), self.fused, lr=lr, weight_decay=weight_decay)
         self.train_losses: list[float] = []
         self.val_losses: list[float] = []
@@ -166,7 +169,9 @@ class VAETrainer:
         if isinstance(loader, DataLoader) and isinstance(ds, UserInteractionDataset):
             shuffle = isinstance(loader.sampler, RandomSampler)
             gen = getattr(loader.sampler, "generator", None) if shuffle else None
-            return self.fused.run_epoch(ds.device_data(self.device), loader.batch_size, shuffle, beta_fn, p_drop,
+            data = ds.device_data(self.device)
+            data.dp_global = self.fused.dp is not None  # every rank has every user; ranks slice global batches
+            return self.fused.run_epoch(data, loader.batch_size, shuffle, beta_fn, p_drop,
                                         train=train, drop_last=loader.drop_last, generator=gen)
         # generic iterable of dense [B, N] batches
         tot = np.zeros(3)
@@ -273,10 +278,16 @@ def train_hybrid_vae(
     ignore_embeddings: bool = False,
     precision: str | None = None,
 ) -> None:
+    # under torchrun (WORLD_SIZE > 1): one process per GPU, user-batch data parallel over RCCL; batch_size is
+    # per GPU (the global batch is batch_size x world) and only rank 0 writes checkpoints and the history
+    group = init_from_env() if (device is None or str(device).startswith("cuda")) else None
+    main_rank = is_main(group)
     dev = _get_device(device)
-    logger.info(f"Using device: {dev}")
+    logger.info(f"Using device: {dev}" + (f" (rank {torch.distributed.get_rank()} of "
+                                           f"{torch.distributed.get_world_size()})" if group is not None else ""))
     output_path = Path(output_dir)
-    output_path.mkdir(parents=True, exist_ok=True)
+    if main_rank:
+        output_path.mkdir(parents=True, exist_ok=True)
 
     full_matrix, train_df, val_df, mappings = load_training_data(data_dir)
     user_to_idx, item_to_idx = mappings["user_to_idx"], mappings["item_to_idx"]
@@ -304,7 +315,7 @@ def train_hybrid_vae(
                               anneal_steps=anneal_steps)
     logger.info(f"Model: {sum(p.numel() for p in model.parameters()):,} params")
 
-    trainer = VAETrainer(model, dev, learning_rate, weight_decay, precision=precision)
+    trainer = VAETrainer(model, dev, learning_rate, weight_decay, precision=precision, process_group=group)
     best_val_loss, patience_counter = float("inf"), 0
     start_time = time.time()
     for epoch in range(epochs):
@@ -324,20 +335,22 @@ def train_hybrid_vae(
             patience_counter = 0
         else:
             patience_counter += 1
-        trainer.save_checkpoint(
-            output_path / f"checkpoint_epoch_{epoch + 1}.pth", epoch + 1, is_best,
-            extra={"train_metrics": train_metrics, "val_metrics": val_metrics,
-                   "model_config": {"n_items": n_items, "latent_dim": latent_dim, "hidden_dims": hidden_dims,
-                                    "beta": beta, "dropout": dropout}})
+        if main_rank:  # replicas are bit-identical: one writer
+            trainer.save_checkpoint(
+                output_path / f"checkpoint_epoch_{epoch + 1}.pth", epoch + 1, is_best,
+                extra={"train_metrics": train_metrics, "val_metrics": val_metrics,
+                       "model_config": {"n_items": n_items, "latent_dim": latent_dim, "hidden_dims": hidden_dims,
+                                        "beta": beta, "dropout": dropout}})
         if patience_counter >= patience:
             logger.info(f"Early stopping at epoch {epoch + 1}")
             break
 
     training_time = time.time() - start_time
-    with open(output_path / "training_history.json", "w") as f:
-        json.dump({"train_losses": trainer.train_losses, "val_losses": trainer.val_losses,
-                   "train_recon_losses": trainer.train_recon_losses, "train_kl_losses": trainer.train_kl_losses,
-                   "training_time_seconds": round(training_time, 2)}, f, indent=2)
+    if main_rank:
+        with open(output_path / "training_history.json", "w") as f:
+            json.dump({"train_losses": trainer.train_losses, "val_losses": trainer.val_losses,
+                       "train_recon_losses": trainer.train_recon_losses, "train_kl_losses": trainer.train_kl_losses,
+                       "training_time_seconds": round(training_time, 2)}, f, indent=2)
     logger.info(f"Training complete! Best val loss: {best_val_loss:.4f}")
     logger.info(f"Total training time: {training_time:.1f}s")
 
@@ -367,6 +380,8 @@ def main() -> None:
                      epochs=args.epochs, learning_rate=args.learning_rate, weight_decay=args.weight_decay,
                      beta=args.beta, dropout=args.dropout, use_annealing=args.use_annealing, patience=args.patience,
                      device=args.device, ignore_embeddings=args.ignore_embeddings, precision=args.precision)
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -1,9 +1,13 @@
 """Data-parallel fused training on the GPU: two ranks sharing cuda:0 over gloo (a one-GPU rehearsal of the
 RCCL path -- the same executor code, collectives staged through host memory).
 
-Checks that the replicas stay bit-identical through graph-captured epochs (the exchange runs between the two
-captured graphs of a step), that they learn, and that the merged first-layer gradient equals the mean of the
-ranks' row gradients.
+  * a 2-rank step over batches of B users equals a 1-rank step over their union of 2B users (dropout masks
+    and reparameterisation noise injected, the union's slices on each rank): losses, every parameter and both
+    Adam moments, up to the order of the dense reductions (the first-layer row gradient of the union is
+    rebuilt from the gathered (x, da) by the same kernels, in the union's batch order);
+  * replicas stay bit-identical through graph-captured epochs, over pre-sharded equal data and over the
+    shared-permutation sharding of the drop-in trainer (uneven last batch: one rank may have no users), and
+    they learn.
 """
 import os
 import socket
@@ -61,6 +65,133 @@ def _worker_body(rank, world, port, q):
            int(fused.step_dev.item())))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _step_worker(rank, world, port, q):
+    try:
+        _step_body(rank, world, port, q)
+    except BaseException:
+        import traceback
+        traceback.print_exc()
+        raise
+
+
+def _step_body(rank, world, port, q):
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path[:0] = [str(root / "recommendation-system_amd"), str(root), str(root / "tests" / "golden")]
+    import numpy as np
+    import torch.distributed as dist
+    from gen import synth_csr, synth_embeddings
+    from hvae.executor import FusedTrainer
+    from src.ml.model import HybridVAE
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n_users, n_items, d, L, Hd, B, p = 200, 700, 384, 64, [256], 24, 0.3
+    X = synth_csr(n_users, n_items, lam=5.0, seed=31)
+    E = synth_embeddings(n_items, d, seed=32)
+    g = torch.Generator().manual_seed(33)
+    union = torch.randperm(n_users, generator=g)[: world * B].int()
+    enc = (torch.rand(world * B, Hd[0], generator=g) >= p).float() / (1 - p)
+    proj = (torch.rand(world * B, d, generator=g) >= p).float() / (1 - p)
+    eps = torch.randn(world * B, L, generator=g)
+
+    def run(group, rows, sl):
+        torch.manual_seed(0)
+        model = HybridVAE(n_items, E, latent_dim=L, hidden_dims=Hd, dropout=p, beta=0.2).to(dev)
+        fused = FusedTrainer(model, dev, precision="bf16", seed=3, use_graphs=False, process_group=group)
+        data = fused.device_data(X, list(range(n_users)))
+        ext = {"enc_masks": [enc[sl].to(dev)], "proj_mask": proj[sl].to(dev), "eps": eps[sl].to(dev)}
+        losses = []
+        for _ in range(2):
+            losses.append(fused.step_batch(data, rows.to(dev), len(rows), 0.2, p, train=True, ext=ext).cpu().numpy())
+        torch.cuda.synchronize()
+        return losses, fused.flat.cpu().numpy(), fused.m.cpu().numpy(), fused.v.cpu().numpy()
+
+    mine = slice(rank * B, (rank + 1) * B)
+    dp = run(dist.group.WORLD, union[mine], mine)
+    ref = run(None, union, slice(0, world * B)) if rank == 0 else None
+    q.put((rank, dp, ref))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_step_equals_union_step(hip_device):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_step_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (_, (l0, f0, m0, v0), ref), (_, (l1, f1, m1, v1), _) = res
+    lr, fr, mr, vr = ref
+    assert (f0 == f1).all() and (m0 == m1).all() and (v0 == v1).all()  # replicas identical
+    import numpy as np
+    for s in range(2):  # the union batch's loss = mean of the two equal shares
+        np.testing.assert_allclose((l0[s] + l1[s]) / 2, lr[s], rtol=2e-5, atol=1e-6)
+    rel = lambda a, b: float(np.abs(a.astype(np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
+    assert rel(f0, fr) < 2e-5 and rel(m0, mr) < 2e-4 and rel(v0, vr) < 2e-4
+
+
+def _global_worker(rank, world, port, q):
+    try:
+        import sys
+        from pathlib import Path
+        root = Path(__file__).resolve().parents[1]
+        sys.path[:0] = [str(root / "recommendation-system_amd"), str(root), str(root / "tests" / "golden")]
+        import torch.distributed as dist
+        from gen import synth_csr, synth_embeddings
+        from hvae.executor import ConstBeta, FusedTrainer
+        from src.ml.model import HybridVAE
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        X = synth_csr(417, 900, seed=41)  # 417 = 6 x (2 x 32) + 33: a last global batch of 17 + 16
+        E = synth_embeddings(900, 128, seed=42)
+        torch.manual_seed(0)
+        model = HybridVAE(900, E, latent_dim=64, hidden_dims=[128], dropout=0.3, beta=0.2).to(dev)
+        fused = FusedTrainer(model, dev, precision="bf16", seed=5, use_graphs=True, process_group=dist.group.WORLD)
+        data = fused.device_data(X, list(range(417)))
+        data.dp_global = True
+        r = [fused.run_epoch(data, 32, True, ConstBeta(0.2), 0.3) for _ in range(3)]
+        torch.cuda.synchronize()
+        q.put((rank, r, fused.flat.cpu().numpy(), int(fused.step_dev.item())))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        traceback.print_exc()
+        raise
+
+
+def test_dp_global_sharding_epochs(hip_device):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_global_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    (_, ra, fa, sa), (_, rb, fb, sb) = res
+    assert sa == sb == 3 * 7  # 6 full global batches + the partial one, per epoch
+    assert ra == rb  # the union losses, all-reduced
+    assert (fa == fb).all()
+    assert ra[-1]["total_loss"] < ra[0]["total_loss"]
 
 
 def test_dp_two_ranks_one_gpu(hip_device):
