@@ -101,16 +101,23 @@ def _step_body(rank, world, port, q):
     eps = torch.randn(world * B, L, generator=g)
 
     def run(group, rows, sl):
+        from hvae import ops
         torch.manual_seed(0)
         model = HybridVAE(n_items, E, latent_dim=L, hidden_dims=Hd, dropout=p, beta=0.2).to(dev)
-        fused = FusedTrainer(model, dev, precision="bf16", seed=3, use_graphs=False, process_group=group)
+        # fp32 decoder: the bf16 sweep's P rounding depends on its item-split plan, which depends on the batch
+        # size (B vs 2B), a 1e-3 effect that would hide the exchange's own exactness
+        fused = FusedTrainer(model, dev, precision="fp32", seed=3, use_graphs=False, process_group=group)
         data = fused.device_data(X, list(range(n_users)))
         ext = {"enc_masks": [enc[sl].to(dev)], "proj_mask": proj[sl].to(dev), "eps": eps[sl].to(dev)}
-        losses = []
-        for _ in range(2):
-            losses.append(fused.step_batch(data, rows.to(dev), len(rows), 0.2, p, train=True, ext=ext).cpu().numpy())
+        losses = [fused.step_batch(data, rows.to(dev), len(rows), 0.2, p, train=True, ext=ext).cpu().numpy()]
+        # step 1's gradients (what clip + Adam consume): the small dense ones, the first layer's rows, the norm
+        rg = fused.dp.merged if fused.dp is not None else fused._bufs[(len(rows), True)].rg
+        w1 = torch.zeros(n_items, Hd[0], device=dev)
+        ops.rowgrad_to_dense(rg, w1)
+        grads = (fused.g_small.cpu().numpy(), w1.cpu().numpy(), float(fused.norm.item()))
+        losses.append(fused.step_batch(data, rows.to(dev), len(rows), 0.2, p, train=True, ext=ext).cpu().numpy())
         torch.cuda.synchronize()
-        return losses, fused.flat.cpu().numpy(), fused.m.cpu().numpy(), fused.v.cpu().numpy()
+        return losses, grads, fused.flat.cpu().numpy()
 
     mine = slice(rank * B, (rank + 1) * B)
     dp = run(dist.group.WORLD, union[mine], mine)
@@ -132,14 +139,21 @@ def test_dp_step_equals_union_step(hip_device):
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    (_, (l0, f0, m0, v0), ref), (_, (l1, f1, m1, v1), _) = res
-    lr, fr, mr, vr = ref
-    assert (f0 == f1).all() and (m0 == m1).all() and (v0 == v1).all()  # replicas identical
+    (_, (l0, g0, f0), ref), (_, (l1, g1, f1), _) = res
+    lr_, gr, fr = ref
+    assert (f0 == f1).all()  # replicas identical
     import numpy as np
     for s in range(2):  # the union batch's loss = mean of the two equal shares
-        np.testing.assert_allclose((l0[s] + l1[s]) / 2, lr[s], rtol=2e-5, atol=1e-6)
+        np.testing.assert_allclose((l0[s] + l1[s]) / 2, lr_[s], rtol=2e-5, atol=1e-6)
     rel = lambda a, b: float(np.abs(a.astype(np.float64) - b).max() / max(np.abs(b).max(), 1e-30))
-    assert rel(f0, fr) < 2e-5 and rel(m0, mr) < 2e-4 and rel(v0, vr) < 2e-4
+    # step 1's gradients: equal up to the order of the dense reductions over users (B + B vs 2B); the first
+    # layer's row gradient is rebuilt from the gathered (x, da) in the union's batch order
+    assert rel(g0[0], gr[0]) < 2e-5, rel(g0[0], gr[0])
+    assert rel(g0[1], gr[1]) < 2e-5, rel(g0[1], gr[1])
+    assert abs(g0[2] - gr[2]) <= 2e-5 * gr[2]
+    # parameters after two Adam steps: Adam turns a near-zero gradient's sign into a +-lr step, so compare
+    # within 2 lr per step of each other
+    assert float(np.abs(f0.astype(np.float64) - fr).max()) <= 2 * 2 * 1e-3 * (1 + 1e-3)
 
 
 def _global_worker(rank, world, port, q):

@@ -3,12 +3,12 @@
 The All_Beauty data cannot be fetched here, so the check runs on the All_Beauty-shaped planted-cluster
 dataset of tests/golden/gen.py (22,363 users x 12,101 items, d = 384) against
 tests/golden/ndcg_planted.json: NDCG@10 of the reference's own CPU trainer and evaluator
-(src/ml/train.py:199-332, src/ml/evaluate.py:294-340) over 3 training seeds, best config
+(src/ml/train.py:199-332, src/ml/evaluate.py:294-340) over 8 training seeds, best config
 (latent 128, hidden [512], dropout 0.3, beta 0.2, lr 1e-3, batch 64, 20 epochs), 1 + 99 negatives drawn
 with numpy seeded 1234 right before evaluation (so both sides rank the same candidate lists).
 Training randomness differs (dropout / reparameterisation draws), so parity is statistical: the
-mean over 3 seeds here must be within 0.004 of the reference mean (~3.6 sigma of the difference of
-two 3-seed means at the reference's seed spread of 0.0013).
+mean over 8 seeds here must be within north_star's 0.002 of the reference's 8-seed mean (the reference's
+seed spread is 0.0010, so 0.002 is ~4 sigma of the difference of two 8-seed means).
 """
 import json
 import sys
@@ -26,7 +26,7 @@ from gen import PLANTED_CONFIG, digest, synth_planted, write_planted_artifacts  
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.timeout(900)
+@pytest.mark.timeout(1200)
 @pytest.mark.parametrize("precision", [None, "fp8"])
 def test_ndcg_parity_planted(hip_device, tmp_path, precision):
     """precision None = the default bf16 decoder; "fp8" = the block-scaled e4m3 sweep (BASELINE configs[4])."""
@@ -40,7 +40,9 @@ def test_ndcg_parity_planted(hip_device, tmp_path, precision):
     assert d == fix["data_digest"], "planted dataset differs from the one the reference was run on"
     data, emb = write_planted_artifacts(tmp_path)
     got = []
-    for s in range(3):
+    n_seeds = 8
+    assert len(fix["runs"]) >= n_seeds, "the reference fixture must hold at least as many seeds"
+    for s in range(n_seeds):
         out = tmp_path / f"models_{s}"
         torch.manual_seed(s)
         np.random.seed(s)
@@ -54,4 +56,4 @@ def test_ndcg_parity_planted(hip_device, tmp_path, precision):
         print(f"[{precision or 'bf16'}] seed {s}: NDCG@10 {res[10]['ndcg']:.4f} HR@10 {res[10]['hit_ratio']:.4f}", flush=True)
     mean = float(np.mean(got))
     print(f"[{precision or 'bf16'}] NDCG@10 mean {mean:.4f} vs reference {fix['ndcg10_mean']:.4f} +- {fix['ndcg10_std']:.4f}")
-    assert abs(mean - fix["ndcg10_mean"]) < 0.004
+    assert abs(mean - fix["ndcg10_mean"]) < 0.002
