@@ -749,6 +749,22 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
 #ifndef DEC3_DMA
 #define DEC3_DMA 0
 #endif
+// diagnostic build (DEC3_STAMPS=1): per-wave s_memtime phase sums of the main loop, read back with
+// hvae_debug_dec3_stamps (never in a shipped build: the stamps' SMEM waits perturb the schedule)
+#ifndef DEC3_STAMPS
+#define DEC3_STAMPS 0
+#endif
+#if DEC3_STAMPS
+__device__ unsigned long long g_dec3_stamps[4096][8];
+#define DEC3_STAMP(i)                                         \
+  do {                                                        \
+    const unsigned long long n_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += n_ - st_prev;                                \
+    st_prev = n_;                                             \
+  } while (0)
+#else
+#define DEC3_STAMP(i) do {} while (0)
+#endif
 #ifndef DEC3_DMA_PRE
 #define DEC3_DMA_PRE 0  // (DEC3_DMA 0) pieces issued before GEMM1's first MFMA (0, 3, 6 = 11.07, 11.13, 11.19 ms)
 #endif
@@ -757,6 +773,9 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
 #endif
 #ifndef DEC3_G2_AHEAD
 #define DEC3_G2_AHEAD 2  // GEMM2 A operand d-blocks in flight
+#endif
+#ifndef DEC3_SM_VGPR
+#define DEC3_SM_VGPR 0
 #endif
 __host__ __device__ constexpr int d3_lds_bytes(int D) { return 3 * ((D / 128) * 8192) + 4 * 2048 + 4 * 1024; }
 
@@ -1001,13 +1020,24 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
   }
 
   // the loop is instantiated per D half (dh) so that every register pick of a half is static
+#if DEC3_STAMPS
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long st_prev = __builtin_amdgcn_s_memtime();
+#endif
   auto sweep = [&](auto dh_c) {
   constexpr int DHC = decltype(dh_c)::value;
   int cur = 0;
   for (int64_t t = t_beg; t < t_end; ++t) {
+    DEC3_STAMP(0);  // [0] end of the previous iteration -> here
+#if DEC3_SM_VGPR
+#pragma unroll
+    for (int r = 0; r < 8; ++r) asm volatile("" : "+v"(sm[r]));  // keep the loop-carried half in VGPRs
+#endif
     // [A(t)]: tile t + 1 has landed; the partner's partial half of S^T(t) is published
     if (DEC3_ABL != 1 && DEC3_ABL != 3) wait_vmcnt<0>();
+    DEC3_STAMP(1);  // [1] LDS-DMA wait
     if (DEC3_ABL != 2 && DEC3_ABL != 3) barrier();
+    DEC3_STAMP(2);  // [2] barrier A
     const int nxt = cur == NS - 1 ? 0 : cur + 1;
     const int64_t t_dma = min(t + 2, t_end - 1);
     const int s_dma = cur == 0 ? NS - 1 : cur - 1;
@@ -1047,9 +1077,11 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
         constexpr int PRE = DEC3_DMA == 0 ? DEC3_DMA_PRE : 0;
         if (kDma && g < P1 - PRE) issue_pieces(soff_dma, s_dma, PRE + g, PRE + g + 1, PRE == 0 && g == 0);
       });
+      DEC3_STAMP(3);  // [3] GEMM1 (+ softmax, DMA issue)
       // P(t) own half out; [B(t)]; the partner's partial half of S^T(t + 1) out; GEMM2(t), own half first
       if (DEC3_ABL != 4) *reinterpret_cast<uint4*>(xp + (w * 64 + lane) * 4) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
       if (DEC3_ABL != 2 && DEC3_ABL != 3) barrier();
+      DEC3_STAMP(4);  // [4] P out + barrier B
       if (DEC3_ABL != 4) {
         float* dst = xs + w * 512;  // the partner's half of the new partial (static registers)
 #pragma unroll
@@ -1066,10 +1098,12 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
         if (kDma && P1 + db / 2 < PW && (db & 1) == 0)
           issue_pieces(soff_dma, s_dma, P1 + db / 2, P1 + db / 2 + 1, false);
       });
+      DEC3_STAMP(5);  // [5] half-S out + GEMM2 own half
       gemm2_half(lds + cur * TB, 1 - DHC, __builtin_bit_cast(bf16x8, po), [&](int db) {
         const int i = P1 + (DB + db) / 2;
         if (kDma && i < PW && (db & 1) == 0) issue_pieces(soff_dma, s_dma, i, i + 1, false);
       });
+      DEC3_STAMP(6);  // [6] GEMM2 partner half
 #pragma unroll
       for (int r = 0; r < 8; ++r) sm[r] = s_new[8 * DHC + r];
     }
@@ -1078,6 +1112,12 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
   };
   if (dh == 0) sweep(std::integral_constant<int, 0>{});
   else sweep(std::integral_constant<int, 1>{});
+#if DEC3_STAMPS
+  if (lane == 0 && blockIdx.x * 4 + w < 4096) {
+    st_acc[7] = (unsigned long long)(t_end > t_beg ? t_end - t_beg : 0);
+    for (int i = 0; i < 8; ++i) g_dec3_stamps[blockIdx.x * 4 + w][i] = st_acc[i];
+  }
+#endif
 
   wait_vmcnt<0>();  // the last tile's LDS-DMA (a duplicate, never read) lands before the ring is released
 
@@ -2417,6 +2457,13 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
 }  // namespace hvae
 
 using namespace hvae;
+
+#if DEC3_STAMPS
+extern "C" int hvae_debug_dec3_stamps(void* out, size_t bytes) {  // diagnostic builds only (not in the ABI)
+  HVAE_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dec3_stamps), std::min(bytes, sizeof(g_dec3_stamps))));
+  return HVAE_OK;
+}
+#endif
 
 extern "C" int hvae_decoder_supported(int dtype, int64_t D) {
   if (dtype == HVAE_BF16) return D == 64 || D == 128 || D == 256 || D == 384 || (D == 768 && !dec_use_v1());
