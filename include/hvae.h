@@ -397,6 +397,24 @@ int hvae_rank_first(const float* scores, int64_t R, int64_t C, int32_t* rank, vo
 int hvae_topk(const float* scores, int64_t R, int64_t N, int64_t ld, const hvae_csr_batch* exclude,
               int64_t K, int32_t* idx, float* val, void* stream);
 
+/* Fused exact top-K over all N items without the [R, N] score matrix (full-ranking
+ * eval and the /recommend core: RecommendationEvaluator.get_user_recommendations,
+ * src/ml/evaluate.py:137-147; HybridVAE.recommend, src/ml/model.py:236-256; the
+ * /recommend handler, src/api/server.py:115-183, scores -> seen masked to -inf ->
+ * np.argsort(scores)[::-1][:top_k]). U [R, ldu] fp32 user vectors, E_bf16 the bf16
+ * [N, D] image (hvae_decoder_image's first part), E32 the fp32 [N, D] embeddings,
+ * e32_maxnorm = max_i ||E32_i|| (device scalar). A bf16 MFMA sweep keeps every item
+ * that can still be in a user's top-(K + |seen|) by a provable bound, then the
+ * candidates are rescored in fp32 and ordered (score desc, item desc), as hvae_topk.
+ * idx / val [R, K]; flag[r] = 1 marks rows the fused path could not certify (candidate
+ * overflow, fewer than K unseen items, K + |seen| > 256): the caller ranks those
+ * exactly (hvae_gemm_f32 + hvae_topk). D in {64, 128, 256, 384, 512, 768}, K <= 256. */
+size_t hvae_topk_fused_workspace(int64_t R, int64_t N, int64_t D, int64_t K);
+int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, const float* E32,
+                    const float* e32_maxnorm, int64_t N, int64_t D, const hvae_csr_batch* exclude,
+                    int64_t R, int64_t K, int32_t* idx, float* val, int32_t* flag, void* ws,
+                    size_t ws_bytes, void* stream);
+
 /* fp32 -> bf16 (round to nearest even) copy of the frozen embeddings. */
 int hvae_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 

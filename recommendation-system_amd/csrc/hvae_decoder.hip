@@ -30,6 +30,7 @@
 //     and b+8 share one), keeping the split's E slice L2-resident; a merge
 //     kernel combines the (m, l, O) partials.
 #include <algorithm>
+#include <array>
 #include <type_traits>
 
 #include "hvae_common.h"
@@ -777,6 +778,15 @@ __device__ unsigned long long g_dec3_stamps[4096][8];
 #ifndef DEC3_SM_VGPR
 #define DEC3_SM_VGPR 0
 #endif
+// barrier B: -1 = before GEMM2(t), k = after GEMM2's own-half MFMA min(k, D / 64 - 1); at the Syn-10M shard
+// (10 launches x 2 rounds, profiles/r02_dec3_bb.jsonl): -1 11.00 ms, 4 10.88, 8 10.89, last (11) 10.74
+#ifndef DEC3_BB
+#define DEC3_BB 99
+#endif
+// GEMM2(t)'s first A reads: 0 = at its start, k = in GEMM1's MFMA pair NG - k (0: 11.00 ms, 1: 10.99 alone)
+#ifndef DEC3_G2PRE
+#define DEC3_G2PRE 1
+#endif
 __host__ __device__ constexpr int d3_lds_bytes(int D) { return 3 * ((D / 128) * 8192) + 4 * 2048 + 4 * 1024; }
 
 template <int D, bool WITH_O>
@@ -792,6 +802,7 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
   constexpr int TB = NSEG * 8192;
   constexpr int PW = NSEG * 8 / 4;      // 1-KiB LDS-DMA pieces per wave per tile
   constexpr int NS = 3;
+  constexpr int BBI = DEC3_BB < 0 ? -1 : (DEC3_BB < DB ? DEC3_BB : DB - 1);
   static_assert(D % 128 == 0 && KS % 2 == 0 && NG >= 12 && PW <= NG && d3_lds_bytes(D) <= 160 * 1024,
                 "k_dec3_bf16 shape");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -925,31 +936,40 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
   for (int d = 0; d < (WITH_O ? DB : 1); ++d)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
-  // one k-step (items 16 kh .. 16 kh + 15) of GEMM2 over all d-blocks: O^T[DW][32 users] += E^T P^T
-  auto gemm2_half = [&](const unsigned char* buf, int kh, const bf16x8& pf, auto&& fill) {
+  // GEMM2(t) over both k-steps (items 16 kh .. 16 kh + 15), own half first: O^T[DW][32 users] += E^T P^T.
+  // MFMA i (0 .. 2 DB - 1) is k-step kh(i) = i < DB ? own : partner, d-block i % DB; the transposed A reads run
+  // BH MFMAs ahead across the two halves, and the first BH (g2_pre) can go out before the loop (in GEMM1's
+  // last gaps). pf_own is in registers; pf_par is read from LDS in fill(i) for some i < DB.
+  constexpr int BH = DEC3_G2_AHEAD;
+  auto rdT = [&](const unsigned char* buf, int kown, int i) {
+    const int kh = i < DB ? kown : 1 - kown, db = i % DB;
+    const unsigned char* t = buf + cseg + (kh << 12);
+    auto* p0 = (__attribute__((address_space(3))) s16x4*)(void*)(t + laneT0 + ((db >> 2) << 13) + ((db & 3) << 9));
+    auto* p1 = (__attribute__((address_space(3))) s16x4*)(void*)(t + laneT1 + (1 << 11) + ((db >> 2) << 13) +
+                                                                 ((db & 3) << 9));
+    return std::array<s16x4, 2>{__builtin_amdgcn_ds_read_tr16_b64_v4i16(p0), __builtin_amdgcn_ds_read_tr16_b64_v4i16(p1)};
+  };
+  auto g2_pre = [&](const unsigned char* buf, int kown, std::array<s16x4, 2> (&n)[BH]) {
+#pragma unroll
+    for (int j = 0; j < BH; ++j) n[j] = rdT(buf, kown, j);
+  };
+  auto gemm2 = [&](const unsigned char* buf, int kown, std::array<s16x4, 2> (&n)[BH], const bf16x8& pf_own,
+                   const uint4& pf_par,
+                   auto&& fill) {
     if constexpr (WITH_O) {
-      const unsigned char* t0 = buf + cseg + laneT0 + (kh << 12);
-      const unsigned char* t1 = buf + cseg + laneT1 + (kh << 12);
-      auto rdT = [&](int db, int j) {
-        auto* p = (__attribute__((address_space(3))) s16x4*)(void*)((j ? t1 : t0) + (j << 11) + ((db >> 2) << 13) +
-                                                                     ((db & 3) << 9));
-        return __builtin_amdgcn_ds_read_tr16_b64_v4i16(p);
-      };
-      // the transposed reads of a d-block go out BH d-blocks before its MFMA (one ahead left each MFMA
-      // waiting on the LDS latency right after the previous one issued)
-      constexpr int BH = DEC3_G2_AHEAD;
-      s16x4 n[BH][2];
 #pragma unroll
-      for (int j = 0; j < BH; ++j) { n[j][0] = rdT(j, 0); n[j][1] = rdT(j, 1); }
-#pragma unroll
-      for (int db = 0; db < DB; ++db) {
-        const s16x4 c0 = n[db % BH][0], c1 = n[db % BH][1];
-        if (db + BH < DB) { n[db % BH][0] = rdT(db + BH, 0); n[db % BH][1] = rdT(db + BH, 1); }
-        const s16x8 a = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2], c1[3]};
-        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pf, o[db], 0, 0, 0);
-        fill(db);
+      for (int i = 0; i < 2 * DB; ++i) {
+        const std::array<s16x4, 2> c = n[i % BH];
+        if (i + BH < 2 * DB) n[i % BH] = rdT(buf, kown, i + BH);
+        const s16x8 a = {c[0][0], c[0][1], c[0][2], c[0][3], c[1][0], c[1][1], c[1][2], c[1][3]};
+        const bf16x8 pf = i < DB ? pf_own : __builtin_bit_cast(bf16x8, pf_par);
+        o[i % DB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pf, o[i % DB], 0, 0, 0);
+        fill(i);
         __builtin_amdgcn_sched_barrier(0);
       }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2 * DB; ++i) fill(i);  // the exchange and any LDS-DMA placed in GEMM2 still run
     }
   };
   // this wave's half of a partial S^T tile: rows 8 dh .. 8 dh + 7 of the accumulator (items 16 dh ..);
@@ -1052,6 +1072,7 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
       float pv[8];
       uint32_t pk[4];
       const bool tail = t == ntiles - 1 && (N % kBfTI) != 0;  // wave-uniform
+      std::array<s16x4, 2> n2[BH];
       f32x16 s_new = gemm1(lds + nxt * TB, [&] {
         if (kDma && DEC3_DMA == 0) issue_pieces(soff_dma, s_dma, 0, DEC3_DMA_PRE, true);
       }, [&](int g) {
@@ -1076,32 +1097,34 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
         }
         constexpr int PRE = DEC3_DMA == 0 ? DEC3_DMA_PRE : 0;
         if (kDma && g < P1 - PRE) issue_pieces(soff_dma, s_dma, PRE + g, PRE + g + 1, PRE == 0 && g == 0);
+        if (DEC3_G2PRE > 0 && g == NG - DEC3_G2PRE) g2_pre(lds + cur * TB, DHC, n2);  // GEMM2(t)'s first reads
       });
       DEC3_STAMP(3);  // [3] GEMM1 (+ softmax, DMA issue)
-      // P(t) own half out; [B(t)]; the partner's partial half of S^T(t + 1) out; GEMM2(t), own half first
+      // P(t) own half out; [B(t)] (before GEMM2, or after its own-half MFMA DEC3_BB); then the partner's
+      // partial half of S^T(t + 1) out and the partner's P half in; GEMM2(t), own half first
       if (DEC3_ABL != 4) *reinterpret_cast<uint4*>(xp + (w * 64 + lane) * 4) = make_uint4(pk[0], pk[1], pk[2], pk[3]);
-      if (DEC3_ABL != 2 && DEC3_ABL != 3) barrier();
-      DEC3_STAMP(4);  // [4] P out + barrier B
-      if (DEC3_ABL != 4) {
-        float* dst = xs + w * 512;  // the partner's half of the new partial (static registers)
-#pragma unroll
-        for (int r4 = 0; r4 < 2; ++r4) {
-          const int r = 8 * (1 - DHC) + 4 * r4;
-          *reinterpret_cast<float4*>(dst + r4 * 256 + lane * 4) =
-              make_float4(s_new[r], s_new[r + 1], s_new[r + 2], s_new[r + 3]);
-        }
-      }
-      const bf16x8 pown = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
       uint4 po = make_uint4(0u, 0u, 0u, 0u);
-      gemm2_half(lds + cur * TB, DHC, pown, [&](int db) {
-        if (db == 0 && DEC3_ABL != 4) po = *reinterpret_cast<const uint4*>(xp + (pw * 64 + lane) * 4);
-        if (kDma && P1 + db / 2 < PW && (db & 1) == 0)
-          issue_pieces(soff_dma, s_dma, P1 + db / 2, P1 + db / 2 + 1, false);
-      });
-      DEC3_STAMP(5);  // [5] half-S out + GEMM2 own half
-      gemm2_half(lds + cur * TB, 1 - DHC, __builtin_bit_cast(bf16x8, po), [&](int db) {
-        const int i = P1 + (DB + db) / 2;
-        if (kDma && i < PW && (db & 1) == 0) issue_pieces(soff_dma, s_dma, i, i + 1, false);
+      auto exch_b = [&] {
+        if (DEC3_ABL != 2 && DEC3_ABL != 3) barrier();
+        if (DEC3_ABL != 4) {
+          float* dst = xs + w * 512;  // the partner's half of the new partial (static registers)
+#pragma unroll
+          for (int r4 = 0; r4 < 2; ++r4) {
+            const int r = 8 * (1 - DHC) + 4 * r4;
+            *reinterpret_cast<float4*>(dst + r4 * 256 + lane * 4) =
+                make_float4(s_new[r], s_new[r + 1], s_new[r + 2], s_new[r + 3]);
+          }
+          po = *reinterpret_cast<const uint4*>(xp + (pw * 64 + lane) * 4);
+        }
+      };
+      if (BBI < 0) exch_b();
+      DEC3_STAMP(4);  // [4] P out + barrier B
+      if (DEC3_G2PRE == 0) g2_pre(lds + cur * TB, DHC, n2);
+      const bf16x8 pown = __builtin_bit_cast(bf16x8, make_uint4(pk[0], pk[1], pk[2], pk[3]));
+      gemm2(lds + cur * TB, DHC, n2, pown, po, [&](int i) {
+        if (BBI >= 0 && i == BBI) exch_b();
+        if (kDma && P1 + i / 2 < PW && (i & 1) == 0) issue_pieces(soff_dma, s_dma, P1 + i / 2, P1 + i / 2 + 1, false);
+        if (i == DB - 1) DEC3_STAMP(5);  // [5] half-S out + GEMM2 own half
       });
       DEC3_STAMP(6);  // [6] GEMM2 partner half
 #pragma unroll

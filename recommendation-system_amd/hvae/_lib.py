@@ -129,6 +129,9 @@ SIGNATURES = {
     "hvae_score_candidates": (cint, [vp, i64, vp, vp, i64, vp, i64, i64, vp, vp]),
     "hvae_rank_first": (cint, [vp, i64, i64, vp, vp]),
     "hvae_topk": (cint, [vp, i64, i64, i64, P(CsrBatch), i64, vp, vp, vp]),
+    "hvae_topk_fused_workspace": (sz, [i64, i64, i64, i64]),
+    "hvae_topk_fused": (cint, [vp, i64, vp, vp, vp, i64, i64, P(CsrBatch), i64, i64, vp, vp, vp, vp, sz,
+                               vp]),
     "hvae_cast_bf16": (cint, [vp, vp, i64, vp]),
     "hvae_csr_batch_pack": (cint, [P(CsrBatch), f32, vp, vp, vp, i64, vp]),
 }

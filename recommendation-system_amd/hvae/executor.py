@@ -210,11 +210,12 @@ class _StepBuffers:
             need.append(L_.hvae_colsum_workspace(B, n))
         for hd in H:
             need.append(L_.hvae_ln_gelu_drop_bwd_workspace(B, hd))
-        gemms = [(2 * L, H[-1], B), (B, H[-1], 2 * L)]
+        # (m, n, k) of every split-K-capable GEMM of the step: forward, data- and weight-gradient products
+        gemms = [(B, 2 * L, H[-1]), (2 * L, H[-1], B), (B, H[-1], 2 * L)]
         if lay.has_proj:
-            gemms += [(d, d, B), (d, L, B), (B, d, d), (B, L, d)]
+            gemms += [(B, d, L), (B, d, d), (d, d, B), (d, L, B), (B, d, d), (B, L, d)]
         for k in range(1, len(H)):
-            gemms += [(H[k], H[k - 1], B), (B, H[k - 1], H[k])]
+            gemms += [(B, H[k], H[k - 1]), (H[k], H[k - 1], B), (B, H[k - 1], H[k])]
         for (m_, n_, k_) in gemms:
             need.append(L_.hvae_gemm_f32_workspace(m_, n_, k_))
         self.ws = torch.empty(max(int(max(need)), 256), dtype=torch.uint8, device=dev)
@@ -636,6 +637,10 @@ class FusedTrainer:
                                            self.layout.hidden[0], torch.cuda.current_stream(self.device).cuda_stream),
               "adam_lazy_flush")
 
+    def _hyper(self) -> tuple:
+        """The optimizer constants a captured step bakes in (part of its graph key)."""
+        return (self.lr, self.betas, self.eps, self.wd, self.max_norm)
+
     def mark_all_current(self):
         """Every row has had every step applied (after an external dense update of W1t)."""
         self.last_step.copy_(self.step_dev.to(torch.int32).expand_as(self.last_step))
@@ -712,7 +717,7 @@ class FusedTrainer:
             beta = beta_fn(bi)
             bf = self._buffers(B, data.max_batch_nnz(B), train)
             if self.use_graphs and const_beta is not None:
-                if not self._replay(bf, data, train, beta, p_drop, bi, (beta, p_drop)):
+                if not self._replay(bf, data, train, beta, p_drop, bi, (beta, p_drop) + self._hyper()):
                     continue
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
@@ -800,7 +805,7 @@ class FusedTrainer:
             beta = beta_fn(bi)
             bf = self._buffers(B, W * cap, True)
             if self.use_graphs and const_beta is not None:
-                if not self._replay(bf, data, True, beta, p_drop, bi, (beta, p_drop, cap, 1.0 / W)):
+                if not self._replay(bf, data, True, beta, p_drop, bi, (beta, p_drop) + self._hyper() + (cap, 1.0 / W)):
                     continue
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), True, beta, p_drop, advance=B,

@@ -434,3 +434,35 @@ def topk(scores: torch.Tensor, k: int, exclude: Csr | None = None):
     check(lib().hvae_topk(ptr(scores), R, N, scores.stride(0), exclude.ref if exclude is not None else None, k,
                           ptr(idx), ptr(val), stream_of(scores)), "hvae_topk")
     return idx, val
+
+
+def topk_fused(U: torch.Tensor, E_img: "DecoderImage", E32: torch.Tensor, e32_maxnorm: torch.Tensor, k: int,
+               exclude: Csr | None = None, with_flags: bool = False):
+    """Exact top-k of U E32^T per row (score desc, ties -> larger index first; `exclude`'s items of each row
+    left out) without the [R, N] score matrix (hvae_topk_fused). Rows the fused path flags are ranked by the
+    exact path (hvae_gemm_f32 scores + hvae_topk) for those rows only. Returns idx int32 [R, k], val [R, k]
+    (and the flags when with_flags)."""
+    require_hip(U, E32, e32_maxnorm)
+    assert U.stride(1) == 1 and E32.is_contiguous()
+    assert exclude is None or exclude.rows_offset is None
+    R, D = U.shape
+    N = E32.shape[0]
+    idx = torch.empty(R, k, dtype=torch.int32, device=U.device)
+    val = torch.empty(R, k, device=U.device)
+    flag = torch.empty(R, dtype=torch.int32, device=U.device)
+    ws = workspace(U.device, lib().hvae_topk_fused_workspace(R, N, D, k))
+    check(lib().hvae_topk_fused(ptr(U), U.stride(0), ptr(E_img.bf16), ptr(E32), ptr(e32_maxnorm), N, D,
+                                exclude.ref if exclude is not None else None, R, k, ptr(idx), ptr(val), ptr(flag),
+                                ptr(ws), ws.numel(), stream_of(U)), "hvae_topk_fused")
+    bad = torch.nonzero(flag).flatten()
+    if bad.numel():
+        rows = bad.to(torch.int32)
+        S = gemm(U.index_select(0, bad), E32.t())
+        ex = None
+        if exclude is not None:
+            sel = exclude.rows.index_select(0, bad) if exclude.rows is not None else rows
+            ex = Csr(exclude.row_ptr, exclude.col_idx, exclude.vals, exclude.n_items, rows=sel.contiguous())
+        i2, v2 = topk(S, k, exclude=ex)
+        idx.index_copy_(0, bad, i2)
+        val.index_copy_(0, bad, v2)
+    return (idx, val, flag) if with_flags else (idx, val)

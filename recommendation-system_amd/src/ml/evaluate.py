@@ -162,13 +162,14 @@ class RecommendationEvaluator:
         return idx[0], val[0]
 
     def _topk(self, users: np.ndarray, k: int, exclude_seen: bool = True):
+        """Top-k of a batch of users over all items (seen ones excluded): the fused top-K, no [B, N] scores."""
         with torch.no_grad():
-            S = self._scores(users)
+            u = self._user_vectors(users)
             excl = None
             if exclude_seen:
                 rows = torch.as_tensor(np.asarray(users, np.int32), device=self.device)
                 excl = ops.Csr(self._csr.row_ptr, self._csr.col_idx, self._csr.vals, self.n_items, rows=rows)
-            idx, val = ops.topk(S, k, exclude=excl)
+            idx, val = self.model.topk_scores(u, k, exclude=excl)
         return idx.cpu().numpy().astype(np.int64), val.cpu().numpy()
 
     def evaluate_user_with_negatives(self, user_idx: int, test_item_idx: int, n_negatives: int = 99,

@@ -167,16 +167,35 @@ class HybridVAE(nn.Module):
         return mu
 
     def recommend(self, user_embedding: torch.Tensor, top_k: int = 10) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Exact top-k over all items (ties: larger item index first)."""
+        """Exact top-k over all items (ties: larger item index first) -- reference model.py:236-256's
+        torch.topk(decode(z)). The [B, N] scores are never formed: the fused bf16-shortlist / fp32-rescore
+        top-K (hvae_topk_fused) ranks u = projection(z) against E."""
         with torch.no_grad():
-            scores = self.decode(user_embedding)
-            squeeze = scores.dim() == 1
-            s2 = scores.reshape(-1, scores.shape[-1]).contiguous().clone()
-            idx, val = ops.topk(s2, top_k)
-            idx, val = idx.long(), val
+            squeeze = user_embedding.dim() == 1
+            z = user_embedding.reshape(-1, user_embedding.shape[-1])
+            u = self.projection_layer(z).contiguous()
+            idx, val = self.topk_scores(u, top_k)
+            idx = idx.long()
             if squeeze:
                 idx, val = idx[0], val[0]
         return idx, val
+
+    def topk_scores(self, u: torch.Tensor, k: int, exclude: "ops.Csr | None" = None):
+        """Exact top-k of u E^T per row (exclude: CSR rows of items left out), fused where hvae_topk_fused covers
+        the shape (k <= 256, d in 64..768), else through the fp32 score matrix + hvae_topk (both on the GPU)."""
+        E = self.item_embeddings.detach()
+        d = E.shape[1]
+        if k <= 256 and d in (64, 128, 256, 384, 512, 768) and k <= E.shape[0]:
+            key = (E.data_ptr(), E.shape)
+            cache = getattr(self, "_topk_cache", None)
+            if cache is None or cache[0] != key:
+                E32 = E.contiguous()
+                cache = (key, E32, ops.decoder_image(E32), ops.row_norm_max(E32))
+                self._topk_cache = cache
+            _, E32, img, emax = cache
+            return ops.topk_fused(u, img, E32, emax, k, exclude=exclude)
+        S = ops.gemm(u, E.t())
+        return ops.topk(S, k, exclude=exclude)
 
     # -------------------------------------------------- fused eval path ---
     @torch.no_grad()

@@ -107,6 +107,37 @@ class HipAdam(torch.optim.Optimizer):
         self._sync_state()
         return super().state_dict()
 
+    def load_state_dict(self, state_dict):
+        """torch.optim.Adam.load_state_dict, then the loaded moments and step count become the fused state
+        (m, v copied into the flat buffers, step_dev set, every W1t row marked current at that step) and the
+        loaded hyper-parameters the fused step's (resume: reference src/ml/evaluate.py:273-291 loads the same
+        checkpoint dict)."""
+        super().load_state_dict(state_dict)
+        self.fused.flush()  # rows behind the current step catch up before their moments are replaced
+        step = None
+        for p, (m, v) in self._moments.items():
+            st = self.state.get(p)
+            if not st:
+                continue
+            m.copy_(st["exp_avg"])
+            v.copy_(st["exp_avg_sq"])
+            step = int(float(st["step"]))
+            self.state[p] = {"step": torch.tensor(float(step)), "exp_avg": m, "exp_avg_sq": v}
+        if step is not None:
+            self.fused.step_dev.fill_(step)
+            self.fused.host_step = step
+            self.fused._check_steps(0)
+        self.fused.mark_all_current()
+        self.sync_hyper()
+
+    def sync_hyper(self):
+        """param_groups[0]'s lr / betas / eps / weight_decay -> the fused step (an LR scheduler's change is seen
+        by the next epoch; captured graphs are keyed on these values and re-captured)."""
+        g0 = self.param_groups[0]
+        f = self.fused
+        f.lr, f.betas, f.eps, f.wd = float(g0["lr"]), tuple(float(b) for b in g0["betas"]), float(g0["eps"]), \
+            float(g0["weight_decay"])
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
@@ -163,6 +194,7 @@ class VAETrainer:
         return ConstBeta(m.beta)
 
     def _run(self, loader, train: bool) -> dict[str, float]:
+        self.optimizer.sync_hyper()
         p_drop = float(self.model.dropout)
         beta_fn = self._beta_fn() if train else ConstBeta(self.model.beta)
         ds = getattr(loader, "dataset", None)

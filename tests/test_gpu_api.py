@@ -166,3 +166,53 @@ def test_evaluator_matches_reference_protocol(golden, hip_device):
     idx, val = ev._topk(users[:8], 20, True)
     np.testing.assert_array_equal(idx, golden["g4_full_top20"])
     np.testing.assert_allclose(val, golden["g4_full_top20_scores"], rtol=1e-5, atol=1e-5)
+
+
+def test_resume_from_checkpoint_is_bitwise(hip_device, tmp_path):
+    """save_checkpoint -> HybridVAE.load_state_dict + optimizer.load_state_dict -> one more epoch equals the
+    uninterrupted run bit for bit (params, Adam moments, step). Reference resume path: src/ml/train.py:126-145,
+    src/ml/evaluate.py:273-291; torch.optim.Adam.load_state_dict semantics."""
+    from src.ml.model import HybridVAE
+    from src.ml.train import UserInteractionDataset, VAETrainer
+    X = synth_csr(200, 300, seed=21)
+    E = synth_embeddings(300, 128, seed=22)
+    loader = torch.utils.data.DataLoader(UserInteractionDataset(X), batch_size=32, shuffle=False)
+
+    def trainer():
+        torch.manual_seed(0)  # same init and the same Philox seed for dropout / eps
+        return VAETrainer(HybridVAE(300, E, latent_dim=64, hidden_dims=[128], dropout=0.3, beta=0.2), hip_device,
+                          lr=1e-3)
+
+    a = trainer()
+    a.train_epoch(loader)
+    a.save_checkpoint(tmp_path / "c.pth", 1)
+    a.train_epoch(loader)
+    b = trainer()
+    ck = torch.load(tmp_path / "c.pth", map_location=hip_device, weights_only=True)
+    b.model.load_state_dict(ck["model_state_dict"])
+    b.optimizer.load_state_dict(ck["optimizer_state_dict"])
+    sd = b.optimizer.state_dict()
+    assert int(sd["state"][0]["step"]) == 7  # ceil(200 / 32) steps in the first epoch
+    b.train_epoch(loader)
+    for t in ("flat", "m", "v", "step_dev"):
+        assert torch.equal(getattr(a.fused, t), getattr(b.fused, t)), t
+
+
+def test_optimizer_lr_change_reaches_fused_step(hip_device):
+    """A change of optimizer.param_groups[0]['lr'] (an LR scheduler) is used by the next epoch's fused Adam."""
+    from src.ml.model import HybridVAE
+    from src.ml.train import UserInteractionDataset, VAETrainer
+    X = synth_csr(128, 300, seed=23)
+    E = synth_embeddings(300, 128, seed=24)
+    loader = torch.utils.data.DataLoader(UserInteractionDataset(X), batch_size=32, shuffle=False)
+    outs = []
+    for lr_second in (1e-3, 1e-4):
+        torch.manual_seed(0)
+        t = VAETrainer(HybridVAE(300, E, latent_dim=64, hidden_dims=[128], dropout=0.3, beta=0.2), hip_device,
+                       lr=1e-3)
+        t.train_epoch(loader)
+        t.optimizer.param_groups[0]["lr"] = lr_second
+        t.train_epoch(loader)
+        assert t.fused.lr == lr_second
+        outs.append(t.fused.flat.clone())
+    assert not torch.equal(outs[0], outs[1])

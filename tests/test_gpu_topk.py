@@ -1,0 +1,112 @@
+"""Fused exact top-K (hvae_topk_fused: bf16 MFMA shortlist + fp32 rescore, no [R, N] score matrix) against a
+float64 ranking of the same fp32 inputs.
+
+Reference semantics: RecommendationEvaluator.get_user_recommendations (src/ml/evaluate.py:137-147) and the
+/recommend handler (src/api/server.py:115-183): scores = u E^T, seen items -> -inf, argsort descending, first
+top_k. Indices must be identical except between items whose float64 scores are within fp32 rounding of each
+other (the reference's own fp32 sgemm cannot order those either); returned scores equal the float64 score of the
+returned item to 2e-6 relative."""
+import numpy as np
+import pytest
+import torch
+
+from gen import synth_csr, synth_embeddings
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(hip_device, R, N, D, seed, scale=4.0):
+    from hvae import ops
+    E = torch.as_tensor(synth_embeddings(N, D, seed=seed))
+    g = torch.Generator().manual_seed(seed + 1)
+    U = torch.randn(R, D, generator=g) * (scale / D ** 0.5)
+    Ed = E.to(hip_device)
+    img = ops.decoder_image(Ed)
+    emax = ops.row_norm_max(Ed)
+    return U, E, U.to(hip_device), Ed, img, emax
+
+
+def _check(idx, val, U, E, k, seen=None):
+    S = U.double() @ E.double().t()
+    if seen is not None:
+        for r, items in enumerate(seen):
+            S[r, items] = -np.inf
+    idx = idx.cpu().long()
+    val = val.cpu().double()
+    tol = 2e-6 * S.abs().max().item()
+    for r in range(S.shape[0]):
+        order = sorted(range(S.shape[1]), key=lambda i: (-S[r, i].item(), -i))[:k] if S.shape[1] <= 4096 else None
+        if order is None:
+            top = torch.topk(S[r], k + 16)
+            cand = sorted(zip(top.values.tolist(), top.indices.tolist()), key=lambda t: (-t[0], -t[1]))
+            order = [i for _, i in cand[:k]]
+        got = idx[r].tolist()
+        assert len(set(got)) == k, r
+        for j in range(k):
+            if got[j] != order[j]:
+                assert abs(S[r, got[j]].item() - S[r, order[j]].item()) <= tol, (r, j, got[j], order[j])
+            assert abs(val[r, j].item() - S[r, got[j]].item()) <= tol, (r, j)
+        if seen is not None:
+            assert not set(got) & set(seen[r].tolist()), r
+
+
+@pytest.mark.parametrize("R,N,D,k", [(64, 12101, 384, 10), (300, 100000, 384, 20), (37, 5003, 768, 50),
+                                     (9, 2000, 128, 100), (130, 30011, 256, 10), (33, 777, 64, 5),
+                                     (40, 20000, 512, 16)])
+def test_topk_fused_exact(hip_device, R, N, D, k):
+    from hvae import ops
+    U, E, Ud, Ed, img, emax = _case(hip_device, R, N, D, seed=N + D)
+    idx, val, flag = ops.topk_fused(Ud, img, Ed, emax, k, with_flags=True)
+    assert int(flag.sum()) == 0  # the fused path certified every row itself
+    _check(idx, val, U, E, k)
+
+
+@pytest.mark.parametrize("R,N,D,k", [(64, 12101, 384, 10), (50, 40000, 768, 20)])
+def test_topk_fused_exclude_seen(hip_device, R, N, D, k):
+    """exclude_seen: K_u = k + |seen_u| shortlist, seen items removed before ranking (server.py:152-155)."""
+    from hvae import ops
+    U, E, Ud, Ed, img, emax = _case(hip_device, R, N, D, seed=7 * N)
+    X = synth_csr(R, N, lam=15.0, seed=N)
+    csr = ops.csr_from_scipy(X, hip_device)
+    rows = torch.arange(R, dtype=torch.int32, device=hip_device)
+    ex = ops.Csr(csr.row_ptr, csr.col_idx, csr.vals, N, rows=rows)
+    idx, val, flag = ops.topk_fused(Ud, img, Ed, emax, k, exclude=ex, with_flags=True)
+    assert int(flag.sum()) == 0
+    seen = [torch.as_tensor(X[r].indices.astype(np.int64)) for r in range(R)]
+    _check(idx, val, U, E, k, seen)
+    # the same as the exact score-matrix path (hvae_gemm_f32 + hvae_topk)
+    S = ops.gemm(Ud, Ed.t())
+    i2, _ = ops.topk(S, k, exclude=ex)
+    assert (idx.cpu() == i2.cpu()).float().mean() > 0.99
+
+
+def test_topk_fused_flagged_rows_take_the_exact_path(hip_device):
+    """Rows the fused kernel cannot certify (here: more seen items than the shortlist heap, and an all-seen row
+    leaving fewer than k items) are flagged and ranked by the exact path; the answer stays exact."""
+    from hvae import ops
+    R, N, D, k = 6, 3000, 128, 8
+    U, E, Ud, Ed, img, emax = _case(hip_device, R, N, D, seed=5)
+    from scipy.sparse import csr_matrix
+    rng = np.random.default_rng(0)
+    rows_l, cols_l = [], []
+    sizes = [3, 400, 0, 10, 2995, 260]  # row 1: 400 + k > 256 -> flagged; row 4: 5 unseen < k -> flagged
+    for r, s in enumerate(sizes):
+        c = rng.choice(N, s, replace=False)
+        rows_l += [r] * s
+        cols_l += c.tolist()
+    X = csr_matrix((np.ones(len(rows_l), np.float32), (rows_l, cols_l)), shape=(R, N))
+    csr = ops.csr_from_scipy(X, hip_device)
+    ex = ops.Csr(csr.row_ptr, csr.col_idx, csr.vals, N, rows=torch.arange(R, dtype=torch.int32, device=hip_device))
+    idx, val, flag = ops.topk_fused(Ud, img, Ed, emax, k, exclude=ex, with_flags=True)
+    f = flag.cpu().tolist()
+    assert f[1] == 1 and f[4] == 1 and f[5] == 1 and f[0] == 0 and f[2] == 0 and f[3] == 0
+    X.sort_indices()
+    seen = [torch.as_tensor(X[r].indices.astype(np.int64)) for r in range(R)]
+    ok = [r for r in range(R) if r != 4]
+    _check(idx[ok], val[ok], U[ok], E, k, [seen[r] for r in ok])
+    # row 4 has 5 unseen items: those 5 first (exact order), then -inf
+    S4 = (U[4].double() @ E.double().t())
+    S4[seen[4]] = -np.inf
+    top5 = sorted(range(N), key=lambda i: (-S4[i].item(), -i))[:5]
+    assert idx[4, :5].cpu().tolist() == top5
+    assert torch.isinf(val[4, 5:]).all()

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from gen import TRAIN_CONFIGS, synth_csr, synth_embeddings
+from gen import EVAL_CONFIG, TRAIN_CONFIGS, synth_csr, synth_embeddings
 from oracle import ref_cpu as R
 
 pytestmark = pytest.mark.gpu
@@ -43,16 +43,20 @@ def _ext(golden, name, step, c, device):
     return ext
 
 
-@pytest.mark.parametrize("name", sorted(TRAIN_CONFIGS))
-def test_fused_step_matches_reference(golden, hip_device, name):
+def _step_errors(golden, hip_device, name, precision):
+    """Two fused steps with the reference's masks and noise injected; the largest relative deviation from golden
+    G2 of each compared quantity (losses, clip norm, pre-clip grads of step 1, params / m / v after step 2)."""
     from hvae import ops
-    c, X, E, model, fused, data = _build(name, hip_device)
+    c, X, E, model, fused, data = _build(name, hip_device, precision)
     B = c["n_users"]
+    err = {"loss": 0.0, "norm": 0.0}
     for step in (1, 2):
         loss3 = fused.step_batch(data, None, B, c["beta"], c["dropout"], train=True,
                                  ext=_ext(golden, name, step, c, hip_device))
-        np.testing.assert_allclose(loss3.cpu().numpy(), golden[f"g2{name}_loss"][step - 1], rtol=2e-5, atol=1e-6)
-        assert abs(fused.norm.item() - golden[f"g2{name}_norm"][step - 1]) <= 2e-5 * golden[f"g2{name}_norm"][step - 1]
+        ref = np.asarray(golden[f"g2{name}_loss"][step - 1])
+        err["loss"] = max(err["loss"], float(np.max(np.abs(loss3.cpu().numpy() - ref) / np.abs(ref))))
+        nr = golden[f"g2{name}_norm"][step - 1]
+        err["norm"] = max(err["norm"], abs(fused.norm.item() - nr) / nr)
         if step == 1:
             # pre-clip gradients (the reference's p.grad before clip_grad_norm_)
             for n in R.param_names(R.init_params(c["n_items"], E, c["latent"], c["hidden"], seed=c["seed"])):
@@ -69,33 +73,83 @@ def test_fused_step_matches_reference(golden, hip_device, name):
                            "fc_logvar.bias": bg[L:]}[n]
                 else:
                     got = fused.G[n]
-                assert _maxrel(got, ref) < 2e-5, n
+                err[f"grad:{n}"] = _maxrel(got, ref)
     params = dict(model.named_parameters())
-    opt_m = {}
-    for n, p in params.items():
-        # Adam maps near-zero gradients to O(lr) steps: compare params relative to their magnitude
-        assert _maxrel(p, golden[f"g2{name}_s2_param_{n}"]) < 5e-4, n
     lay = fused.layout
-    for n in params:
+    for n, p in params.items():
+        ref = golden[f"g2{name}_s2_param_{n}"]
+        if precision == "fp32":  # params relative to their magnitude
+            err[f"param:{n}"] = _maxrel(p, ref)
+        else:
+            # Adam's early steps are ~lr * sign(g): a gradient near 0 whose sign the decoder's rounding flips
+            # moves its element by 2 lr (biases start at 0, so any max-relative bar fails on them); the bar is
+            # on the RMS deviation in units of lr over the tensor
+            dev = p.detach().double().cpu() - torch.as_tensor(ref).double()
+            err[f"param:{n}"] = float(dev.pow(2).mean().sqrt()) / c["lr"]
         if n == "encoder.0.weight":
             m, v = fused.m_w1t.t(), fused.v_w1t.t()
         else:
             m, v = lay.view(fused.m, n), lay.view(fused.v, n)
-        assert _maxrel(m, golden[f"g2{name}_s2_m_{n}"]) < 5e-5, n
-        assert _maxrel(v, golden[f"g2{name}_s2_v_{n}"]) < 5e-5, n
+        err[f"m:{n}"] = _maxrel(m, golden[f"g2{name}_s2_m_{n}"])
+        err[f"v:{n}"] = _maxrel(v, golden[f"g2{name}_s2_v_{n}"])
+    return err
 
 
-@pytest.mark.parametrize("name", ["A", "C"])
-def test_fused_step_bf16_decoder(golden, hip_device, name):
-    """bf16 decoder MFMA: same step, looser tolerance (scores carry bf16 rounding of u and E)."""
-    c, X, E, model, fused, data = _build(name, hip_device, precision="bf16")
-    if fused.precision != "bf16":
-        pytest.skip("no bf16 decoder for this d")
-    B = c["n_users"]
-    loss3 = fused.step_batch(data, None, B, c["beta"], c["dropout"], train=True,
-                             ext=_ext(golden, name, 1, c, hip_device))
-    np.testing.assert_allclose(loss3.cpu().numpy(), golden[f"g2{name}_loss"][0], rtol=2e-3)
-    assert abs(fused.norm.item() - golden[f"g2{name}_norm"][0]) <= 1e-2 * golden[f"g2{name}_norm"][0]
+def _check(err, tol, label):
+    print(label, {k: f"{v:.2e}" for k, v in err.items()})
+    bad = {k: v for k, v in err.items() if v > tol[k.split(":")[0]]}
+    assert not bad, (label, bad)
+
+
+# Bars per decoder precision: relative, max over elements, scaled by the reference tensor's max ("param" in
+# low precision: RMS deviation in units of lr, see _step_errors). Measured on MI355X (profiles/r02_train_pins.log),
+# max over configs A / C: bf16 loss 2e-4, norm 1.1e-3, grads 3.9e-3, m / v 4.1e-3; fp8 (A) loss 6.7e-4,
+# norm 8e-3, grads 4.7e-2, m 8e-2, v 9.1e-2.
+#   fp32: the fused kernels in exact fp32 (reduction order only);
+#   bf16: S = u E^T from bf16-rounded u and E (2^-9 relative each) and P rounded to bf16 for O = P E;
+#   fp8:  e4m3 u and E (2^-4 relative rounding) and P in e4m3 blocks: ~10x bf16's deviations.
+STEP_TOL = {
+    "fp32": {"loss": 2e-5, "norm": 2e-5, "grad": 2e-5, "param": 5e-4, "m": 5e-5, "v": 5e-5},
+    "bf16": {"loss": 2e-3, "norm": 5e-3, "grad": 1e-2, "param": 0.15, "m": 1e-2, "v": 1.5e-2},
+    "fp8": {"loss": 5e-3, "norm": 3e-2, "grad": 1.2e-1, "param": 0.6, "m": 2e-1, "v": 2.5e-1},
+}
+
+
+@pytest.mark.parametrize("name", sorted(TRAIN_CONFIGS))
+def test_fused_step_matches_reference(golden, hip_device, name):
+    _check(_step_errors(golden, hip_device, name, "fp32"), STEP_TOL["fp32"], f"fp32 {name}")
+
+
+@pytest.mark.parametrize("name,precision", [("A", "bf16"), ("C", "bf16"), ("A", "fp8")])
+def test_fused_step_low_precision_decoder(golden, hip_device, name, precision):
+    """bf16 / fp8 decoder MFMA: the same two steps against golden G2 at the bars of STEP_TOL (production
+    precisions; the whole train step, not only its losses)."""
+    from hvae import ops, _lib
+    d = TRAIN_CONFIGS[name]["d"]
+    if not ops.decoder_supported(_lib.HVAE_BF16 if precision == "bf16" else _lib.HVAE_FP8, d):
+        pytest.skip(f"no {precision} decoder for d = {d}")
+    _check(_step_errors(golden, hip_device, name, precision), STEP_TOL[precision], f"{precision} {name}")
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16", "fp8"])
+def test_validate_loss_matches_reference(golden, hip_device, precision):
+    """VAETrainer.validate's per-batch loss (eval mode: z = mu, no dropout; reference src/ml/train.py:105-124,
+    model.py:157-179) from the fused step against the reference's eval-mode loss terms on the G1 inputs."""
+    from hvae.executor import FusedTrainer
+    from src.ml.model import HybridVAE
+    c = EVAL_CONFIG
+    X = synth_csr(c["n_users"], c["n_items"], seed=100)
+    E = synth_embeddings(c["n_items"], c["d"], seed=101)
+    torch.manual_seed(c["seed"])
+    model = HybridVAE(c["n_items"], E, latent_dim=c["latent"], hidden_dims=c["hidden"], dropout=0.3,
+                      beta=c["beta"]).to(hip_device)
+    fused = FusedTrainer(model, hip_device, precision=precision, use_graphs=False)
+    data = fused.device_data(X, list(range(c["n_users"])))
+    loss3 = fused.step_batch(data, None, c["n_users"], c["beta"], 0.3, train=False).cpu().numpy()
+    ref = golden["g1_loss"]
+    err = np.abs(loss3 - ref) / np.abs(ref)
+    print(precision, "val loss rel err", err)
+    assert np.all(err < STEP_TOL[precision]["loss"]), (loss3, ref)
 
 
 def test_graph_replay_is_bitwise_eager(hip_device):
