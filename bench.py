@@ -11,7 +11,8 @@ GPU -- a 1.25 M-user shard (10 M users / 8 GPUs) of the 10M x 1M synthetic,
 d = 768, latent 128, hidden [512], 4096 users per GPU per step, bf16 decoder
 MFMA. Inputs (CSR, weights, frozen E) are resident in HBM before the timed
 region. N > 1 runs one process per GPU (torchrun), user-batch data parallel
-with the gradient exchange over RCCL (weak scaling: B users per GPU per step).
+with the gradient exchange over RCCL (weak scaling: B users per GPU per step;
+--scaling strong splits a fixed --global-batch over the GPUs).
 
 Prints ONE JSON line on rank 0, with a live roofline for the dominant kernel
 (HIP events around its launches on the stream it runs on) and the CPU
@@ -222,12 +223,22 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe-steps", type=int, default=50)
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: --batch-size users per GPU per step (default); strong: --global-batch users per "
+                         "step split over the GPUs (SURVEY §8d: both curves)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: users per step over all GPUs (default: the workload's batch)")
     args = ap.parse_args()
 
     w = dict(WORKLOADS[args.workload])
     if args.batch_size:
         w["batch"] = args.batch_size
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.scaling == "strong":
+        G = args.global_batch or w["batch"]
+        if G % world:
+            raise SystemExit(f"--global-batch {G} is not divisible by {world} GPUs")
+        w["batch"] = G // world
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = max(torch.cuda.device_count(), 1)
@@ -345,7 +356,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (Zipf(0.8) items, 5+Poisson rows, L2-normalised random E; random-init weights)",

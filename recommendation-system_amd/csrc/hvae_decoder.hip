@@ -1171,6 +1171,325 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
   }
 }
 
+// ------------------------------------------------------------- version 4 ---
+// D = 768, one barrier per tile and no partial-S exchange. Version 3 splits GEMM1 over D, so the pair's
+// partial S^T halves cross LDS every tile (2 KiB each way) and a second barrier orders them. Here wave
+// (ug, dh) computes S^T of ITS 16 items over all of D for its 32 users with v_mfma_f32_16x16x32_bf16
+// (u over all of D in 192 VGPRs as the B operand; one E row read serves both 16-user halves), so its
+// scores are complete and only P crosses LDS:
+//   iteration t: [barrier: tile t + 1 landed, P(t) halves published] -> LDS-DMA of t + 2 into the slot
+//   GEMM2(t - 1) freed -> GEMM1(t + 1) (48 MFMAs of 16 cycles) -> GEMM2(t) over both k-steps with P(t) read
+//   back from LDS in the B layout (24 MFMAs of 32 cycles), the 8 exponentials of tile t + 1 in its gaps ->
+//   P(t + 1) own half out (P double-buffered by tile parity).
+// O (the wave's D half, 192 AGPRs), the LDS image, the DMA pieces, the GEMM2 reads and the fixed-offset /
+// flag rules are version 3's; P is stored per user in GEMM2's k order (position 8 (q >> 2 & 1) + 4 (q >> 3)
+// + (q & 3) for item q of a half), with an 80-B row stride so that the B-layout reads hit every bank once.
+#ifndef DEC4_DMA
+#define DEC4_DMA 0  // LDS-DMA pieces: 0 = in GEMM1's gaps, 1 = in GEMM2's, 2 = half in each
+#endif
+// timing ablations (A/B builds only, results invalid): 1 = no LDS-DMA / vmcnt waits in the loop,
+// 2 = no barrier in the loop, 3 = no exponentials / P stores
+#ifndef DEC4_ABL
+#define DEC4_ABL 0
+#endif
+#ifndef DEC4_G1_AHEAD
+#define DEC4_G1_AHEAD 2  // GEMM1 A operand k-steps in flight
+#endif
+__host__ __device__ constexpr int d4_lds_bytes(int D) { return 3 * ((D / 128) * 8192) + 2 * 2 * 32 * 80 + 4 * 64 * 4; }
+
+template <int D, bool WITH_O>
+__global__ void __launch_bounds__(256) k_dec4_bf16(const float* __restrict__ U, int64_t ldu,
+                                                   const bf16_t* __restrict__ E, const float* __restrict__ e_maxnorm,
+                                                   int64_t nb, int64_t N, int splits, int64_t tiles_per_split,
+                                                   DecOut out) {
+  constexpr int DW = D / 2;         // GEMM2: dims owned by one wave
+  constexpr int DB = DW / 32;       // GEMM2 d-blocks
+  constexpr int KS = D / 32;        // GEMM1 k-steps (16x16x32, all of D)
+  constexpr int NSEG = D / 128;
+  constexpr int TB = NSEG * 8192;
+  constexpr int PW = NSEG * 8 / 4;  // 1-KiB LDS-DMA pieces per wave per tile
+  constexpr int NS = 3;
+  constexpr int PST = 80;           // P row stride (bytes)
+  static_assert(D % 128 == 0 && (DW / 32) % 4 == 0 && PW % 2 == 0 && d4_lds_bytes(D) <= 160 * 1024,
+                "k_dec4_bf16 shape");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned char* pbuf = lds + NS * TB;                                 // [2 parity][2 ug][32 users][PST]
+  float* xm = reinterpret_cast<float*>(lds + NS * TB + 2 * 2 * 32 * PST);  // [4 w][64]: max / sum exchange
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
+  const int c16 = lane & 15, g = lane >> 4;  // GEMM1 layout: users c16 + 16 nb, items 4 g .. 4 g + 3
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ug = w & 1, dh = w >> 1, pw = w ^ 2;
+  const int split = blockIdx.x % splits;
+  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 64 + ug * 32;
+  const int64_t user = u0 + col;  // GEMM2 / output layout
+  const bool wave_active = u0 < nb;
+  const int64_t ntiles = (N + kBfTI - 1) / kBfTI;
+  const int64_t t_beg = (int64_t)split * tiles_per_split;
+  const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
+  const int dbase = dh * DW;
+  const float emax = *e_maxnorm;  // before any LDS-DMA is in flight
+
+  // u as GEMM1's B operand: lane holds U[u0 + c16 + 16 nb][32 ks + 8 g .. + 7]
+  uint4 uf[KS][2];
+  float usq[2] = {0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) {
+      const int64_t uu = u0 + c16 + 16 * n2;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+      if (uu < nb) {
+        a = *reinterpret_cast<const float4*>(U + uu * ldu + 32 * ks + 8 * g);
+        b = *reinterpret_cast<const float4*>(U + uu * ldu + 32 * ks + 8 * g + 4);
+      }
+      usq[n2] += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+      uf[ks][n2] = make_uint4(pack_bf16x2(a.x, a.y), pack_bf16x2(a.z, a.w), pack_bf16x2(b.x, b.y),
+                              pack_bf16x2(b.z, b.w));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float bound[2];
+#pragma unroll
+  for (int n2 = 0; n2 < 2; ++n2) {
+    float v = usq[n2];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    bound[n2] = sqrtf(v) * emax * 1.02f;
+  }
+
+  // LDS-DMA into version 2's image (version 3's pieces)
+  int vlane[2];
+#pragma unroll
+  for (int pb = 0; pb < 2; ++pb) {
+    const int row = 8 * pb + ((lane >> 2) & 7);
+    vlane[pb] = ((lane >> 2) & 7) * (D * 2) + 64 * (lane >> 5) + 16 * ((lane & 3) ^ ((row >> 2) & 3));
+  }
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(E), (short)0, (int)(N * D * 2), 0x00020000);
+  const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
+  auto issue_pieces = [&](uint32_t soff, int slot_i, int i0, int i1, bool fresh) {
+    const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const int p = w * PW + i;
+      const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (i & 1));
+      const int vo = vlane[(i >> 1) & 1];
+      if (fresh && i == i0)
+        asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+      else
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+    }
+  };
+  auto tile_soff = [&](int64_t t) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(kBfTI * D * 2)));
+  };
+  auto barrier = [&] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // GEMM1: S^T[16 own items][32 users] over all of D; A = image rows 16 dh + c16, chunk 4 ks + g
+  const int r1 = 16 * dh + c16;
+  const int laneA = ((r1 >> 3) << 11) + ((r1 & 7) << 6) + ((g ^ ((r1 >> 2) & 3)) << 4);
+  auto gemm1 = [&](const unsigned char* buf, f32x4 (&s)[2], auto&& fill) {
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[n2][r] = 0.f;
+    const unsigned char* b0 = buf + laneA;
+    auto rdA = [&](int ks) {
+      return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(b0 + ((ks >> 2) << 13) + ((ks & 3) << 9)));
+    };
+    constexpr int AH = DEC4_G1_AHEAD;
+    bf16x8 a[AH];
+#pragma unroll
+    for (int j = 0; j < AH; ++j) a[j] = rdA(j);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8 c = a[ks % AH];
+      if (ks + AH < KS) a[ks % AH] = rdA(ks + AH);
+      s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c, __builtin_bit_cast(bf16x8, uf[ks][0]), s[0], 0, 0, 0);
+      s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c, __builtin_bit_cast(bf16x8, uf[ks][1]), s[1], 0, 0, 0);
+      fill(ks);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("" : "+v"(s[0]), "+v"(s[1]));  // S^T in VGPRs (the softmax reads it; O owns the AGPRs)
+  };
+  // GEMM2 (version 3's reads): O^T[DW][32 users] += E^T P^T over k-steps 0 (items 0..15) and 1 (16..31)
+  const int g1 = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
+  const int cseg = (dbase / 128) << 13;
+  const int laneT0 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((0 + h) & 3)) << 4) + 8 * (pp & 1);
+  const int laneT1 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((2 + h) & 3)) << 4) + 8 * (pp & 1);
+  f32x16 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  constexpr int BH = 2;
+  auto rdT = [&](const unsigned char* buf, int i) {
+    const int kh = i / DB, db = i % DB;
+    const unsigned char* t = buf + cseg + (kh << 12);
+    auto* p0 = (__attribute__((address_space(3))) s16x4*)(void*)(t + laneT0 + ((db >> 2) << 13) + ((db & 3) << 9));
+    auto* p1 = (__attribute__((address_space(3))) s16x4*)(void*)(t + laneT1 + (1 << 11) + ((db >> 2) << 13) +
+                                                                 ((db & 3) << 9));
+    return std::array<s16x4, 2>{__builtin_amdgcn_ds_read_tr16_b64_v4i16(p0), __builtin_amdgcn_ds_read_tr16_b64_v4i16(p1)};
+  };
+  auto gemm2 = [&](const unsigned char* buf, const uint4& pf0, const uint4& pf1, auto&& fill) {
+    if constexpr (WITH_O) {
+      std::array<s16x4, 2> n[BH];
+#pragma unroll
+      for (int j = 0; j < BH; ++j) n[j] = rdT(buf, j);
+#pragma unroll
+      for (int i = 0; i < 2 * DB; ++i) {
+        const std::array<s16x4, 2> c = n[i % BH];
+        if (i + BH < 2 * DB) n[i % BH] = rdT(buf, i + BH);
+        const s16x8 a = {c[0][0], c[0][1], c[0][2], c[0][3], c[1][0], c[1][1], c[1][2], c[1][3]};
+        o[i % DB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                           __builtin_bit_cast(bf16x8, i < DB ? pf0 : pf1), o[i % DB],
+                                                           0, 0, 0);
+        fill(i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2 * DB; ++i) fill(i);
+    }
+  };
+  // P rows: pbuf[par][ug][user][PST]; own half at k-step dh; lane's items 4 g .. 4 g + 3 -> positions
+  // 16 dh + 8 (g & 1) + 4 (g >> 1)
+  auto p_row = [&](int par, int uu) { return pbuf + ((par * 2 + ug) * 32 + uu) * PST; };
+  const int ppos = 2 * (16 * dh + 8 * (g & 1) + 4 * (g >> 1));
+
+  float m[2] = {0.f, 0.f}, mL[2] = {0.f, 0.f}, lsum[2] = {0.f, 0.f};
+  f32x4 s_nx[2];
+  // tail: own items 16 dh + 4 g + i of tile t past N leave the softmax
+  auto mask_tail = [&](f32x4 (&s)[2], int64_t t) {
+    if (t == ntiles - 1 && (N % kBfTI) != 0) {
+      const int lim = (int)(N - t * kBfTI) - 16 * dh - 4 * g;
+#pragma unroll
+      for (int n2 = 0; n2 < 2; ++n2)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[n2][r] = r >= lim ? -INFINITY : s[n2][r];
+    }
+  };
+  if (t_beg < t_end) {
+    issue_pieces(tile_soff(t_beg), 0, 0, PW, true);
+    issue_pieces(tile_soff(min(t_beg + 1, t_end - 1)), 1, 0, PW, true);
+    wait_vmcnt<PW>();
+  }
+  barrier();
+  if (t_beg < t_end) {
+    // first tile: its max over both halves sets the pair's fixed offset m (version 2's rule)
+    gemm1(lds, s_nx, [](int) {});
+    mask_tail(s_nx, t_beg);
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) {
+      float mx = fmaxf(fmaxf(s_nx[n2][0], s_nx[n2][1]), fmaxf(s_nx[n2][2], s_nx[n2][3]));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (g == 0) xm[w * 64 + c16 + 16 * n2] = mx;
+      m[n2] = mx;
+    }
+    barrier();
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) {
+      m[n2] = fmaxf(fmaxf(m[n2], xm[pw * 64 + c16 + 16 * n2]), bound[n2] - kOffsetSpan);
+      mL[n2] = m[n2] * kLog2e;
+    }
+    // P(t_beg) own half -> parity 0
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) {
+      float pv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        pv[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_nx[n2][r], kLog2e, -mL[n2]));
+        lsum[n2] += pv[r];
+      }
+      *reinterpret_cast<uint2*>(p_row(0, c16 + 16 * n2) + ppos) =
+          make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
+    }
+  }
+
+  for (int64_t t = t_beg; t < t_end; ++t) {
+    const int li = (int)(t - t_beg);
+    const int cur = li % NS, nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
+    // [t]: tile t + 1 has landed, P(t) halves are published (the xm reads of the prologue are done)
+    if (DEC4_ABL != 1) wait_vmcnt<0>();
+    if (DEC4_ABL != 2) barrier();
+    const int64_t t_dma = min(t + 2, t_end - 1);
+    const uint32_t soff_dma = tile_soff(t_dma);
+    // P(t) in GEMM2's B layout: user col, positions 8 h .. 8 h + 7 of k-steps 0 and 1
+    const uint4 pf0 = *reinterpret_cast<const uint4*>(p_row(par, col) + 16 * h);
+    const uint4 pf1 = *reinterpret_cast<const uint4*>(p_row(par, col) + 32 + 16 * h);
+    // GEMM1(t + 1) (a stale slot after the last tile: one code path, result unused) with the DMA of t + 2
+    gemm1(lds + nxt * TB, s_nx, [&](int ks) {
+      constexpr int P1 = DEC4_DMA == 0 ? PW : DEC4_DMA == 1 ? 0 : PW / 2;  // pieces in GEMM1
+      if (DEC4_ABL != 1 && (ks & 1) == 1 && ks / 2 < P1) issue_pieces(soff_dma, s_dma, ks / 2, ks / 2 + 1, ks == 1);
+    });
+    mask_tail(s_nx, t + 1);
+    // GEMM2(t); the softmax of tile t + 1 in its gaps (after the last tile it runs on the unused GEMM1 result:
+    // its l terms are weighted 0 and its P half is never read -- no branch, so nothing is sunk out of the gaps)
+    const float lw = t + 1 < t_end ? 1.f : 0.f;
+    float pv[8];
+    uint32_t pk[4];
+    gemm2(lds + cur * TB, pf0, pf1, [&](int i) {
+      if (DEC4_ABL != 3 && i >= 1 && i <= 8) {
+        const int e = i - 1, n2 = e >> 2, r = e & 3;
+        pv[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_nx[n2][r], kLog2e, -mL[n2]));
+        lsum[n2] = __builtin_fmaf(pv[e], lw, lsum[n2]);
+        if (r & 1) pk[e >> 1] = pack_bf16x2(pv[e - 1], pv[e]);
+        if (e == 3 || e == 7)
+          *reinterpret_cast<uint2*>(p_row(par ^ 1, c16 + 16 * n2) + ppos) = make_uint2(pk[2 * n2], pk[2 * n2 + 1]);
+      }
+      constexpr int P1 = DEC4_DMA == 0 ? PW : DEC4_DMA == 1 ? 0 : PW / 2;
+      if (DEC4_ABL != 1 && (i & 1) == 0 && P1 + i / 2 < PW)
+        issue_pieces(soff_dma, s_dma, P1 + i / 2, P1 + i / 2 + 1, P1 == 0 && i == 0);
+    });
+  }
+
+  wait_vmcnt<0>();  // the last tile's LDS-DMA (a duplicate, never read) lands before the ring is released
+
+  // l = own items (4 lanes g) + partner's items; then per user in the GEMM2 / output layout
+#pragma unroll
+  for (int n2 = 0; n2 < 2; ++n2) {
+    lsum[n2] += __shfl_xor(lsum[n2], 16, 64);
+    lsum[n2] += __shfl_xor(lsum[n2], 32, 64);
+  }
+  barrier();  // every wave is past its last read of xm
+  if (g == 0) {
+    xm[w * 64 + c16] = lsum[0];
+    xm[w * 64 + c16 + 16] = lsum[1];
+    xm[w * 64 + 32 + c16] = m[0];
+    xm[w * 64 + 32 + c16 + 16] = m[1];
+  }
+  barrier();
+  if (!wave_active || t_beg >= t_end || user >= nb) return;
+  const float lown = xm[w * 64 + col], lo = xm[pw * 64 + col], mu = xm[w * 64 + 32 + col];
+  const float ltot = dh == 0 ? lown + lo : lo + lown;
+  if (h == 0 && dh == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
+  const int64_t row = out.direct ? user : (int64_t)split * nb + user;
+  if (h == 0 && dh == 0) {
+    if (out.direct) out.lse[user] = mu + logf(ltot);
+    else { out.m[row] = mu; out.l[row] = ltot; }
+  }
+  if (WITH_O) {
+    const float sc = out.direct ? 1.0f / ltot : 1.0f;
+#pragma unroll
+    for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
+        *reinterpret_cast<float4*>(out.O + row * D + dd) =
+            make_float4(o[d][4 * g4] * sc, o[d][4 * g4 + 1] * sc, o[d][4 * g4 + 2] * sc, o[d][4 * g4 + 3] * sc);
+      }
+  }
+}
+
 // ------------------------------------------------------------------- fp8 ---
 // The same sweep on the block-scaled fp8 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, OCP e4m3 operands,
 // twice the bf16 rate; BASELINE configs[4]). Both products carry exact power-of-two scales:
@@ -2243,6 +2562,7 @@ struct DecPlan {
   size_t lds;
   int v2;    // bf16 version-2 sweep (k_dec2_bf16)
   int v3;    // bf16 version-3 sweep (k_dec3_bf16, D = 768)
+  int v4;    // bf16 version-4 sweep (k_dec4_bf16, D = 768)
   int ds;    // its D split (1 or 2)
   int nw;    // its waves per block (4, or 8 with ds = 2)
   int64_t upb;
@@ -2274,6 +2594,8 @@ static int dec_forced_nw() {
 static bool v2_supported(int64_t D) { return D == 64 || D == 128 || D == 256 || D == 384 || D == 768; }
 // HVAE_DEC_V3=0 keeps the version-2 sweep at D = 768 (A/B; read at every plan, so a test can switch it)
 static bool v3_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V3", 1) != 0; }
+// HVAE_DEC_V4=0 keeps version 3 at D = 768 (A/B; read at every plan)
+static bool v4_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V4", 1) != 0; }
 
 static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
   s = std::max<int64_t>(1, std::min<int64_t>(s, std::min<int64_t>(tiles, kMaxSplits)));
@@ -2300,6 +2622,7 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   const bool bf = dtype == HVAE_BF16;
   p.v2 = bf && !dec_use_v1() && v2_supported(D);
   p.v3 = p.v2 && v3_supported(D);
+  p.v4 = p.v3 && v4_supported(D);
   p.ds = p.v2 && (D > 384 || nb <= 64) ? 2 : 1;
   if (p.v2 && D <= 384 && (dec_forced_ds() == 1 || dec_forced_ds() == 2)) p.ds = dec_forced_ds();
   p.nw = p.v2 && p.ds == 2 && nb > 64 && D <= 384 ? 8 : 4;
@@ -2391,6 +2714,22 @@ static int launch_bf16_v3(const float* U, int64_t ldu, const void* E, const floa
 }
 
 template <int D, bool WO>
+static int launch_bf16_v4(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                          const DecPlan& p, DecOut o, hipStream_t st) {
+  constexpr int lds = d4_lds_bytes(D);
+  static_assert(lds <= 160 * 1024, "k_dec4_bf16 LDS");
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec4_bf16<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr_set = true;
+  }
+  k_dec4_bf16<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N, p.splits,
+                                                          p.tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec4_bf16");
+  return HVAE_OK;
+}
+
+template <int D, bool WO>
 static int launch_fp8(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                       const DecPlan& p, DecOut o, hipStream_t st) {
   constexpr int DS = D > 384 ? 2 : 1;
@@ -2434,6 +2773,8 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
       case 768: return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       default: break;
     }
+  } else if (dtype == HVAE_BF16 && p.v4 && D == 768) {
+    return launch_bf16_v4<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
   } else if (dtype == HVAE_BF16 && p.v3 && D == 768) {
     return launch_bf16_v3<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
   } else if (dtype == HVAE_BF16 && p.v2) {

@@ -12,7 +12,7 @@ n_b lse_b - u_b . sum_j x_bj E_j and d(u) = (n_b O_b - sum_j x_bj E_j) / B (fp32
 as hvae_decoder.hip's finalize).
 
 Also: 64 users x 1M items (256 item splits: the grouped split merge), users whose |u| forces the flagged
-exact recompute at d = 768, version 3 of the d = 768 sweep against version 2 (HVAE_DEC_V3=0), and one fused
+exact recompute at d = 768, versions 4 and 3 of the d = 768 sweep against version 2 (HVAE_DEC_V4=0 / HVAE_DEC_V3=0), and one fused
 Syn-1M-shaped train step whose exact lazy Adam stays bitwise equal to the dense update over 3 replays.
 """
 import os
@@ -124,9 +124,10 @@ def test_decoder_train_full_shape(ops, hip_device, dtype, nb, N, D):
 
 
 @pytest.mark.timeout(300)
-def test_decoder_d768_v3_matches_v2(ops, hip_device, monkeypatch):
-    """Version 3 (item-half softmax ownership) against version 2 (whole-tile softmax in both waves) of the
-    d = 768 bf16 sweep: both round the same bf16 operands; only fp32 summation order differs."""
+def test_decoder_d768_versions_agree(ops, hip_device, monkeypatch):
+    """Versions 4 (item-split GEMM1, one barrier per tile) and 3 (item-half softmax ownership) against version 2
+    (whole-tile softmax in both waves) of the d = 768 bf16 sweep: all round the same bf16 operands (P to bf16
+    included); only fp32 summation order differs."""
     nb, N, D = 700, 50_001, 768
     E, U = _inputs(hip_device, nb, N, D, seed=11)
     X = synth_csr(nb, N, lam=15.0, seed=3)
@@ -134,12 +135,15 @@ def test_decoder_d768_v3_matches_v2(ops, hip_device, monkeypatch):
     img = ops.decoder_image(E)
     enorm = ops.row_norm_max(img)
     out = {}
-    for v in ("1", "0"):
-        monkeypatch.setenv("HVAE_DEC_V3", v)
-        out[v] = ops.decoder_train(xd, U, img, enorm, E, 1.0 / nb, want_o=True)
-    (l3, o3, r3, d3), (l2, o2, r2, d2) = out["1"], out["0"]
-    assert (l3 - l2).abs().max() < 1e-4
-    assert _maxrel(o3, o2) < 5e-3 and _maxrel(r3, r2) < 1e-5 and _maxrel(d3, d2) < 5e-3
+    for name, v3, v4 in (("v4", "1", "1"), ("v3", "1", "0"), ("v2", "0", "0")):
+        monkeypatch.setenv("HVAE_DEC_V3", v3)
+        monkeypatch.setenv("HVAE_DEC_V4", v4)
+        out[name] = ops.decoder_train(xd, U, img, enorm, E, 1.0 / nb, want_o=True)
+    l2, o2, r2, d2 = out["v2"]
+    for name in ("v4", "v3"):
+        la, oa, ra, da = out[name]
+        assert (la - l2).abs().max() < 1e-4, name
+        assert _maxrel(oa, o2) < 5e-3 and _maxrel(ra, r2) < 1e-5 and _maxrel(da, d2) < 5e-3, name
 
 
 @pytest.mark.timeout(300)
