@@ -155,6 +155,60 @@ class HipAdam(torch.optim.Optimizer):
         return loss
 
 
+class ModuleAdam(torch.optim.Optimizer):
+    """torch.optim.Adam on the module's own parameter tensors, applied by libhvae (hvae_adam_dense), with the
+    reference's clip_grad_norm_(max_norm) folded in (hvae_clip_grad_norm over the concatenated gradients, its
+    coefficient applied inside the Adam kernel). Used by VAETrainer when the item embeddings are trainable
+    (HybridVAE(freeze_embeddings=False), reference model.py:72-75): E is then a [N, d] parameter with a dense
+    gradient, which the fused step's layout does not hold. state_dict() has torch.optim.Adam's layout."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.0):
+        defaults = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, amsgrad=False, maximize=False,
+                        foreach=None, capturable=False, differentiable=False, fused=None,
+                        decoupled_weight_decay=False)
+        super().__init__(params, defaults)
+        plist = [p for g in self.param_groups for p in g["params"]]
+        dev = plist[0].device
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.norm = torch.zeros(1, device=dev)
+        self.coef = torch.ones(1, device=dev)
+        for p in plist:
+            self.state[p] = {"step": torch.tensor(0.0), "exp_avg": torch.zeros_like(p),
+                             "exp_avg_sq": torch.zeros_like(p)}
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        steps = [int(float(st["step"])) for st in self.state.values() if "step" in st]
+        if steps:
+            self.step_dev.fill_(steps[0])
+
+    @torch.no_grad()
+    def step(self, closure=None, max_norm: float | None = None):
+        """One Adam step on every parameter with a gradient; max_norm: clip the global gradient norm first
+        (torch.nn.utils.clip_grad_norm_ semantics, train.py:96)."""
+        loss = closure() if closure is not None else None
+        params = [p for g in self.param_groups for p in g["params"] if p.grad is not None]
+        if not params:
+            return loss
+        g0 = self.param_groups[0]
+        coef = None
+        if max_norm is not None:
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            ops.clip_grad_norm(flat, None, max_norm, self.norm, self.coef)
+            coef = self.coef
+        cfg = ops.adam_config(g0["lr"], g0["betas"], g0["eps"], g0["weight_decay"], self.step_dev, coef)
+        for p in params:
+            st = self.state[p]
+            g = torch.empty_like(p)  # p's memory order (W1 is an item-major view): p, m, v, g elementwise aligned
+            g.copy_(p.grad)
+            ops.adam_dense(cfg, p, st["exp_avg"], st["exp_avg_sq"], g)
+        ops.counter_add(self.step_dev, 1)
+        t = float(self.step_dev.item())
+        for p in params:
+            self.state[p]["step"] = torch.tensor(t)
+        return loss
+
+
 # =============================================================================
 # Trainer
 # =============================================================================
@@ -172,15 +226,23 @@ class VAETrainer:
             device = torch.device("cuda", torch.cuda.current_device())
         self.model = model.to(device)
         self.device = device
-        self.fused = FusedTrainer(self.model, device, lr=lr, weight_decay=weight_decay,
-                                  precision=precision or (config.PRECISION or None), process_group=process_group)
-        self.optimizer = HipAdam(model.parameters(), self.fused, lr=lr, weight_decay=weight_decay)
+        if getattr(model, "item_embeddings_trainable", False):
+            # trainable E: the module-API step on libhvae kernels (scores materialised per batch, as the
+            # reference does), E updated with the other parameters
+            if process_group is not None:
+                raise NotImplementedError("data parallelism covers the fused (frozen-embedding) trainer")
+            self.fused = None
+            self.optimizer = ModuleAdam(model.parameters(), lr=lr, weight_decay=weight_decay)
+        else:
+            self.fused = FusedTrainer(self.model, device, lr=lr, weight_decay=weight_decay,
+                                      precision=precision or (config.PRECISION or None), process_group=process_group)
+            self.optimizer = HipAdam(model.parameters(), self.fused, lr=lr, weight_decay=weight_decay)
         self.train_losses: list[float] = []
         self.val_losses: list[float] = []
         self.train_recon_losses: list[float] = []
         self.train_kl_losses: list[float] = []
         logger.info(f"Trainer on {device}, {sum(p.numel() for p in model.parameters()):,} params, "
-                    f"decoder {self.fused.precision}")
+                    f"decoder {self.fused.precision if self.fused is not None else 'module path (trainable E)'}")
 
     # beta of one training batch (reference: _compute_loss, train.py:71-79)
     def _beta_fn(self):
@@ -193,7 +255,34 @@ class VAETrainer:
             return fn
         return ConstBeta(m.beta)
 
+    def _run_module(self, loader, train: bool) -> dict[str, float]:
+        """Reference train_epoch / validate (train.py:81-124) on the module API: dense batches, forward, loss,
+        backward, clip 5.0, Adam -- every op a libhvae kernel."""
+        tot = np.zeros(3)
+        n = 0
+        for batch in loader:
+            x = batch.to(self.device).float()
+            if train:
+                self.optimizer.zero_grad()
+                recon_x, mu, logvar = self.model(x)
+                if hasattr(self.model, "compute_loss"):
+                    loss, recon, kl = self.model.compute_loss(recon_x, x, mu, logvar)
+                    self.model.step_annealing()
+                else:
+                    loss, recon, kl = vae_loss_function(recon_x, x, mu, logvar, self.model.beta)
+                loss.backward()
+                self.optimizer.step(max_norm=5.0)
+            else:
+                with torch.no_grad():
+                    recon_x, mu, logvar = self.model(x)
+                    loss, recon, kl = vae_loss_function(recon_x, x, mu, logvar, self.model.beta)
+            tot += np.array([loss.item(), recon.item(), kl.item()])
+            n += 1
+        return {"total_loss": tot[0] / n, "recon_loss": tot[1] / n, "kl_loss": tot[2] / n}
+
     def _run(self, loader, train: bool) -> dict[str, float]:
+        if self.fused is None:
+            return self._run_module(loader, train)
         self.optimizer.sync_hyper()
         p_drop = float(self.model.dropout)
         beta_fn = self._beta_fn() if train else ConstBeta(self.model.beta)
