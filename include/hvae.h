@@ -415,6 +415,31 @@ int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, const float
                     int64_t R, int64_t K, int32_t* idx, float* val, int32_t* flag, void* ws,
                     size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------- data artifacts (host) -- */
+/* A host CSR plus the file's users, allocated by hvae_read_interactions and
+ * released by hvae_host_csr_free. */
+typedef struct hvae_host_csr {
+  int64_t* row_ptr;     /* [n_rows + 1]                                        */
+  int32_t* col_idx;     /* [nnz], ascending within a row                       */
+  float* vals;          /* [nnz], duplicate (user, item) rows summed            */
+  int64_t n_rows, n_cols, nnz;
+  int64_t* users;       /* [n_users_seen] users of the file, first appearance   */
+  int64_t n_users_seen;
+  int64_t n_records;    /* data rows read                                       */
+} hvae_host_csr;
+/* train.csv / val.csv -> CSR (load_training_data + _build_matrix +
+ * get_user_indices_from_df, src/ml/train.py:153-193): rows with
+ * binary_rating == 1 when positives_only and the column exists, user_id /
+ * asin looked up in the mappings' keys (user_keys: n_users NUL-separated keys,
+ * key i <-> index i; likewise items), shape (n_users, n_items). One pass over
+ * the memory-mapped file, RFC 4180 quoting. A positive row whose user or item
+ * the mappings do not know is an error (HVAE_ERR_ARG), as in the reference.
+ * Host only: no device work. */
+int hvae_read_interactions(const char* csv_path, const char* user_keys, int64_t user_keys_len, int64_t n_users,
+                           const char* item_keys, int64_t item_keys_len, int64_t n_items, int positives_only,
+                           hvae_host_csr* out);
+void hvae_host_csr_free(hvae_host_csr* c);
+
 /* fp32 -> bf16 (round to nearest even) copy of the frozen embeddings. */
 int hvae_cast_bf16(const float* x, void* y, int64_t n, void* stream);
 

@@ -42,6 +42,11 @@ class CsrBatch(C.Structure):
                 ("n_items", i64)]
 
 
+class HostCsr(C.Structure):  # hvae_host_csr
+    _fields_ = [("row_ptr", vp), ("col_idx", vp), ("vals", vp), ("n_rows", i64), ("n_cols", i64), ("nnz", i64),
+                ("users", vp), ("n_users_seen", i64), ("n_records", i64)]
+
+
 class RowGrad(C.Structure):
     _fields_ = [
         ("cnt", vp), ("slot_of", vp), ("item_of", vp), ("seg_off", vp), ("fill", vp),
@@ -133,6 +138,9 @@ SIGNATURES = {
     "hvae_topk_fused": (cint, [vp, i64, vp, vp, vp, i64, i64, P(CsrBatch), i64, i64, vp, vp, vp, vp, sz,
                                vp]),
     "hvae_cast_bf16": (cint, [vp, vp, i64, vp]),
+    "hvae_read_interactions": (cint, [C.c_char_p, C.c_char_p, i64, i64, C.c_char_p, i64, i64, cint,
+                                      P(HostCsr)]),
+    "hvae_host_csr_free": (None, [P(HostCsr)]),
     "hvae_csr_batch_pack": (cint, [P(CsrBatch), f32, vp, vp, vp, i64, vp]),
 }
 

@@ -23,6 +23,7 @@ import torch
 from scipy.sparse import csr_matrix
 from torch.utils.data import DataLoader, Dataset, RandomSampler
 
+from hvae import io as hio
 from hvae import ops
 from hvae.dist import init_from_env, is_main
 from hvae.executor import ConstBeta, DeviceData, FusedTrainer
@@ -410,11 +411,13 @@ def train_hybrid_vae(
     if main_rank:
         output_path.mkdir(parents=True, exist_ok=True)
 
-    full_matrix, train_df, val_df, mappings = load_training_data(data_dir)
-    user_to_idx, item_to_idx = mappings["user_to_idx"], mappings["item_to_idx"]
-    n_items = full_matrix.shape[1]
-    train_matrix = _build_matrix(train_df, user_to_idx, item_to_idx, full_matrix.shape)
-    val_matrix = _build_matrix(val_df, user_to_idx, item_to_idx, full_matrix.shape)
+    # load_training_data + _build_matrix + get_user_indices_from_df in one native pass per file (hvae/io.py);
+    # the matrices and user lists are those of the reference's pandas path (tests/test_io_cpu.py)
+    t_load = time.perf_counter()
+    shape, train_matrix, val_matrix, train_users, val_users, mappings = hio.load_training_csr(data_dir)
+    n_items = shape[1]
+    logger.info(f"Loaded: matrix {shape}, train {train_matrix.nnz} / val {val_matrix.nnz} positives "
+                f"({time.perf_counter() - t_load:.2f} s)")
 
     emb_path = Path(embeddings_path)
     mappings_path = emb_path.with_name(f"{emb_path.stem}_mappings.pkl")
@@ -425,9 +428,9 @@ def train_hybrid_vae(
         logger.info("Using random embeddings instead of SBERT")
         embeddings = np.random.normal(0, 0.01, embeddings.shape).astype(np.float32)
 
-    train_loader = DataLoader(UserInteractionDataset(train_matrix, get_user_indices_from_df(train_df, user_to_idx)),
+    train_loader = DataLoader(UserInteractionDataset(train_matrix, train_users),
                               batch_size=batch_size, shuffle=True, num_workers=0)
-    val_loader = DataLoader(UserInteractionDataset(val_matrix, get_user_indices_from_df(val_df, user_to_idx)),
+    val_loader = DataLoader(UserInteractionDataset(val_matrix, val_users),
                             batch_size=batch_size, shuffle=False, num_workers=0)
 
     anneal_steps = int(len(train_loader) * epochs * 0.5)
