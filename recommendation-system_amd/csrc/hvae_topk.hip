@@ -65,7 +65,9 @@ struct TkScanArgs {
   float* seed;         // [R][kTkSeed] sampled bf16 scores
   int32_t* cand;       // [R][nseg][kTkSegCap]
   int32_t* cand_cnt;   // [R][nseg]
-  int nseg;            // splits * 8
+  int nseg;            // segments per user: splits * 8 (wave_users 0) or splits * 2 (wave_users 1)
+  int wave_users;      // 1: a block's 4 waves take 4 user groups over the same tiles (E read once per block
+                       // from L2, the repeats served by the CU's L1); 0: one user group, waves split the tiles
 };
 
 __device__ __forceinline__ int tk_ku(const TkScanArgs& a, int64_t r) {
@@ -105,6 +107,7 @@ struct TkScorer {
                (y.z * y.z + y.w * y.w);
         uf[g][j] = make_uint4(tk_pack_bf16x2(x.x, x.y), tk_pack_bf16x2(x.z, x.w), tk_pack_bf16x2(y.x, y.y),
                               tk_pack_bf16x2(y.z, y.w));
+        __builtin_amdgcn_sched_barrier(0);
       }
     usq += __shfl_xor(usq, 32, 64);
     eps = sqrtf(usq) * (*a.e_maxnorm) * (0x1p-8f + 0x1p-17f + 4.0f * D * 0x1p-24f) * 1.02f;
@@ -189,40 +192,29 @@ __global__ void __launch_bounds__(256) k_topk_seed_select(TkScanArgs a, int nsam
   }
 }
 
-template <int D>
-__global__ void __launch_bounds__(256) k_topk_scan(TkScanArgs a) {
-  extern __shared__ float heap_lds[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int split = blockIdx.x % a.splits;
-  const int64_t user = (int64_t)(blockIdx.x / a.splits) * 32 + (lane & 31);
-  const bool live = user < a.R;
-  const int64_t ntiles = (a.N + 31) / 32;
-  const int64_t t0 = (int64_t)split * a.tiles_per_split;
-  const int64_t t1 = min(ntiles, t0 + a.tiles_per_split);
-  const int64_t nw = t1 > t0 + w ? (t1 - t0 - w + 3) / 4 : 0;  // this wave's tiles: t0 + w, t0 + w + 4, ...
-  TkScorer<D> sc;
-  sc.load(a, user, live, lane);
-  const int h = sc.h;
-  const int ku = live ? min(tk_ku(a, user), kTkHeap) : 0;  // K_u > kTkHeap: flagged by k_topk_select
-  const float eps = sc.eps;
-
-  float* hp = heap_lds + (size_t)(w * 32 + (lane & 31)) * kTkHeap;
-  if (h == 0)
-    for (int i = 0; i < kTkHeap; ++i) hp[i] = -INFINITY;
-  float tau = live ? tk_unord(a.g_tau[user]) : -INFINITY;  // bound t; the filter is s~ >= t - eps_u
+// The per-tile selection of one wave's 32 users (shared by both scans): the heap of per-tile maxima (the pair's
+// h == 0 lane), the bound t (own heap root - eps_u, other waves' via the atomic max), candidate emission.
+struct TkSelect {
+  float* hp;
+  int cap, ku, h, sgw;
+  int64_t user, seg;
+  bool live;
+  float eps, tau;
   int cnt = 0;
-  const int64_t seg = (user * a.nseg + (int64_t)(split * 4 + w) * 2 + h) * kTkSegCap;
-
-  for (int64_t j = 0; j < nw; ++j) {
-    const int64_t t = t0 + w + 4 * j;
-    const f32x16_t s = sc.score(a, t);
-    // heap of per-tile maxima: replace the root and sift down (the pair's h == 0 lane)
+  __device__ __forceinline__ TkSelect(const TkScanArgs& a, float* heap, int cap_, int64_t user_, bool live_, int h_,
+                                      float eps_, int ku_, int sgw_)
+      : hp(heap), cap(cap_), ku(ku_ <= cap_ ? ku_ : 0), h(h_), sgw(sgw_), user(user_), live(live_), eps(eps_) {
+    if (h == 0)
+      for (int i = 0; i < cap; ++i) hp[i] = -INFINITY;
+    tau = live ? tk_unord(a.g_tau[user]) : -INFINITY;  // bound t; the filter is s~ >= t - eps_u
+    seg = (user * a.nseg + sgw + h) * kTkSegCap;
+  }
+  __device__ __forceinline__ void consume(const TkScanArgs& a, const f32x16_t& s, int64_t t, int64_t j) {
     float m = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) m = fmaxf(m, s[r]);
     m = fmaxf(m, __shfl_xor(m, 32, 64));
-    if (h == 0 && ku > 0 && m > hp[0]) {
+    if (h == 0 && ku > 0 && m > hp[0]) {  // replace the root, sift down
       int i = 0;
       while (true) {
         const int l = 2 * i + 1;
@@ -236,7 +228,7 @@ __global__ void __launch_bounds__(256) k_topk_scan(TkScanArgs a) {
       hp[i] = m;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the h == 0 lane's writes land before the pair reads
-    const float root = hp[0];
+    const float root = ku > 0 ? hp[0] : -INFINITY;
     if (live && root - eps > tau) {
       tau = root - eps;
       tau = fmaxf(tau, tk_unord(atomicMax(a.g_tau + user, tk_ord(tau))));
@@ -253,7 +245,178 @@ __global__ void __launch_bounds__(256) k_topk_scan(TkScanArgs a) {
         }
     }
   }
-  if (live) a.cand_cnt[user * a.nseg + (split * 4 + w) * 2 + h] = cnt;
+};
+
+template <int D>
+__global__ void __launch_bounds__(256) k_topk_scan(TkScanArgs a) {
+  extern __shared__ float heap_lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int split = blockIdx.x % a.splits;
+  const int64_t user = a.wave_users ? (int64_t)(blockIdx.x / a.splits) * 128 + 32 * w + (lane & 31)
+                                    : (int64_t)(blockIdx.x / a.splits) * 32 + (lane & 31);
+  const bool live = user < a.R;
+  const int64_t ntiles = (a.N + 31) / 32;
+  const int64_t t0 = (int64_t)split * a.tiles_per_split;
+  const int64_t t1 = min(ntiles, t0 + a.tiles_per_split);
+  // this wave's tiles: t0 + tw, t0 + tw + ts, ... (every tile of the split with wave_users)
+  const int tw = a.wave_users ? 0 : w, ts = a.wave_users ? 1 : 4;
+  const int64_t nw = t1 > t0 + tw ? (t1 - t0 - tw + ts - 1) / ts : 0;
+  const int sgw = a.wave_users ? split * 2 : (split * 4 + w) * 2;  // the wave's first segment of the user
+  TkScorer<D> sc;
+  sc.load(a, user, live, lane);
+  const int h = sc.h;
+  const int ku = live ? min(tk_ku(a, user), kTkHeap) : 0;  // K_u > kTkHeap: flagged by k_topk_select
+  const float eps = sc.eps;
+
+  TkSelect sel(a, heap_lds + (size_t)(w * 32 + (lane & 31)) * kTkHeap, kTkHeap, user, live, h, eps, ku, sgw);
+  for (int64_t j = 0; j < nw; ++j) {
+    const int64_t t = t0 + tw + ts * j;
+    sel.consume(a, sc.score(a, t), t, j);
+  }
+  const int cnt = sel.cnt;
+  if (live) a.cand_cnt[user * a.nseg + sgw + h] = cnt;
+}
+
+
+// ---- LDS-staged scan (D a multiple of 128): a block's 4 waves take 4 groups of 32 users over the same tiles;
+// each 32-item E tile arrives once per block by LDS-DMA (three-slot ring, the decoder's image and piece map,
+// one barrier per tile) and the 32x32x16 A operands are ds_read_b128 row reads of it. Per-user heaps of up to
+// kTkHeapL tile maxima (a user with K_u beyond it keeps the seed / other waves' bound, which is still valid).
+// ring slots and heap capacity per D (LDS: slots x the tile + 4 waves x 32 users x the heap): d = 768 keeps two
+// slots (the next tile's DMA overlaps the current tile's MFMAs) so that K_u up to 64 keeps its heap
+template <int D>
+constexpr int tkl_ns() { return D >= 768 ? 2 : 3; }
+template <int D>
+constexpr int tkl_heap() { return D >= 768 ? 64 : 128; }
+template <int D>
+constexpr int tkl_lds_bytes() { return tkl_ns<D>() * ((D / 128) * 8192) + 4 * 32 * tkl_heap<D>() * 4; }
+
+__device__ __forceinline__ uint32_t tk_lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+template <int n>
+__device__ __forceinline__ void tk_wait_vmcnt() {
+  static_assert(n >= 0 && n < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14));
+}
+
+template <int D>
+__global__ void __launch_bounds__(256) k_topk_scan_lds(TkScanArgs a) {
+  constexpr int NSEG = D / 128, TB = NSEG * 8192, PW = NSEG * 8 / 4, NS = tkl_ns<D>(), KS = D / 16;
+  constexpr int HC = tkl_heap<D>();
+  static_assert(D % 128 == 0 && tkl_lds_bytes<D>() <= 160 * 1024, "k_topk_scan_lds shape");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  float* heaps = reinterpret_cast<float*>(lds + NS * TB);
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int split = blockIdx.x % a.splits;
+  const int64_t user = (int64_t)(blockIdx.x / a.splits) * 128 + 32 * w + col;
+  const bool live = user < a.R;
+  const int64_t ntiles = (a.N + 31) / 32;
+  const int64_t t0 = (int64_t)split * a.tiles_per_split;
+  const int64_t t1 = min(ntiles, t0 + a.tiles_per_split);
+  const int64_t nt = t1 > t0 ? t1 - t0 : 0;
+  const float emax = *a.e_maxnorm;  // before any LDS-DMA is in flight
+
+  // u as the B operand: lane holds U[user][16 ks + 8 h .. + 7]
+  uint4 uf[KS];
+  float usq = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    float4 x = make_float4(0.f, 0.f, 0.f, 0.f), y = x;
+    if (live) {
+      x = *reinterpret_cast<const float4*>(a.U + user * a.ldu + 16 * ks + 8 * h);
+      y = *reinterpret_cast<const float4*>(a.U + user * a.ldu + 16 * ks + 8 * h + 4);
+    }
+    usq += (x.x * x.x + x.y * x.y) + (x.z * x.z + x.w * x.w) + (y.x * y.x + y.y * y.y) + (y.z * y.z + y.w * y.w);
+    uf[ks] = make_uint4(tk_pack_bf16x2(x.x, x.y), tk_pack_bf16x2(x.z, x.w), tk_pack_bf16x2(y.x, y.y),
+                        tk_pack_bf16x2(y.z, y.w));
+    __builtin_amdgcn_sched_barrier(0);  // a few k-steps' loads in flight, not all (register peak)
+  }
+  usq += __shfl_xor(usq, 32, 64);
+  const float eps = sqrtf(usq) * emax * (0x1p-8f + 0x1p-17f + 4.0f * D * 0x1p-24f) * 1.02f;
+  const int ku = live ? tk_ku(a, user) : 0;
+
+  // LDS-DMA (the decoder's version-2 image: 8-row x 32-column subtiles, 2-bit chunk XOR)
+  int vlane[2];
+#pragma unroll
+  for (int pb = 0; pb < 2; ++pb) {
+    const int row = 8 * pb + ((lane >> 2) & 7);
+    vlane[pb] = ((lane >> 2) & 7) * (D * 2) + 64 * (lane >> 5) + 16 * ((lane & 3) ^ ((row >> 2) & 3));
+  }
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.E), (short)0, (int)(a.N * D * 2), 0x00020000);
+  const uint32_t ring0 = tk_lds_addr(lds) + (uint32_t)(w * PW * 1024);
+  auto issue_pieces = [&](uint32_t soff, int slot_i, int i0, int i1, bool fresh) {
+    const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
+#pragma unroll
+    for (int i = i0; i < i1; ++i) {
+      const int p = w * PW + i;  // wave-uniform; PW need not be a multiple of 4 here, so p's own bits
+      const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
+      const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
+      if (fresh && i == i0)
+        asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+      else
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                     :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+    }
+  };
+  auto tile_soff = [&](int64_t t) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(32 * D * 2))); };
+  auto barrier = [&] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  const int laneA0 = ((col >> 3) << 11) + ((col & 7) << 6) + (((0 + h) ^ ((col >> 2) & 3)) << 4);
+  const int laneA1 = ((col >> 3) << 11) + ((col & 7) << 6) + (((2 + h) ^ ((col >> 2) & 3)) << 4);
+
+  TkSelect sel(a, heaps + (w * 32 + col) * HC, HC, user, live, h, eps, ku, split * 2);
+  if (nt > 0) {
+    issue_pieces(tile_soff(t0), 0, 0, PW, true);
+    if (NS == 3) issue_pieces(tile_soff(min(t0 + 1, t1 - 1)), 1, 0, PW, true);
+  }
+  for (int64_t j = 0; j < nt; ++j) {
+    const int64_t t = t0 + j;
+    const int cur = (int)(j % NS), s_dma = (int)((j + NS - 1) % NS);
+    // tile t has landed (three slots: issued two iterations back, younger ops may stay in flight; two slots:
+    // issued in the previous iteration, so everything is waited for)
+    if constexpr (NS == 3) tk_wait_vmcnt<PW>();
+    else tk_wait_vmcnt<0>();
+    barrier();  // every wave's pieces of t; every wave is done with the slot the next DMA reuses
+    const uint32_t soff_dma = tile_soff(min(t + NS - 1, t1 - 1));
+    const unsigned char* b0 = lds + cur * TB + laneA0;
+    const unsigned char* b1 = lds + cur * TB + laneA1;
+    auto rdA = [&](int ks) {
+      const int grp = ks >> 1;
+      return __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(((ks & 1) ? b1 : b0) + ((grp >> 2) << 13) +
+                                                                          ((grp & 3) << 9)));
+    };
+    f32x16_t s;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s[r] = 0.f;
+    bf16x8_t an[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) an[q] = rdA(q);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const bf16x8_t c = an[ks & 3];
+      if (ks + 4 < KS) an[ks & 3] = rdA(ks + 4);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c, __builtin_bit_cast(bf16x8_t, uf[ks]), s, 0, 0, 0);
+      if ((ks & 1) == 1 && (ks >> 1) < PW) issue_pieces(soff_dma, s_dma, ks >> 1, (ks >> 1) + 1, ks == 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (KS / 2 < PW) issue_pieces(soff_dma, s_dma, KS / 2, PW, false);
+    if (t * 32 + 32 > a.N) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h >= a.N) s[r] = -INFINITY;
+    }
+    sel.consume(a, s, t, j);
+  }
+  tk_wait_vmcnt<0>();  // the LDS-DMA lands before the block's LDS is released
+  if (live) a.cand_cnt[user * a.nseg + split * 2 + h] = sel.cnt;
 }
 
 // (score desc, item desc): a before b
@@ -279,6 +442,7 @@ struct TkSelArgs {
   int32_t* flag; // [R]
 };
 
+template <int NK>  // D / 64
 __global__ void __launch_bounds__(256) k_topk_select(TkSelArgs a) {
   __shared__ float ss[kTkMaxCand];
   __shared__ int si[kTkMaxCand];
@@ -335,15 +499,30 @@ __global__ void __launch_bounds__(256) k_topk_select(TkSelArgs a) {
     for (int i = tid; i < n; i += 256) si[o + i] = a.cand[(r * a.nseg + sgi) * kTkSegCap + i];
   }
   __syncthreads();
-  // exact fp32 rescore: one wave per candidate, lanes over D
+  // exact fp32 rescore: 16 lanes per candidate, 4 candidates per wave pass; lane g of a group owns float4
+  // columns g + 16 k (k < NK) of u (in registers) and of the candidate's E row, all NK loads in flight; the sum
+  // is over k in order, then a fixed xor tree over the group (deterministic)
   const float* u = a.U + r * a.ldu;
-  for (int c = w; c < C; c += 4) {
-    const int it = si[c];
-    const float* e = a.E32 + (int64_t)it * a.D;
-    float s = 0.f;
-    for (int64_t d = lane; d < a.D; d += 64) s += u[d] * e[d];
-    s = wave_sum(s);
-    if (lane == 0) {
+  const int g = lane & 15, slot = lane >> 4;
+  float4 u4[NK];
+#pragma unroll
+  for (int k = 0; k < NK; ++k) u4[k] = *reinterpret_cast<const float4*>(u + 4 * (g + 16 * k));
+  for (int c0 = w * 4; c0 < C; c0 += 16) {
+    const int c = c0 + slot;
+    const int it = c < C ? si[c] : 0;
+    const float4* e = reinterpret_cast<const float4*>(a.E32 + (int64_t)it * (16 * 4 * NK));
+    float4 e4[NK];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) e4[k] = e[g + 16 * k];
+    float sdot = 0.f;
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+      sdot += (u4[k].x * e4[k].x + u4[k].y * e4[k].y) + (u4[k].z * e4[k].z + u4[k].w * e4[k].w);
+    sdot += __shfl_xor(sdot, 8, 64);
+    sdot += __shfl_xor(sdot, 4, 64);
+    sdot += __shfl_xor(sdot, 2, 64);
+    sdot += __shfl_xor(sdot, 1, 64);
+    if (g == 0 && c < C) {
       int lo = 0, hi = nseen;  // binary search in the sorted seen list
       while (lo < hi) {
         const int md = (lo + hi) >> 1;
@@ -351,9 +530,10 @@ __global__ void __launch_bounds__(256) k_topk_select(TkSelArgs a) {
         else hi = md;
       }
       const bool is_seen = lo < nseen && seen[lo] == it;
-      ss[c] = (is_seen || s != s) ? -INFINITY : s;
+      ss[c] = (is_seen || sdot != sdot) ? -INFINITY : sdot;
     }
   }
+  __syncthreads();
   int P2 = 1;
   while (P2 < C) P2 <<= 1;
   for (int i = C + tid; i < P2; i += 256) { ss[i] = -INFINITY; si[i] = -1; }
@@ -380,13 +560,22 @@ __global__ void __launch_bounds__(256) k_topk_select(TkSelArgs a) {
   }
 }
 
-static int tk_splits(int64_t R, int64_t N, int K) {
-  const int64_t groups = cdiv(R, 32);
+static int tk_lds_scan(int64_t D) {  // HVAE_TOPK_LDS=0 keeps the global-load scan (A/B)
+  const char* v = getenv("HVAE_TOPK_LDS");
+  return D % 128 == 0 && ((v && *v) ? (atoi(v) != 0) : 1);
+}
+
+static int tk_wave_users() {  // HVAE_TOPK_WAVE_USERS=0 selects the tile-split mapping (A/B)
+  const char* v = getenv("HVAE_TOPK_WAVE_USERS");
+  return (v && *v) ? (atoi(v) != 0) : 1;
+}
+
+static int tk_splits(int64_t R, int64_t N, int wave_users) {
+  const int64_t groups = cdiv(R, wave_users ? 128 : 32);
   const int64_t tiles = cdiv(N, 32);
   int64_t s = std::max<int64_t>(1, cdiv(256, groups));  // ~256 blocks (one per CU: 128 KiB of heaps each)
-  s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 16));  // >= 4 tiles per wave
-  s = std::min<int64_t>(s, 128);  // nseg = 8 s <= 1024
-  (void)K;
+  s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / (wave_users ? 4 : 16)));  // >= 4 tiles per wave
+  s = std::min<int64_t>(s, wave_users ? 512 : 128);  // nseg <= 1024
   return (int)s;
 }
 
@@ -395,8 +584,9 @@ static int tk_splits(int64_t R, int64_t N, int K) {
 using namespace hvae;
 
 extern "C" size_t hvae_topk_fused_workspace(int64_t R, int64_t N, int64_t D, int64_t K) {
-  const int s = tk_splits(R, N, (int)K);
-  const size_t nseg = (size_t)s * 8;
+  const int wu = tk_lds_scan(D) ? 1 : tk_wave_users();
+  const int s = tk_splits(R, N, wu);
+  const size_t nseg = (size_t)s * (wu ? 2 : 8);
   return 256 + (size_t)R * 8 + (size_t)R * nseg * 4 + (size_t)R * nseg * kTkSegCap * 4 + (size_t)R * kTkSeed * 4;
 }
 
@@ -414,8 +604,10 @@ extern "C" int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, 
   if (exclude)
     HVAE_REQUIRE(exclude->row_ptr && exclude->col_idx && exclude->nb == R, "hvae_topk_fused: bad exclude");
   hipStream_t st = as_stream(stream);
-  const int splits = tk_splits(R, N, (int)K);
-  const int nseg = splits * 8;
+  const bool lds_scan = tk_lds_scan(D);
+  const int wu = lds_scan ? 1 : tk_wave_users();
+  const int splits = tk_splits(R, N, wu);
+  const int nseg = splits * (wu ? 2 : 8);
   unsigned char* p = static_cast<unsigned char*>(ws);
   int* g_tau = reinterpret_cast<int*>(p + 256);
   float* g_eps = reinterpret_cast<float*>(g_tau + R);
@@ -427,13 +619,20 @@ extern "C" int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, 
   TkScanArgs sa{U, ldu, static_cast<const bf16_t*>(E_bf16), e32_maxnorm, R, N,
                 exclude ? exclude->row_ptr : nullptr, exclude ? exclude->rows : nullptr,
                 exclude ? exclude->rows_offset : nullptr, (int)K, splits, cdiv(cdiv(N, 32), splits), g_tau, g_eps,
-                seed, cand, cnt, nseg};
+                seed, cand, cnt, nseg, wu};
   const int64_t ntiles = cdiv(N, 32);
   const int nsample = (int)std::min<int64_t>(ntiles, kTkSeedTiles);
   const int64_t stride = std::max<int64_t>(1, ntiles / nsample);
-  const unsigned groups = (unsigned)cdiv(R, 32);
-  const unsigned blocks = (unsigned)(groups * splits);
+  const unsigned groups = (unsigned)cdiv(R, 32);  // the seed pass: one block per 32 users
+  const unsigned blocks = (unsigned)(cdiv(R, wu ? 128 : 32) * splits);
   const size_t lds = (size_t)4 * 32 * kTkHeap * 4;
+#define TK_SCAN_LDS(DD)                                                                                 \
+  {                                                                                                       \
+    constexpr int DL = DD % 128 == 0 ? DD : 128;                                                          \
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_topk_scan_lds<DL>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                 tkl_lds_bytes<DL>()));                                                   \
+    k_topk_scan_lds<DL><<<blocks, 256, tkl_lds_bytes<DL>(), st>>>(sa);                                   \
+  }
   switch (D) {
 #define TK_CASE(DD)                                                                                       \
   case DD:                                                                                                \
@@ -441,18 +640,30 @@ extern "C" int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, 
     HVAE_LAUNCH_CHECK("k_topk_seed");                                                                     \
     k_topk_seed_select<<<(unsigned)R, 256, 0, st>>>(sa, nsample);                                         \
     HVAE_LAUNCH_CHECK("k_topk_seed_select");                                                              \
-    HVAE_HIP(hipFuncSetAttribute((const void*)k_topk_scan<DD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                 (int)lds));                                                              \
-    k_topk_scan<DD><<<blocks, 256, lds, st>>>(sa);                                                        \
+    if (DD % 128 == 0 && lds_scan) {                                                                      \
+      TK_SCAN_LDS(DD)                                                                                     \
+    } else {                                                                                              \
+      HVAE_HIP(hipFuncSetAttribute((const void*)k_topk_scan<DD>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                   (int)lds));                                                            \
+      k_topk_scan<DD><<<blocks, 256, lds, st>>>(sa);                                                      \
+    }                                                                                                     \
     HVAE_LAUNCH_CHECK("k_topk_scan");                                                                     \
     break;
     TK_CASE(64) TK_CASE(128) TK_CASE(256) TK_CASE(384) TK_CASE(512) TK_CASE(768)
 #undef TK_CASE
+#undef TK_SCAN_LDS
   }
   TkSelArgs la{U, ldu, E32, R, N, D, exclude ? exclude->row_ptr : nullptr, exclude ? exclude->col_idx : nullptr,
                exclude ? exclude->rows : nullptr, exclude ? exclude->rows_offset : nullptr, (int)K, cand, cnt, nseg,
                idx, val, flag};
-  k_topk_select<<<(unsigned)R, 256, 0, st>>>(la);
+  switch (D) {
+    case 64: k_topk_select<1><<<(unsigned)R, 256, 0, st>>>(la); break;
+    case 128: k_topk_select<2><<<(unsigned)R, 256, 0, st>>>(la); break;
+    case 256: k_topk_select<4><<<(unsigned)R, 256, 0, st>>>(la); break;
+    case 384: k_topk_select<6><<<(unsigned)R, 256, 0, st>>>(la); break;
+    case 512: k_topk_select<8><<<(unsigned)R, 256, 0, st>>>(la); break;
+    default: k_topk_select<12><<<(unsigned)R, 256, 0, st>>>(la); break;
+  }
   HVAE_LAUNCH_CHECK("k_topk_select");
   return HVAE_OK;
 }

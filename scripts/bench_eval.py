@@ -72,7 +72,17 @@ def main():
         S = ops.gemm(u, model.item_embeddings.t())
         return ops.topk(S, k, exclude=c)
 
-    arms = [("topk_fused", run_fused)] + ([] if args.skip_matrix else [("topk_matrix", run_matrix)])
+    import os
+
+    def run_fused_global(rows):  # A/B: the scan reading E fragments straight from global memory
+        os.environ["HVAE_TOPK_LDS"] = "0"
+        try:
+            return run_fused(rows)
+        finally:
+            os.environ.pop("HVAE_TOPK_LDS")
+
+    arms = [("topk_fused", run_fused), ("topk_fused_global_scan", run_fused_global)] + \
+        ([] if args.skip_matrix else [("topk_matrix", run_matrix)])
     res = {}
     rows = [batch_rows() for _ in range(args.reps)]  # the same batches for every arm
     for name, fn in arms:
