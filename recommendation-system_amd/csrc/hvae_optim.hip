@@ -369,7 +369,10 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
 // with t) through step t with g = 0 -- skipping rows with a gradient, which the first
 // group owns -- so that no row ever lags more than kLazySweep steps; the rest run the
 // dense segment. Row work is column-parallel (RowMap).
-constexpr int kLazySweep = 8;
+#ifndef HVAE_LAZY_SWEEP
+#define HVAE_LAZY_SWEEP 8
+#endif
+constexpr int kLazySweep = HVAE_LAZY_SWEEP;
 __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restrict__ tab, float* __restrict__ p,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    int32_t* __restrict__ last_step, const float* __restrict__ rows,
