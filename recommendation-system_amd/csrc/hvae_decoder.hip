@@ -1195,10 +1195,15 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
 #ifndef DEC4_G1_AHEAD
 #define DEC4_G1_AHEAD 2  // GEMM1 A operand k-steps in flight
 #endif
-__host__ __device__ constexpr int d4_lds_bytes(int D) { return 3 * ((D / 128) * 8192) + 2 * 2 * 32 * 80 + 4 * 64 * 4; }
+// NW waves per block = NW / 2 user groups x 2 D halves (NW = 8: two waves per SIMD, <= 256 registers each --
+// d = 384, where u over all of D takes 96 VGPRs and O's half 96 AGPRs). A D half that is not a whole number of
+// 128-column segments (d = 384) owns every other 32-column d-block instead (block 2 db + dh).
+__host__ __device__ constexpr int d4_lds_bytes(int D, int NW) {
+  return 3 * ((D / 128) * 8192) + 2 * (NW / 2) * 32 * 80 + NW * 64 * 4;
+}
 
-template <int D, bool WITH_O>
-__global__ void __launch_bounds__(256) k_dec4_bf16(const float* __restrict__ U, int64_t ldu,
+template <int D, int NW, bool WITH_O>
+__global__ void __launch_bounds__(64 * NW) k_dec4_bf16(const float* __restrict__ U, int64_t ldu,
                                                    const bf16_t* __restrict__ E, const float* __restrict__ e_maxnorm,
                                                    int64_t nb, int64_t N, int splits, int64_t tiles_per_split,
                                                    DecOut out) {
@@ -1207,21 +1212,23 @@ __global__ void __launch_bounds__(256) k_dec4_bf16(const float* __restrict__ U, 
   constexpr int KS = D / 32;        // GEMM1 k-steps (16x16x32, all of D)
   constexpr int NSEG = D / 128;
   constexpr int TB = NSEG * 8192;
-  constexpr int PW = NSEG * 8 / 4;  // 1-KiB LDS-DMA pieces per wave per tile
+  constexpr int NUG = NW / 2;       // user groups per block
+  constexpr int PW = NSEG * 8 / NW; // 1-KiB LDS-DMA pieces per wave per tile
   constexpr int NS = 3;
   constexpr int PST = 80;           // P row stride (bytes)
-  static_assert(D % 128 == 0 && (DW / 32) % 4 == 0 && PW % 2 == 0 && d4_lds_bytes(D) <= 160 * 1024,
+  constexpr bool SEGH = DW % 128 == 0;  // a D half is whole segments (else interleaved d-blocks)
+  static_assert(D % 128 == 0 && (NSEG * 8) % NW == 0 && (NW == 4 || NW == 8) && d4_lds_bytes(D, NW) <= 160 * 1024,
                 "k_dec4_bf16 shape");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  unsigned char* pbuf = lds + NS * TB;                                 // [2 parity][2 ug][32 users][PST]
-  float* xm = reinterpret_cast<float*>(lds + NS * TB + 2 * 2 * 32 * PST);  // [4 w][64]: max / sum exchange
+  unsigned char* pbuf = lds + NS * TB;                                     // [2 parity][NUG ug][32 users][PST]
+  float* xm = reinterpret_cast<float*>(lds + NS * TB + 2 * NUG * 32 * PST);  // [NW w][64]: max / sum exchange
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
   const int c16 = lane & 15, g = lane >> 4;  // GEMM1 layout: users c16 + 16 nb, items 4 g .. 4 g + 3
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ug = w & 1, dh = w >> 1, pw = w ^ 2;
+  const int ug = w & (NUG - 1), dh = w / NUG, pw = w ^ NUG;
   const int split = blockIdx.x % splits;
-  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 64 + ug * 32;
+  const int64_t u0 = (int64_t)(blockIdx.x / splits) * (32 * NUG) + ug * 32;
   const int64_t user = u0 + col;  // GEMM2 / output layout
   const bool wave_active = u0 < nb;
   const int64_t ntiles = (N + kBfTI - 1) / kBfTI;
@@ -1272,9 +1279,9 @@ __global__ void __launch_bounds__(256) k_dec4_bf16(const float* __restrict__ U, 
     const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
 #pragma unroll
     for (int i = i0; i < i1; ++i) {
-      const int p = w * PW + i;
-      const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (i & 1));
-      const int vo = vlane[(i >> 1) & 1];
+      const int p = w * PW + i;  // wave-uniform; its own bits (PW need not be a multiple of 4)
+      const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
+      const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
       if (fresh && i == i0)
         asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                      :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
@@ -1322,7 +1329,10 @@ __global__ void __launch_bounds__(256) k_dec4_bf16(const float* __restrict__ U, 
   };
   // GEMM2 (version 3's reads): O^T[DW][32 users] += E^T P^T over k-steps 0 (items 0..15) and 1 (16..31)
   const int g1 = (lane >> 4) & 1, q = (lane >> 2) & 3, pp = lane & 3;
-  const int cseg = (dbase / 128) << 13;
+  // the wave's d-block db: global 32-column block dbase / 32 + db (SEGH) or 2 db + dh
+  const int cseg = SEGH ? (dbase / 128) << 13 : dh << 9;
+  auto dboff = [](int db) { return SEGH ? ((db >> 2) << 13) + ((db & 3) << 9) : ((db >> 1) << 13) + ((db & 1) << 10); };
+  auto dcol = [&](int db) { return SEGH ? dbase + 32 * db : 32 * (2 * db + dh); };
   const int laneT0 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((0 + h) & 3)) << 4) + 8 * (pp & 1);
   const int laneT1 = ((4 * h + q) << 6) + (((2 * g1 + (pp >> 1)) ^ ((2 + h) & 3)) << 4) + 8 * (pp & 1);
   f32x16 o[WITH_O ? DB : 1];
@@ -1334,9 +1344,8 @@ __global__ void __launch_bounds__(256) k_dec4_bf16(const float* __restrict__ U, 
   auto rdT = [&](const unsigned char* buf, int i) {
     const int kh = i / DB, db = i % DB;
     const unsigned char* t = buf + cseg + (kh << 12);
-    auto* p0 = (__attribute__((address_space(3))) s16x4*)(void*)(t + laneT0 + ((db >> 2) << 13) + ((db & 3) << 9));
-    auto* p1 = (__attribute__((address_space(3))) s16x4*)(void*)(t + laneT1 + (1 << 11) + ((db >> 2) << 13) +
-                                                                 ((db & 3) << 9));
+    auto* p0 = (__attribute__((address_space(3))) s16x4*)(void*)(t + laneT0 + dboff(db));
+    auto* p1 = (__attribute__((address_space(3))) s16x4*)(void*)(t + laneT1 + (1 << 11) + dboff(db));
     return std::array<s16x4, 2>{__builtin_amdgcn_ds_read_tr16_b64_v4i16(p0), __builtin_amdgcn_ds_read_tr16_b64_v4i16(p1)};
   };
   auto gemm2 = [&](const unsigned char* buf, const uint4& pf0, const uint4& pf1, auto&& fill) {
@@ -1362,7 +1371,7 @@ __global__ void __launch_bounds__(256) k_dec4_bf16(const float* __restrict__ U, 
   };
   // P rows: pbuf[par][ug][user][PST]; own half at k-step dh; lane's items 4 g .. 4 g + 3 -> positions
   // 16 dh + 8 (g & 1) + 4 (g >> 1)
-  auto p_row = [&](int par, int uu) { return pbuf + ((par * 2 + ug) * 32 + uu) * PST; };
+  auto p_row = [&](int par, int uu) { return pbuf + ((par * NUG + ug) * 32 + uu) * PST; };
   const int ppos = 2 * (16 * dh + 8 * (g & 1) + 4 * (g >> 1));
 
   float m[2] = {0.f, 0.f}, mL[2] = {0.f, 0.f}, lsum[2] = {0.f, 0.f};
@@ -1483,7 +1492,7 @@ __global__ void __launch_bounds__(256) k_dec4_bf16(const float* __restrict__ U, 
     for (int d = 0; d < (WITH_O ? DB : 1); ++d)
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
-        const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
+        const int dd = dcol(d) + 8 * g4 + 4 * h;
         *reinterpret_cast<float4*>(out.O + row * D + dd) =
             make_float4(o[d][4 * g4] * sc, o[d][4 * g4 + 1] * sc, o[d][4 * g4 + 2] * sc, o[d][4 * g4 + 3] * sc);
       }
@@ -2562,7 +2571,7 @@ struct DecPlan {
   size_t lds;
   int v2;    // bf16 version-2 sweep (k_dec2_bf16)
   int v3;    // bf16 version-3 sweep (k_dec3_bf16, D = 768)
-  int v4;    // bf16 version-4 sweep (k_dec4_bf16, D = 768)
+  int v4;    // bf16 version-4 sweep (k_dec4_bf16: D = 768 with 4 waves, D = 384 with 8)
   int ds;    // its D split (1 or 2)
   int nw;    // its waves per block (4, or 8 with ds = 2)
   int64_t upb;
@@ -2596,6 +2605,8 @@ static bool v2_supported(int64_t D) { return D == 64 || D == 128 || D == 256 || 
 static bool v3_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V3", 1) != 0; }
 // HVAE_DEC_V4=0 keeps version 3 at D = 768 (A/B; read at every plan)
 static bool v4_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V4", 1) != 0; }
+// HVAE_DEC_V4_384=1 runs version 4 with 8 waves at D = 384 (large batches) instead of version 2's DS = 1 sweep
+static bool v4_384(int64_t D, int64_t nb) { return D == 384 && nb > 64 && env_int("HVAE_DEC_V4_384", 0) != 0; }
 
 static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
   s = std::max<int64_t>(1, std::min<int64_t>(s, std::min<int64_t>(tiles, kMaxSplits)));
@@ -2622,12 +2633,12 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   const bool bf = dtype == HVAE_BF16;
   p.v2 = bf && !dec_use_v1() && v2_supported(D);
   p.v3 = p.v2 && v3_supported(D);
-  p.v4 = p.v3 && v4_supported(D);
+  p.v4 = (p.v3 && v4_supported(D)) || (p.v2 && v4_384(D, nb));
   p.ds = p.v2 && (D > 384 || nb <= 64) ? 2 : 1;
   if (p.v2 && D <= 384 && (dec_forced_ds() == 1 || dec_forced_ds() == 2)) p.ds = dec_forced_ds();
   p.nw = p.v2 && p.ds == 2 && nb > 64 && D <= 384 ? 8 : 4;
   if (p.v2 && p.ds == 2 && D <= 384 && (dec_forced_nw() == 4 || dec_forced_nw() == 8)) p.nw = dec_forced_nw();
-  p.upb = bf ? (p.v3 ? 64 : p.v2 ? 32 * p.nw / p.ds : kBfUsersPerBlock) : kF32UsersPerBlock;
+  p.upb = bf ? (p.v4 && D == 384 ? 128 : p.v3 ? 64 : p.v2 ? 32 * p.nw / p.ds : kBfUsersPerBlock) : kF32UsersPerBlock;
   const int64_t ti = bf ? kBfTI : kF32TI;
   const int64_t target = bf ? 256 : 512;
   const int64_t nub = cdiv(nb, p.upb), tiles = cdiv(N, ti);
@@ -2716,15 +2727,17 @@ static int launch_bf16_v3(const float* U, int64_t ldu, const void* E, const floa
 template <int D, bool WO>
 static int launch_bf16_v4(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                           const DecPlan& p, DecOut o, hipStream_t st) {
-  constexpr int lds = d4_lds_bytes(D);
+  constexpr int NW = D == 768 ? 4 : 8;
+  constexpr int lds = d4_lds_bytes(D, NW);
   static_assert(lds <= 160 * 1024, "k_dec4_bf16 LDS");
   static bool attr_set = false;
   if (!attr_set) {
-    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec4_bf16<D, WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec4_bf16<D, NW, WO>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 lds));
     attr_set = true;
   }
-  k_dec4_bf16<D, WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N, p.splits,
-                                                          p.tiles_per_split, o);
+  k_dec4_bf16<D, NW, WO><<<(unsigned)p.blocks, 64 * NW, lds, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N,
+                                                                  p.splits, p.tiles_per_split, o);
   HVAE_LAUNCH_CHECK("k_dec4_bf16");
   return HVAE_OK;
 }
@@ -2775,6 +2788,8 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
     }
   } else if (dtype == HVAE_BF16 && p.v4 && D == 768) {
     return launch_bf16_v4<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+  } else if (dtype == HVAE_BF16 && p.v4 && D == 384) {
+    return launch_bf16_v4<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
   } else if (dtype == HVAE_BF16 && p.v3 && D == 768) {
     return launch_bf16_v3<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
   } else if (dtype == HVAE_BF16 && p.v2) {
