@@ -2610,7 +2610,7 @@ static bool v4_384(int64_t D, int64_t nb) { return D == 384 && nb > 64 && env_in
 
 static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
   s = std::max<int64_t>(1, std::min<int64_t>(s, std::min<int64_t>(tiles, kMaxSplits)));
-  p.tiles_per_split = cdiv(tiles, s);
+  p.tiles_per_split = std::max<int64_t>(1, cdiv(tiles, s));  // N = 0: one empty split
   p.splits = (int)cdiv(tiles, p.tiles_per_split);
 }
 
@@ -2620,7 +2620,7 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
     p.ds = D > 384 ? 2 : 1;
     p.upb = 128 / p.ds;
     const int64_t nub = cdiv(nb, p.upb), tiles = cdiv(N, kF8TI);
-    int64_t s = cdiv(256, nub);
+    int64_t s = cdiv(256, std::max<int64_t>(1, nub));  // nb = 0: a workspace query
     s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 2));
     s = std::min<int64_t>(s, std::max<int64_t>(1, N / std::max<int64_t>(1, 2 * nb)));
     if (s >= 8) s = s / 8 * 8;
@@ -2642,7 +2642,7 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   const int64_t ti = bf ? kBfTI : kF32TI;
   const int64_t target = bf ? 256 : 512;
   const int64_t nub = cdiv(nb, p.upb), tiles = cdiv(N, ti);
-  int64_t s = cdiv(target, nub);
+  int64_t s = cdiv(target, std::max<int64_t>(1, nub));
   s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / 2));
   // each split writes nb (D + 2) floats of partials: keep them below ~2x the E bytes it streams
   s = std::min<int64_t>(s, std::max<int64_t>(1, (bf ? N : 2 * N) / std::max<int64_t>(1, 2 * nb)));

@@ -411,7 +411,7 @@ static int gemm_splits(int64_t M, int64_t N, int64_t K) {
   const int bt = gemm_tile(M, N, K);
   const int64_t tiles = cdiv(M, bt) * cdiv(N, bt);
   const int64_t kreg = (int64_t)GBK * kRegStages;
-  if (K <= kreg || tiles >= 256) return 1;  // short K: all loads in flight at once, no split needed
+  if (K <= kreg || tiles == 0 || tiles >= 256) return 1;  // (tiles == 0: an empty product)  // short K: all loads in flight at once, no split needed
   // about 256 blocks, with no floor at K / kreg: a block may stream more k-tiles than it stages in
   // registers. Fewer partial tiles measured faster on MI355X: 256x512x4096 47.1 -> 39.9 us, 384x384x4096
   // 46.9 -> 45.6 us (profiles/r01_gemm_dw_splitk_ab_v19.jsonl)

@@ -571,7 +571,7 @@ static int tk_wave_users() {  // HVAE_TOPK_WAVE_USERS=0 selects the tile-split m
 }
 
 static int tk_splits(int64_t R, int64_t N, int wave_users) {
-  const int64_t groups = cdiv(R, wave_users ? 128 : 32);
+  const int64_t groups = std::max<int64_t>(1, cdiv(R, wave_users ? 128 : 32));  // R = 0: a workspace query
   const int64_t tiles = cdiv(N, 32);
   int64_t s = std::max<int64_t>(1, cdiv(256, groups));  // ~256 blocks (one per CU: 128 KiB of heaps each)
   s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / (wave_users ? 4 : 16)));  // >= 4 tiles per wave

@@ -110,3 +110,33 @@ def test_topk_fused_flagged_rows_take_the_exact_path(hip_device):
     top5 = sorted(range(N), key=lambda i: (-S4[i].item(), -i))[:5]
     assert idx[4, :5].cpu().tolist() == top5
     assert torch.isinf(val[4, 5:]).all()
+
+
+@pytest.mark.parametrize("R,N,D,k", [(1, 200_000, 768, 10), (5, 20, 128, 5), (3, 50, 256, 50), (2, 31, 64, 7),
+                                     (70, 4097, 384, 1)])
+def test_topk_fused_edge_shapes(hip_device, R, N, D, k):
+    """A single user over 200 K items, fewer items than one 32-item tile, k = N, a partial last tile, k = 1."""
+    from hvae import ops
+    U, E, Ud, Ed, img, emax = _case(hip_device, R, N, D, seed=3 * N + D)
+    idx, val = ops.topk_fused(Ud, img, Ed, emax, k)
+    _check(idx, val, U, E, k)
+
+
+def test_topk_fused_exclusion_edges(hip_device):
+    """Rows with nothing seen, and a row whose unseen items number exactly k."""
+    from scipy.sparse import csr_matrix
+    from hvae import ops
+    R, N, D, k = 4, 600, 128, 6
+    U, E, Ud, Ed, img, emax = _case(hip_device, R, N, D, seed=17)
+    rows = [2] * (N - k) + [3, 3]
+    cols = list(range(N - k)) + [7, 590]
+    X = csr_matrix((np.ones(len(rows), np.float32), (rows, cols)), shape=(R, N))
+    csr = ops.csr_from_scipy(X, hip_device)
+    ex = ops.Csr(csr.row_ptr, csr.col_idx, csr.vals, N, rows=torch.arange(R, dtype=torch.int32, device=hip_device))
+    idx, val = ops.topk_fused(Ud, img, Ed, emax, k, exclude=ex)
+    X.sort_indices()
+    seen = [torch.as_tensor(X[r].indices.astype(np.int64)) for r in range(R)]
+    _check(idx, val, U, E, k, seen)
+    assert sorted(idx[2].cpu().tolist()) == list(range(N - k, N))  # exactly the k unseen items
+    R0 = ops.topk_fused(Ud[:0], img, Ed, emax, k)
+    assert R0[0].shape == (0, k)
