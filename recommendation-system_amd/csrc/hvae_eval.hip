@@ -105,9 +105,9 @@ using namespace hvae;
 extern "C" int hvae_score_candidates(const float* U, int64_t ldu, const int32_t* user_row, const float* E32,
                                      int64_t D, const int32_t* cand, int64_t R, int64_t C, float* scores,
                                      void* stream) {
-  HVAE_REQUIRE(U && user_row && E32 && cand && scores && ldu >= D && D > 0 && C > 0,
-               "hvae_score_candidates: bad args");
-  if (R == 0) return HVAE_OK;
+  HVAE_REQUIRE(R >= 0 && ldu >= D && D > 0 && C > 0, "hvae_score_candidates: bad args");
+  if (R == 0) return HVAE_OK;  // empty outputs may have null data pointers
+  HVAE_REQUIRE(U && user_row && E32 && cand && scores, "hvae_score_candidates: null pointer");
   k_score_candidates<<<(unsigned)cdiv(R, 4), 256, 0, as_stream(stream)>>>(U, ldu, user_row, E32, D, cand, R,
                                                                           C, scores);
   HVAE_LAUNCH_CHECK("k_score_candidates");
@@ -115,8 +115,9 @@ extern "C" int hvae_score_candidates(const float* U, int64_t ldu, const int32_t*
 }
 
 extern "C" int hvae_rank_first(const float* scores, int64_t R, int64_t C, int32_t* rank, void* stream) {
-  HVAE_REQUIRE(scores && rank && C > 0, "hvae_rank_first: bad args");
+  HVAE_REQUIRE(R >= 0 && C > 0, "hvae_rank_first: bad args");
   if (R == 0) return HVAE_OK;
+  HVAE_REQUIRE(scores && rank, "hvae_rank_first: null pointer");
   k_rank_first<<<(unsigned)cdiv(R, 256), 256, 0, as_stream(stream)>>>(scores, R, C, rank);
   HVAE_LAUNCH_CHECK("k_rank_first");
   return HVAE_OK;
@@ -124,9 +125,9 @@ extern "C" int hvae_rank_first(const float* scores, int64_t R, int64_t C, int32_
 
 extern "C" int hvae_topk(const float* scores, int64_t R, int64_t N, int64_t ld, const hvae_csr_batch* exclude,
                          int64_t K, int32_t* idx, float* val, void* stream) {
-  HVAE_REQUIRE(scores && idx && ld >= N && K > 0 && K <= N && K <= 1024 && N < INT32_MAX,
-               "hvae_topk: bad args");
+  HVAE_REQUIRE(R >= 0 && ld >= N && K > 0 && K <= N && K <= 1024 && N < INT32_MAX, "hvae_topk: bad args");
   if (R == 0) return HVAE_OK;
+  HVAE_REQUIRE(scores && idx, "hvae_topk: null pointer");
   hipStream_t st = as_stream(stream);
   if (exclude) {
     HVAE_REQUIRE(exclude->row_ptr && exclude->col_idx && exclude->nb == R, "hvae_topk: bad exclude");

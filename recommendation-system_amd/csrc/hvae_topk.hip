@@ -594,12 +594,11 @@ extern "C" int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, 
                                const float* e32_maxnorm, int64_t N, int64_t D, const hvae_csr_batch* exclude,
                                int64_t R, int64_t K, int32_t* idx, float* val, int32_t* flag, void* ws,
                                size_t ws_bytes, void* stream) {
-  HVAE_REQUIRE(U && E_bf16 && E32 && e32_maxnorm && idx && flag && ldu >= D && K > 0 && K <= kTkHeap &&
-                   K <= N && N < INT32_MAX,
-               "hvae_topk_fused: bad args");
+  HVAE_REQUIRE(R >= 0 && ldu >= D && K > 0 && K <= kTkHeap && K <= N && N < INT32_MAX, "hvae_topk_fused: bad args");
   HVAE_REQUIRE(D == 64 || D == 128 || D == 256 || D == 384 || D == 512 || D == 768,
                "hvae_topk_fused: D must be 64, 128, 256, 384, 512 or 768");
-  if (R == 0) return HVAE_OK;
+  if (R == 0) return HVAE_OK;  // an empty batch: its (empty) output tensors may have null data pointers
+  HVAE_REQUIRE(U && E_bf16 && E32 && e32_maxnorm && idx && flag, "hvae_topk_fused: null pointer");
   HVAE_REQUIRE(ws && ws_bytes >= hvae_topk_fused_workspace(R, N, D, K), "hvae_topk_fused: workspace too small");
   if (exclude)
     HVAE_REQUIRE(exclude->row_ptr && exclude->col_idx && exclude->nb == R, "hvae_topk_fused: bad exclude");

@@ -20,10 +20,10 @@ import torch  # noqa: E402
 from hvae import _lib, ops  # noqa: E402
 from hvae._lib import check, lib  # noqa: E402
 
-H, L, D = 512, 128, 384
+H, L = 512, 128
 
 
-def shapes(B):
+def shapes(B, D=384):
     # (name, M, N, K, trans_a, trans_b) -- nn.Linear forward is NT, data grads NN, weight grads TN
     return [
         ("fwd_heads", B, 2 * L, H, False, True),
@@ -42,11 +42,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--d", type=int, default=384, help="SBERT width (384: All_Beauty / Syn-1M, 768: Syn-10M)")
+    ap.add_argument("--only", default=None, help="comma-separated shape names")
+    ap.add_argument("--no-torch", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device="cpu").manual_seed(0)
     out = {}
-    for name, M, N, K, ta, tb in shapes(args.batch):
+    for name, M, N, K, ta, tb in shapes(args.batch, args.d):
+        if args.only and name not in args.only.split(","):
+            continue
         a = torch.randn(K, M, generator=g).to(dev).t() if ta else torch.randn(M, K, generator=g).to(dev)
         b = torch.randn(N, K, generator=g).to(dev).t() if tb else torch.randn(K, N, generator=g).to(dev)
         rs = torch.empty(M, device=dev)
@@ -64,6 +69,11 @@ def main():
         check(lib().hvae_probe_arm(None, 0), "disarm")
         ref = a.double() @ b.double()
         err = float((c.double() - ref).abs().max() / ref.abs().max())
+        if args.no_torch:
+            out[name] = {"M": M, "N": N, "K": K, "hvae_us": round(avg.value, 2), "rel_err": err,
+                         "tflops": round(2.0 * M * N * K / avg.value / 1e6, 1)}
+            print(json.dumps({name: out[name]}), flush=True)
+            continue
         # torch.mm for scale
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(10):
@@ -75,7 +85,8 @@ def main():
         e.record()
         torch.cuda.synchronize()
         out[name] = {"M": M, "N": N, "K": K, "hvae_us": round(avg.value, 2), "torch_mm_us": round(
-            s.elapsed_time(e) * 1e3 / args.reps, 2), "rel_err": err}
+            s.elapsed_time(e) * 1e3 / args.reps, 2), "rel_err": err,
+            "tflops": round(2.0 * M * N * K / avg.value / 1e6, 1)}
         print(json.dumps({name: out[name]}), flush=True)
 
 
