@@ -191,6 +191,90 @@ def train_step(p: dict[str, torch.Tensor], state: dict, x: torch.Tensor, beta: f
     return {"grads": g, "loss": losses, "total_norm": total, "coef": coef}
 
 
+class CpuTrainer:
+    """The reference's train step as its own modules run it, for bench.py's cpu_baseline leg.
+
+    train_step above is the checker (explicit tensors, autograd.grad on clones); this class is the same
+    math laid out the way VAETrainer.train_epoch executes it (src/ml/train.py:81-103), so that its CPU
+    time stands for the reference's: nn.Linear / nn.LayerNorm / nn.GELU / nn.Dropout in the encoder's
+    Sequential order (src/ml/model.py:103-136), F.log_softmax in the loss (:259-292), loss.backward(),
+    clip_grad_norm_(5.0) and torch.optim.Adam over model.parameters() order. Dropout masks and the
+    reparameterisation noise may be injected (then the step equals train_step's;
+    tests/test_oracle_golden.py pins that), else they are drawn as the reference draws them.
+    """
+
+    def __init__(self, p: dict[str, torch.Tensor], dropout: float, lr: float = 1e-3, weight_decay: float = 0.0):
+        nn = torch.nn
+        self.dropout = dropout
+        enc = []
+        for k, h in enumerate(hidden_layout(p)):
+            i = 4 * k
+            lin = nn.Linear(p[f"encoder.{i}.weight"].shape[1], h)
+            ln = nn.LayerNorm(h)
+            with torch.no_grad():
+                lin.weight.copy_(p[f"encoder.{i}.weight"]); lin.bias.copy_(p[f"encoder.{i}.bias"])
+                ln.weight.copy_(p[f"encoder.{i + 1}.weight"]); ln.bias.copy_(p[f"encoder.{i + 1}.bias"])
+            enc.append((lin, ln))
+        self.enc = enc
+
+        def linear(name):
+            w = p[f"{name}.weight"]
+            m = nn.Linear(w.shape[1], w.shape[0])
+            with torch.no_grad():
+                m.weight.copy_(w); m.bias.copy_(p[f"{name}.bias"])
+            return m
+        self.fc_mu, self.fc_logvar = linear("fc_mu"), linear("fc_logvar")
+        self.proj = (linear("projection_layer.0"), linear("projection_layer.3")) \
+            if "projection_layer.0.weight" in p else None
+        self.E = p["item_embeddings"]
+        params = []
+        for lin, ln in enc:
+            params += [lin.weight, lin.bias, ln.weight, ln.bias]
+        params += [self.fc_mu.weight, self.fc_mu.bias, self.fc_logvar.weight, self.fc_logvar.bias]
+        if self.proj:
+            params += [self.proj[0].weight, self.proj[0].bias, self.proj[1].weight, self.proj[1].bias]
+        self.params = params
+        self.opt = torch.optim.Adam(params, lr=lr, weight_decay=weight_decay)
+
+    def _drop(self, h, mask):
+        return h * mask if mask is not None else torch.nn.functional.dropout(h, self.dropout, training=True)
+
+    def step(self, x: torch.Tensor, beta: float, enc_masks=None, proj_mask=None, eps=None) -> float:
+        F = torch.nn.functional
+        self.opt.zero_grad()
+        h = x
+        for k, (lin, ln) in enumerate(self.enc):
+            h = self._drop(F.gelu(ln(lin(h))), enc_masks[k] if enc_masks is not None else None)
+        mu, logvar = self.fc_mu(h), self.fc_logvar(h)
+        std = torch.exp(0.5 * logvar)
+        z = mu + (eps if eps is not None else torch.randn_like(std)) * std
+        u = z
+        if self.proj:
+            u = self.proj[1](self._drop(F.gelu(self.proj[0](z)), proj_mask))
+        scores = u @ self.E.t()
+        recon = -torch.mean(torch.sum(x * F.log_softmax(scores, dim=-1), dim=-1))
+        kl = -0.5 * torch.sum(1 + logvar - mu.pow(2) - logvar.exp()) / x.shape[0]
+        loss = recon + beta * kl
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(self.params, max_norm=5.0)
+        self.opt.step()
+        return float(loss.item())
+
+    def state(self) -> dict[str, torch.Tensor]:
+        """Parameters under the reference's state-dict names (for the pinning test)."""
+        out = {}
+        for k, (lin, ln) in enumerate(self.enc):
+            i = 4 * k
+            out[f"encoder.{i}.weight"], out[f"encoder.{i}.bias"] = lin.weight, lin.bias
+            out[f"encoder.{i + 1}.weight"], out[f"encoder.{i + 1}.bias"] = ln.weight, ln.bias
+        out["fc_mu.weight"], out["fc_mu.bias"] = self.fc_mu.weight, self.fc_mu.bias
+        out["fc_logvar.weight"], out["fc_logvar.bias"] = self.fc_logvar.weight, self.fc_logvar.bias
+        if self.proj:
+            out["projection_layer.0.weight"], out["projection_layer.0.bias"] = self.proj[0].weight, self.proj[0].bias
+            out["projection_layer.3.weight"], out["projection_layer.3.bias"] = self.proj[1].weight, self.proj[1].bias
+        return {k: v.detach() for k, v in out.items()}
+
+
 # ------------------------------------------------------------------ data ---
 def build_matrix(users: np.ndarray, items: np.ndarray, binary: np.ndarray | None, shape) -> "scipy.sparse.csr_matrix":
     """_build_matrix (src/ml/train.py:175-182): positives only, duplicates summed."""

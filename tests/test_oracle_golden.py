@@ -96,6 +96,26 @@ def test_train_steps(golden, name):
         _close_max(state[n][1], golden[f"g2{name}_s2_v_{n}"], 1e-5, f"v {n}")
 
 
+@pytest.mark.parametrize("name", sorted(TRAIN_CONFIGS))
+def test_cpu_trainer_steps(golden, name):
+    """The module-based CPU trainer (bench.py's cpu_baseline) takes the reference's steps too."""
+    c = TRAIN_CONFIGS[name]
+    X = synth_csr(c["n_users"], c["n_items"], lam=c.get("lam", 3.0), seed=200 + c["seed"])
+    E = synth_embeddings(c["n_items"], c["d"], seed=300 + c["seed"])
+    p = R.init_params(c["n_items"], E, c["latent"], c["hidden"], seed=c["seed"])
+    x = torch.as_tensor(X.toarray(), dtype=torch.float32)
+    tr = R.CpuTrainer(p, c.get("dropout", 0.3), lr=c["lr"], weight_decay=c.get("wd", 0.0))
+    has_proj = c["latent"] != c["d"]
+    for step in (1, 2):
+        g = lambda k: torch.as_tensor(golden[f"g2{name}_s{step}_{k}"])
+        enc = [g(f"encmask{k}") for k in range(len(c["hidden"]))]
+        loss = tr.step(x, c["beta"], enc_masks=enc, proj_mask=g("projmask") if has_proj else None, eps=g("eps"))
+        _close(loss, golden[f"g2{name}_loss"][step - 1][0], 1e-5, 1e-6, f"loss step {step}")
+    st = tr.state()
+    for n in R.param_names(p):
+        _close_max(st[n], golden[f"g2{name}_s2_param_{n}"], 2e-4, f"param {n}")
+
+
 def test_metric_kats(golden):
     for trial, k, rec, ndcg, hr in golden["g3_kat"]:
         recd, rel = golden[f"g3_rec_{int(trial)}"], golden[f"g3_rel_{int(trial)}"]
