@@ -2572,6 +2572,7 @@ struct DecPlan {
   int v2;    // bf16 version-2 sweep (k_dec2_bf16)
   int v3;    // bf16 version-3 sweep (k_dec3_bf16, D = 768)
   int v4;    // bf16 version-4 sweep (k_dec4_bf16: D = 768 with 4 waves, D = 384 with 8)
+  int v5;    // bf16 version-5 sweep (k_dec5_bf16, D = 768: 8 waves, GEMM1 and GEMM2 on different waves)
   int ds;    // its D split (1 or 2)
   int nw;    // its waves per block (4, or 8 with ds = 2)
   int64_t upb;
@@ -2607,6 +2608,12 @@ static bool v3_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V3", 
 static bool v4_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V4", 1) != 0; }
 // HVAE_DEC_V4_384=1 runs version 4 with 8 waves at D = 384 (large batches) instead of version 2's DS = 1 sweep
 static bool v4_384(int64_t D, int64_t nb) { return D == 384 && nb > 64 && env_int("HVAE_DEC_V4_384", 0) != 0; }
+// HVAE_DEC_V5=1 runs version 5 (hvae_decoder5.hip: producer / consumer waves, two per SIMD) at D = 768
+// (A/B; read at every plan)
+static bool v5_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V5", 0) != 0; }
+int dec5_launch(bool with_o, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                int splits, int64_t tiles_per_split, int64_t blocks, int* flag, float* m, float* l, float* O,
+                float* lse, int direct, hipStream_t st);
 
 static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
   s = std::max<int64_t>(1, std::min<int64_t>(s, std::min<int64_t>(tiles, kMaxSplits)));
@@ -2634,6 +2641,7 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   p.v2 = bf && !dec_use_v1() && v2_supported(D);
   p.v3 = p.v2 && v3_supported(D);
   p.v4 = (p.v3 && v4_supported(D)) || (p.v2 && v4_384(D, nb));
+  p.v5 = p.v4 && v5_supported(D);  // same users per block (64), splits and partial layout as version 4
   p.ds = p.v2 && (D > 384 || nb <= 64) ? 2 : 1;
   if (p.v2 && D <= 384 && (dec_forced_ds() == 1 || dec_forced_ds() == 2)) p.ds = dec_forced_ds();
   p.nw = p.v2 && p.ds == 2 && nb > 64 && D <= 384 ? 8 : 4;
@@ -2786,6 +2794,9 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
       case 768: return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       default: break;
     }
+  } else if (dtype == HVAE_BF16 && p.v5 && D == 768) {
+    return dec5_launch(WO, U, ldu, E, enorm, nb, N, p.splits, p.tiles_per_split, p.blocks, o.flag, o.m, o.l, o.O,
+                       o.lse, o.direct, st);
   } else if (dtype == HVAE_BF16 && p.v4 && D == 768) {
     return launch_bf16_v4<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
   } else if (dtype == HVAE_BF16 && p.v4 && D == 384) {

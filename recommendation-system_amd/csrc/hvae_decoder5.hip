@@ -1,0 +1,396 @@
+// hvae_decoder5.hip -- version 5 of the bf16 decoder sweep at d = 768: version 4's work, with the two
+// GEMMs on different waves (producer / consumer specialisation, two waves per SIMD).
+//
+// Version 4 (hvae_decoder.hip, k_dec4_bf16) runs one wave per SIMD that does everything for its
+// (user group ug, D half dh): the LDS-DMA of the next tiles, GEMM1 S^T = E_tile U^T for its 16 items
+// over all of D, the exponentials, and GEMM2 O^T += E_tile^T P^T for its D half. At one wave per
+// SIMD nothing covers the issue cost of the 12 LDS-DMA pieces per tile, nor any LDS-read latency an
+// MFMA waits on (profiles/r02_dec4_ablations.jsonl: the sweep is 18 % faster without the DMA).
+//
+// Here a block is 8 waves, two per SIMD (waves q and q + 4 share one: the workgroup's waves go to the
+// SIMDs in a cyclic order of 4). For q = 0..3, (ug, dh) = (q & 1, q >> 1):
+//   * producer wave q (role 0): U of user group ug over all of D (192 VGPRs); per tile: the LDS-DMA
+//     pieces of tile t + 2, GEMM1 of tile t + 1 for items 16 dh .. 16 dh + 15 (48 16x16x32 MFMAs),
+//     its 8 exponentials, its P half -> LDS;
+//   * consumer wave q + 4 (role 1): O of user group ug over D half dh (192 VGPRs: the file is compiled
+//     with -mllvm -amdgpu-mfma-vgpr-form, so that no AGPR block is allocated beside the producer's
+//     VGPRs and each wave fits the 256 registers of two waves per SIMD); per tile: GEMM2 of tile t
+//     over both item halves (24 32x32x16 MFMAs) with P(t) read back from LDS.
+// The SIMD's two instruction streams interleave in hardware, so one wave's DMA issue, LDS waits and
+// exponentials run under the other's MFMAs. The MFMA work per SIMD and tile is version 4's (1536
+// cycles), as are the LDS image, the DMA piece map, the P layout, the fixed-offset / flag rules and
+// the summation orders, so the outputs equal version 4's bitwise. One barrier per tile:
+//   [barrier: tile t + 1 landed, P(t) published, GEMM2(t - 1) done]
+//   producers: DMA of t + 2 into the slot GEMM2(t - 1) freed | GEMM1(t + 1) | softmax | P(t + 1) out
+//   consumers: GEMM2(t) from slot t % 3 and P(t)
+#include <algorithm>
+#include <array>
+
+#include "hvae_common.h"
+
+namespace hvae {
+namespace dec5 {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kTI = 32;                  // items per tile
+constexpr float kOffsetSpan = 60.0f;     // = hvae_decoder.hip
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kMinL = 8.75651e-27f;
+
+struct Out {
+  int* flag;
+  float* m;
+  float* l;
+  float* O;
+  float* lse;
+  int direct;
+};
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  const bf16x2 v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
+template <int n>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(n >= 0 && n < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14));
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+#ifndef DEC5_G1_AHEAD
+#define DEC5_G1_AHEAD 2  // GEMM1 A operand k-steps in flight
+#endif
+#ifndef DEC5_DMA_B
+#define DEC5_DMA_B 0  // of each (ug, dh)'s 12 LDS-DMA pieces per tile, how many the consumer wave issues
+#endif
+
+constexpr int D = 768;
+constexpr int NS = 3;                    // tile slots
+constexpr int TB = (D / 128) * 8192;     // tile bytes (48 KiB)
+constexpr int PST = 80;                  // P row stride (bytes)
+constexpr int LDS_BYTES = NS * TB + 2 * 2 * 32 * PST + 4 * 64 * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "k_dec5_bf16 LDS");
+
+template <bool WITH_O>
+__global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, int64_t ldu,
+                                                   const bf16_t* __restrict__ E, const float* __restrict__ e_maxnorm,
+                                                   int64_t nb, int64_t N, int splits, int64_t tiles_per_split,
+                                                   Out out) {
+  constexpr int DW = D / 2;      // GEMM2: dims owned by one consumer wave
+  constexpr int DB = DW / 32;    // GEMM2 d-blocks (12)
+  constexpr int KS = D / 32;     // GEMM1 k-steps (24)
+  constexpr int PW = 12;         // 1-KiB LDS-DMA pieces per (ug, dh) per tile
+  constexpr int PB = DEC5_DMA_B;
+  constexpr int PA = PW - PB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned char* pbuf = lds + NS * TB;                                  // [2 parity][2 ug][32 users][PST]
+  float* xm = reinterpret_cast<float*>(lds + NS * TB + 2 * 2 * 32 * PST);  // [2 ug][l 32 | m 32]
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int role = w >> 2, q = w & 3;
+  const int ug = q & 1, dh = q >> 1;
+  const int split = blockIdx.x % splits;
+  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 64 + ug * 32;
+  const int64_t ntiles = (N + kTI - 1) / kTI;
+  const int64_t t_beg = (int64_t)split * tiles_per_split;
+  const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
+  const int dbase = dh * DW;
+
+  // LDS-DMA into version 2's image (version 3's pieces): piece p = q * 12 + i
+  int vlane[2];
+#pragma unroll
+  for (int pb = 0; pb < 2; ++pb) {
+    const int row = 8 * pb + ((lane >> 2) & 7);
+    vlane[pb] = ((lane >> 2) & 7) * (D * 2) + 64 * (lane >> 5) + 16 * ((lane & 3) ^ ((row >> 2) & 3));
+  }
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(E), (short)0, (int)(N * D * 2), 0x00020000);
+  const uint32_t ring0 = lds_addr(lds) + (uint32_t)(q * PW * 1024);
+  auto issue_piece = [&](uint32_t soff, int slot_i, int i, bool fresh) {
+    const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
+    const int p = q * PW + i;
+    const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
+    const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
+    if (fresh)
+      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+    else
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+  };
+  auto tile_soff = [&](int64_t t) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(kTI * D * 2)));
+  };
+  auto barrier = [&] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto p_row = [&](int par, int uu) { return pbuf + ((par * 2 + ug) * 32 + uu) * PST; };
+
+  if (role == 0) {
+    // ------------------------------------------------------------------ producer ---
+    // producer q owns users u0 + 16 uh + c16 (uh = q >> 1) over both item halves of every tile: U of
+    // its 16 users over all of D in 96 VGPRs (version 4 held 32 users' U in 192 and split the items)
+    const int uh = dh;
+    const int64_t ub = u0 + 16 * uh + c16;
+    const float emax = *e_maxnorm;
+    bf16x8 uf[KS];  // GEMM1's B operand: lane holds U[ub][32 ks + 8 g .. + 7]
+    float usq = 0.f;
+    {
+      const int64_t ur = ub < nb ? ub : nb - 1;  // branch-free: rows past nb load row nb - 1, zeroed
+      const float keep = ub < nb ? 1.f : 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        float4 a = *reinterpret_cast<const float4*>(U + ur * ldu + 32 * ks + 8 * g);
+        float4 b = *reinterpret_cast<const float4*>(U + ur * ldu + 32 * ks + 8 * g + 4);
+        a.x *= keep; a.y *= keep; a.z *= keep; a.w *= keep;
+        b.x *= keep; b.y *= keep; b.z *= keep; b.w *= keep;
+        usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+        uf[ks] = bf16x8{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                        (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+      }
+    }
+    float bound;
+    {
+      float v = usq;
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      bound = sqrtf(v) * emax * 1.02f;
+    }
+    // GEMM1: S^T[32 items][16 users] over all of D, item halves ih: A = image rows 16 ih + c16, chunk 4 ks + g
+    int laneA[2];
+#pragma unroll
+    for (int ih = 0; ih < 2; ++ih) {
+      const int r1 = 16 * ih + c16;
+      laneA[ih] = ((r1 >> 3) << 11) + ((r1 & 7) << 6) + ((g ^ ((r1 >> 2) & 3)) << 4);
+    }
+    auto gemm1 = [&](const unsigned char* buf, f32x4 (&s)[2], auto&& fill) {
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[ih][r] = 0.f;
+      auto rdA = [&](int ih, int ks) {
+        return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(buf + laneA[ih] + ((ks >> 2) << 13) +
+                                                                         ((ks & 3) << 9)));
+      };
+      constexpr int AH = DEC5_G1_AHEAD;
+      bf16x8 a[AH][2];
+#pragma unroll
+      for (int j = 0; j < AH; ++j) { a[j][0] = rdA(0, j); a[j][1] = rdA(1, j); }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 c0 = a[ks % AH][0], c1 = a[ks % AH][1];
+        if (ks + AH < KS) { a[ks % AH][0] = rdA(0, ks + AH); a[ks % AH][1] = rdA(1, ks + AH); }
+        s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c0, uf[ks], s[0], 0, 0, 0);
+        s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c1, uf[ks], s[1], 0, 0, 0);
+        fill(ks);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    float m = 0.f, mL = 0.f, lsum = 0.f;
+    f32x4 s_nx[2];
+    auto mask_tail = [&](f32x4 (&s)[2], int64_t t) {
+      if (t == ntiles - 1 && (N % kTI) != 0) {
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih) {
+          const int lim = (int)(N - t * kTI) - 16 * ih - 4 * g;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[ih][r] = r >= lim ? -INFINITY : s[ih][r];
+        }
+      }
+    };
+    auto p_out = [&](int par) {  // the 8 exponentials of s_nx, their sum, the packed P row pieces -> LDS
+      unsigned char* prow = p_row(par, 16 * uh + c16);
+#pragma unroll
+      for (int ih = 0; ih < 2; ++ih) {
+        float pv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pv[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_nx[ih][r], kLog2e, -mL));
+          lsum += pv[r];
+        }
+        *reinterpret_cast<uint2*>(prow + 2 * (16 * ih + 8 * (g & 1) + 4 * (g >> 1))) =
+            make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
+      }
+    };
+    if (t_beg < t_end) {
+      for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg), 0, i, i == 0);
+      if (t_beg + 1 < t_end)
+        for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg + 1), 1, i, false);
+      wait_vmcnt<0>();
+    }
+    barrier();  // [P0] tiles t_beg (and t_beg + 1) landed (consumers' pieces too)
+    if (t_beg < t_end) {
+      // first tile: its max sets the user's fixed offset m (version 2's rule)
+      gemm1(lds, s_nx, [](int) {});
+      mask_tail(s_nx, t_beg);
+      float mx = fmaxf(fmaxf(fmaxf(s_nx[0][0], s_nx[0][1]), fmaxf(s_nx[0][2], s_nx[0][3])),
+                       fmaxf(fmaxf(s_nx[1][0], s_nx[1][1]), fmaxf(s_nx[1][2], s_nx[1][3])));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      m = fmaxf(mx, bound - kOffsetSpan);
+      mL = m * kLog2e;
+      p_out(0);  // P(t_beg) -> parity 0
+    }
+    barrier();  // [P1]
+    for (int64_t t = t_beg; t < t_end; ++t) {
+      const int li = (int)(t - t_beg);
+      const int nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
+      wait_vmcnt<0>();
+      barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
+      if (t + 1 < t_end) {
+        const bool dma = t + 2 < t_end;
+        const uint32_t soff_dma = tile_soff(dma ? t + 2 : t);
+        gemm1(lds + nxt * TB, s_nx, [&](int ks) {
+          if (dma && (ks & 1) == 1 && ks / 2 < PA) issue_piece(soff_dma, s_dma, ks / 2, ks == 1);
+        });
+        mask_tail(s_nx, t + 1);
+        p_out(par ^ 1);
+      }
+    }
+    wait_vmcnt<0>();
+    lsum += __shfl_xor(lsum, 16, 64);  // over the 4 lanes g of the user
+    lsum += __shfl_xor(lsum, 32, 64);
+    barrier();  // [E0]
+    if (g == 0) {
+      xm[ug * 64 + 16 * uh + c16] = lsum;
+      xm[ug * 64 + 32 + 16 * uh + c16] = m;
+    }
+    barrier();  // [E1]
+    return;
+  }
+
+  // -------------------------------------------------------------------- consumer ---
+  // GEMM2 (version 3's reads): O^T[DW][32 users] += E^T P^T over k-steps 0 (items 0..15) and 1 (16..31)
+  const int64_t user = u0 + col;
+  const bool wave_active = u0 < nb;
+  const int g1 = (lane >> 4) & 1, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int cseg = (dbase / 128) << 13;
+  auto dboff = [](int db) { return ((db >> 2) << 13) + ((db & 3) << 9); };
+  const int laneT0 = ((4 * h + qq) << 6) + (((2 * g1 + (pp >> 1)) ^ ((0 + h) & 3)) << 4) + 8 * (pp & 1);
+  const int laneT1 = ((4 * h + qq) << 6) + (((2 * g1 + (pp >> 1)) ^ ((2 + h) & 3)) << 4) + 8 * (pp & 1);
+  f32x16 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  constexpr int BH = 2;
+  auto rdT = [&](const unsigned char* buf, int i) {
+    const int kh = i / DB, db = i % DB;
+    const unsigned char* tt = buf + cseg + (kh << 12);
+    auto* p0 = (__attribute__((address_space(3))) s16x4*)(void*)(tt + laneT0 + dboff(db));
+    auto* p1 = (__attribute__((address_space(3))) s16x4*)(void*)(tt + laneT1 + (1 << 11) + dboff(db));
+    return std::array<s16x4, 2>{__builtin_amdgcn_ds_read_tr16_b64_v4i16(p0), __builtin_amdgcn_ds_read_tr16_b64_v4i16(p1)};
+  };
+  auto gemm2 = [&](const unsigned char* buf, const uint4& pf0, const uint4& pf1, auto&& fill) {
+    if constexpr (WITH_O) {
+      std::array<s16x4, 2> n[BH];
+#pragma unroll
+      for (int j = 0; j < BH; ++j) n[j] = rdT(buf, j);
+#pragma unroll
+      for (int i = 0; i < 2 * DB; ++i) {
+        const std::array<s16x4, 2> c = n[i % BH];
+        if (i + BH < 2 * DB) n[i % BH] = rdT(buf, i + BH);
+        const s16x8 a = {c[0][0], c[0][1], c[0][2], c[0][3], c[1][0], c[1][1], c[1][2], c[1][3]};
+        o[i % DB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                           __builtin_bit_cast(bf16x8, i < DB ? pf0 : pf1), o[i % DB],
+                                                           0, 0, 0);
+        fill(i);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2 * DB; ++i) fill(i);
+    }
+  };
+  if constexpr (PB > 0) {
+    if (t_beg < t_end) {
+      for (int i = PA; i < PW; ++i) issue_piece(tile_soff(t_beg), 0, i, i == PA);
+      if (t_beg + 1 < t_end)
+        for (int i = PA; i < PW; ++i) issue_piece(tile_soff(t_beg + 1), 1, i, false);
+      wait_vmcnt<0>();
+    }
+  }
+  barrier();  // [P0]
+  barrier();  // [P1]
+  for (int64_t t = t_beg; t < t_end; ++t) {
+    const int li = (int)(t - t_beg);
+    const int cur = li % NS, s_dma = (li + 2) % NS, par = li & 1;
+    if constexpr (PB > 0) wait_vmcnt<0>();
+    barrier();  // [L]
+    // P(t) in GEMM2's B layout: user col, positions 8 h .. 8 h + 7 of k-steps 0 and 1
+    const uint4 pf0 = *reinterpret_cast<const uint4*>(p_row(par, col) + 16 * h);
+    const uint4 pf1 = *reinterpret_cast<const uint4*>(p_row(par, col) + 32 + 16 * h);
+    const bool dma = t + 2 < t_end;
+    const uint32_t soff_dma = tile_soff(dma ? t + 2 : t);
+    gemm2(lds + cur * TB, pf0, pf1, [&](int i) {
+      if constexpr (PB > 0)
+        if (dma && (i & 1) == 0 && i / 2 < PB) issue_piece(soff_dma, s_dma, PA + i / 2, i == 0);
+    });
+  }
+  if constexpr (PB > 0) wait_vmcnt<0>();
+  barrier();  // [E0]
+  barrier();  // [E1] producers' (l, m) published
+  if (!wave_active || t_beg >= t_end || user >= nb) return;
+  const float ltot = xm[ug * 64 + col], mu = xm[ug * 64 + 32 + col];
+  if (h == 0 && dh == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
+  const int64_t row = out.direct ? user : (int64_t)split * nb + user;
+  if (h == 0 && dh == 0) {
+    if (out.direct) out.lse[user] = mu + logf(ltot);
+    else { out.m[row] = mu; out.l[row] = ltot; }
+  }
+  if (WITH_O) {
+    const float sc = out.direct ? 1.0f / ltot : 1.0f;
+#pragma unroll
+    for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
+        *reinterpret_cast<float4*>(out.O + row * D + dd) =
+            make_float4(o[d][4 * g4] * sc, o[d][4 * g4 + 1] * sc, o[d][4 * g4 + 2] * sc, o[d][4 * g4 + 3] * sc);
+      }
+  }
+}
+
+}  // namespace dec5
+
+// Launch of the version-5 sweep (d = 768, 64 users per block, blocks = user blocks x splits, block b's
+// split = b % splits): called by hvae_decoder.hip's dispatch with its plan and outputs.
+int dec5_launch(bool with_o, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                int splits, int64_t tiles_per_split, int64_t blocks, int* flag, float* m, float* l, float* O,
+                float* lse, int direct, hipStream_t st) {
+  using namespace dec5;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec5_bf16<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 LDS_BYTES));
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec5_bf16<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 LDS_BYTES));
+    attr_set = true;
+  }
+  Out o{flag, m, l, O, lse, direct};
+  if (with_o)
+    k_dec5_bf16<true><<<(unsigned)blocks, 512, LDS_BYTES, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N, splits,
+                                                                tiles_per_split, o);
+  else
+    k_dec5_bf16<false><<<(unsigned)blocks, 512, LDS_BYTES, st>>>(U, ldu, (const bf16_t*)E, enorm, nb, N, splits,
+                                                                 tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec5_bf16");
+  return HVAE_OK;
+}
+
+}  // namespace hvae

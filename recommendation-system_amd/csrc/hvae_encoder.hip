@@ -365,7 +365,11 @@ __global__ void __launch_bounds__(256) k_rg_count(const int64_t* __restrict__ ro
                                                   const int32_t* __restrict__ col_idx,
                                                   const int32_t* __restrict__ rows,
     const int64_t* __restrict__ rows_offset, int64_t nb,
-                                                  int32_t* __restrict__ cnt) {
+                                                  int32_t* __restrict__ cnt, unsigned long long* __restrict__ lb_state,
+                                                  int64_t lb_words) {
+  // the next launch's look-back state (k_rg_scan_lb): status words and its block-id counter start at zero
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lb_words; i += (int64_t)gridDim.x * blockDim.x)
+    lb_state[i] = 0ull;
   const int lane = threadIdx.x & 63;
   const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= nb) return;
@@ -373,71 +377,31 @@ __global__ void __launch_bounds__(256) k_rg_count(const int64_t* __restrict__ ro
   for (int64_t e = row_ptr[r] + lane; e < row_ptr[r + 1]; e += 64) atomicAdd(&cnt[col_idx[e]], 1);
 }
 
-// per 4096-item block: (#items with cnt > 0, sum of cnt)
-__global__ void __launch_bounds__(256) k_rg_scan1(const int32_t* __restrict__ cnt, int64_t N,
-                                                  int64_t* __restrict__ blocktot /* [nblk][2] */) {
-  __shared__ float red[4];
-  int nf = 0, nc = 0;
-  const int64_t base = (int64_t)blockIdx.x * kScanItemsPerBlock + threadIdx.x * 16;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int64_t j = base + i;
-    const int c = (j < N) ? cnt[j] : 0;
-    nf += c > 0;
-    nc += c;
-  }
-  // counts are small integers: exact in fp32 up to 2^24 per block
-  const float tf = block_sum<256>((float)nf, red);
-  const float tc = block_sum<256>((float)nc, red);
-  if (threadIdx.x == 0) {
-    blocktot[2 * blockIdx.x + 0] = (int64_t)tf;
-    blocktot[2 * blockIdx.x + 1] = (int64_t)tc;
-  }
+// One-pass scan of the per-item counts (decoupled look-back): slots in ascending item order for the
+// items with cnt > 0, their segment offsets, n_unique and seg_off[n_unique]. A block takes the next
+// 4096 items in the order blocks start (block id from an atomic counter, so every block it waits for
+// has already started), publishes its aggregate (#items, #entries), then sums its predecessors'
+// words back to the first inclusive prefix and publishes its own. A status word is
+// [2-bit status | 31-bit items | 31-bit entries] (status 1 aggregate, 2 inclusive prefix), read and
+// written with agent-scope atomics, so no separate data needs fencing. Replaces three launches
+// (block totals, their scan, the block scans).
+__device__ __forceinline__ unsigned long long lb_word(unsigned st, long long f, long long c) {
+  return ((unsigned long long)st << 62) | ((unsigned long long)f << 31) | (unsigned long long)c;
 }
 
-// single block: exclusive scan of the block totals; n_unique, seg_off[n_unique]
-__global__ void __launch_bounds__(1024) k_rg_scan2(int64_t* __restrict__ blocktot, int64_t nblk,
-                                                   int32_t* __restrict__ n_unique,
-                                                   int32_t* __restrict__ seg_off, int64_t cap) {
-  __shared__ int64_t sf[1024], sc[1024];
-  __shared__ int64_t cf, cc;
-  if (threadIdx.x == 0) { cf = 0; cc = 0; }
-  __syncthreads();
-  for (int64_t base = 0; base < nblk; base += 1024) {
-    const int64_t i = base + threadIdx.x;
-    const int64_t vf = (i < nblk) ? blocktot[2 * i] : 0, vc = (i < nblk) ? blocktot[2 * i + 1] : 0;
-    sf[threadIdx.x] = vf;
-    sc[threadIdx.x] = vc;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-      const int64_t tf = (threadIdx.x >= o) ? sf[threadIdx.x - o] : 0;
-      const int64_t tc = (threadIdx.x >= o) ? sc[threadIdx.x - o] : 0;
-      __syncthreads();
-      sf[threadIdx.x] += tf;
-      sc[threadIdx.x] += tc;
-      __syncthreads();
-    }
-    if (i < nblk) {
-      blocktot[2 * i] = cf + sf[threadIdx.x] - vf;
-      blocktot[2 * i + 1] = cc + sc[threadIdx.x] - vc;
-    }
-    __syncthreads();
-    if (threadIdx.x == 1023) { cf += sf[1023]; cc += sc[1023]; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    *n_unique = (int32_t)cf;
-    if (cf <= cap) seg_off[cf] = (int32_t)cc;
-  }
-}
-
-__global__ void __launch_bounds__(256) k_rg_scan3(int32_t* __restrict__ cnt, int64_t N,
-                                                  const int64_t* __restrict__ blockoff,
-                                                  int32_t* __restrict__ slot_of,
-                                                  int32_t* __restrict__ item_of,
-                                                  int32_t* __restrict__ seg_off, int64_t cap) {
+__global__ void __launch_bounds__(256) k_rg_scan_lb(int32_t* __restrict__ cnt, int64_t N,
+                                                    unsigned long long* __restrict__ state, int64_t nblk,
+                                                    int32_t* __restrict__ slot_of, int32_t* __restrict__ item_of,
+                                                    int32_t* __restrict__ seg_off, int64_t cap,
+                                                    int32_t* __restrict__ n_unique) {
   __shared__ int sf[256], sc[256];
-  const int64_t base = (int64_t)blockIdx.x * kScanItemsPerBlock + threadIdx.x * 16;
+  __shared__ int s_bid;
+  __shared__ long long s_pf, s_pc;
+  unsigned* ctr = reinterpret_cast<unsigned*>(state + nblk);
+  if (threadIdx.x == 0) s_bid = (int)__hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int bid = s_bid;
+  const int64_t base = (int64_t)bid * kScanItemsPerBlock + threadIdx.x * 16;
   int c[16];
   int nf = 0, nc = 0;
 #pragma unroll
@@ -458,8 +422,34 @@ __global__ void __launch_bounds__(256) k_rg_scan3(int32_t* __restrict__ cnt, int
     sc[threadIdx.x] += tc;
     __syncthreads();
   }
-  int64_t slot = blockoff[2 * blockIdx.x] + sf[threadIdx.x] - nf;
-  int64_t off = blockoff[2 * blockIdx.x + 1] + sc[threadIdx.x] - nc;
+  if (threadIdx.x == 0) {
+    const long long tf = sf[255], tc = sc[255];
+    long long pf = 0, pc = 0;
+    if (bid == 0) {
+      __hip_atomic_store(&state[0], lb_word(2u, tf, tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&state[bid], lb_word(1u, tf, tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int j = bid - 1; j >= 0; --j) {
+        unsigned long long v;
+        do {
+          v = __hip_atomic_load(&state[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } while ((v >> 62) == 0ull);
+        pf += (long long)((v >> 31) & 0x7fffffffull);
+        pc += (long long)(v & 0x7fffffffull);
+        if ((v >> 62) == 2ull) break;
+      }
+      __hip_atomic_store(&state[bid], lb_word(2u, pf + tf, pc + tc), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_pf = pf;
+    s_pc = pc;
+    if (bid == nblk - 1) {
+      *n_unique = (int32_t)(pf + tf);
+      if (pf + tf <= cap) seg_off[pf + tf] = (int32_t)(pc + tc);
+    }
+  }
+  __syncthreads();
+  int64_t slot = s_pf + sf[threadIdx.x] - nf;
+  int64_t off = s_pc + sc[threadIdx.x] - nc;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     if (c[i] > 0) {
@@ -1143,7 +1133,7 @@ extern "C" int hvae_dense_to_csr(const float* x, int64_t B, int64_t N, int64_t* 
 }
 
 extern "C" size_t hvae_w1_rowgrad_workspace(int64_t n_items) {
-  return (size_t)2 * cdiv(n_items, kScanItemsPerBlock) * sizeof(int64_t);
+  return (size_t)(cdiv(n_items, kScanItemsPerBlock) + 1) * sizeof(int64_t);  // look-back words + block counter
 }
 
 static int rg_check(const hvae_rowgrad* rg) {
@@ -1181,21 +1171,20 @@ extern "C" int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad*
     return HVAE_OK;
   }
   const unsigned rgrid = (unsigned)cdiv(x->nb, 4);
-  k_rg_count<<<rgrid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->rows, x->rows_offset, x->nb, rg->cnt);
+  const bool small_scan = N <= kSmallScanItems;
+  const int64_t nblk = cdiv(N, kScanItemsPerBlock);
+  HVAE_REQUIRE(N < (1ll << 31) && rg->cap < (1ll << 31), "hvae_w1_rowgrad_plan: N or cap >= 2^31");
+  unsigned long long* lb = (unsigned long long*)ws;
+  k_rg_count<<<rgrid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->rows, x->rows_offset, x->nb, rg->cnt, lb,
+                                    small_scan ? 0 : nblk + 1);
   HVAE_LAUNCH_CHECK("k_rg_count");
-  if (N <= kSmallScanItems) {
+  if (small_scan) {
     k_rg_scan_small<<<1, 1024, 0, st>>>(rg->cnt, N, rg->slot_of, rg->item_of, rg->seg_off, rg->cap, rg->n_unique);
     HVAE_LAUNCH_CHECK("k_rg_scan_small");
   } else {
-    const int64_t nblk = cdiv(N, kScanItemsPerBlock);
-    int64_t* blocktot = (int64_t*)ws;
-    k_rg_scan1<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, blocktot);
-    HVAE_LAUNCH_CHECK("k_rg_scan1");
-    k_rg_scan2<<<1, 1024, 0, st>>>(blocktot, nblk, rg->n_unique, rg->seg_off, rg->cap);
-    HVAE_LAUNCH_CHECK("k_rg_scan2");
-    k_rg_scan3<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, blocktot, rg->slot_of, rg->item_of, rg->seg_off,
-                                               rg->cap);
-    HVAE_LAUNCH_CHECK("k_rg_scan3");
+    k_rg_scan_lb<<<(unsigned)nblk, 256, 0, st>>>(rg->cnt, N, lb, nblk, rg->slot_of, rg->item_of, rg->seg_off,
+                                                rg->cap, rg->n_unique);
+    HVAE_LAUNCH_CHECK("k_rg_scan_lb");
   }
   k_rg_scatter<<<rgrid, 256, 0, st>>>(x->row_ptr, x->col_idx, x->vals, x->rows, x->rows_offset, x->nb, rg->slot_of,
                                       rg->seg_off, rg->fill, rg->contrib_row, rg->contrib_val,

@@ -11,6 +11,7 @@
 // (device-scope ticket) sums the partials in split order 0..S-1 and applies
 // the epilogue -- deterministic, and no second launch.
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "hvae_common.h"
@@ -117,6 +118,89 @@ struct GemmP {
 
 template <int BM>
 constexpr int gemm_smem_floats() { return 2 * GTile<BM>::IMG; }
+
+// Epilogue of one block tile (acc in the 16x16 MFMA layout, wave (w >> 1, w & 1) of a 2x2 grid): alpha,
+// beta, the fused epilogue; with split-K (g.slab) the partial tile goes to the slab and the last block to
+// arrive at the tile sums the partials in split order and applies the epilogue.
+template <int BM, int BN>
+__device__ __forceinline__ void gemm_finish(const GemmP& g, const f32x4 (&acc)[BM / 32][BN / 32], unsigned bx,
+                                            unsigned by, unsigned bz, bool do_rowsum, float rowsum) {
+  constexpr int IM = BM / 32, JN = BN / 32;
+  const int64_t M = g.M, N = g.N, ldc = g.ldc;
+  const float alpha = g.alpha, beta = g.beta;
+  float* __restrict__ C = g.C;
+  float* __restrict__ slab = g.slab;
+  unsigned* __restrict__ tickets = g.tickets;
+  const EpiArgs& ep = g.ep;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t m0 = (int64_t)by * BM, n0 = (int64_t)bx * BN;
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  if (do_rowsum && t < BM && m0 + t < M) {
+    if (slab) st_shared_f(&slab[(int64_t)g.gz * M * N + (int64_t)bz * M + m0 + t], rowsum);
+    else ep.opa_rowsum[m0 + t] = alpha * rowsum;
+  }
+  const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP && ep.kind <= HVAE_EPI_DROP_BWD) ? load_step(ep.step_dev) : 0;
+  if (!slab) {
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
+          const int64_t col = n0 + wn + j * 16 + (lane & 15);
+          if (row >= M || col >= N) continue;
+          float c = alpha * acc[i][j][r];
+          if (beta != 0.f) c += beta * C[row * ldc + col];
+          C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c, C);
+        }
+    return;
+  }
+  // ---- split-K: publish the partial tile, the last arrival reduces
+#pragma unroll
+  for (int i = 0; i < IM; ++i)
+#pragma unroll
+    for (int j = 0; j < JN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
+        const int64_t col = n0 + wn + j * 16 + (lane & 15);
+        if (row < M && col < N) st_shared_f(&slab[((int64_t)bz * M + row) * N + col], acc[i][j][r]);
+      }
+  const unsigned tile = by * g.gx + bx;
+  if (!last_block_arrives(&tickets[tile], g.gz)) return;
+  // the tile's elements per thread: one coherent load each per split, all in flight together
+  constexpr int Q = BM * BN / 256;
+  const int S = (int)g.gz;
+  float sum[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) sum[q] = 0.f;
+  for (int z = 0; z < S; ++z) {
+    float v[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int e = t + 256 * q;
+      const int64_t row = m0 + e / BN, col = n0 + e % BN;
+      v[q] = (row < M && col < N) ? ld_shared_f(&slab[((int64_t)z * M + row) * N + col]) : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < Q; ++q) sum[q] += v[q];
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int e = t + 256 * q;
+    const int64_t row = m0 + e / BN, col = n0 + e % BN;
+    if (row >= M || col >= N) continue;
+    float c = alpha * sum[q];
+    if (beta != 0.f) c += beta * C[row * ldc + col];
+    C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c, C);
+  }
+  if (ep.opa_rowsum && bx == 0 && t < BM && m0 + t < M) {
+    float r = 0.f;
+    for (int z = 0; z < S; ++z) r += ld_shared_f(&slab[(int64_t)S * M * N + (int64_t)z * M + m0 + t]);
+    ep.opa_rowsum[m0 + t] = alpha * r;
+  }
+}
 
 // The block (bx, by, bz) of problem g: tile rows by*BM.., columns bx*BN.., k split bz.
 template <bool TA, bool TB, int BM, int BN>
@@ -265,70 +349,186 @@ __device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned
     }
   }
 
-  if (do_rowsum && t < BM && m0 + t < M) {
-    if (slab) st_shared_f(&slab[(int64_t)g.gz * M * N + (int64_t)bz * M + m0 + t], rowsum);
-    else ep.opa_rowsum[m0 + t] = alpha * rowsum;
+  gemm_finish<BM, BN>(g, acc, bx, by, bz, do_rowsum, rowsum);
+}
+
+// ------------------------------------------------------------ fast path ---
+// Tiles that divide the problem (M % BM == N % BN == 0, every k range a multiple of 32, 16-B aligned
+// operands with ld % 4 == 0 -- the batch GEMMs of the train step at B = 4096 or 64): no bounds checks,
+// one barrier per 32-deep k stage, the next stage's global loads in flight under the current stage's
+// MFMAs, and 128-bit fragment reads. Both operands are staged into the same LDS image whatever their
+// memory order: [8 k-chunks][R rows (+4 pad)][4 k], so a lane (row r, k-group q) reads four consecutive
+// k of its row with one ds_read_b128 (16 lanes read 256 contiguous bytes: conflict-free). k-contiguous
+// sources ([r][k]) are copied 16 B at a time; r-contiguous ones ([k][r]) are transposed in the store
+// (4 ds_write_b32 per float4).
+// MFMA order: the 16x16x4 MFMA (s) of 16-k group j sums k = 16 j + 4 q + s over the lane groups q,
+// so the four k of a lane's float4 feed four consecutive MFMAs. Each k still enters the accumulator
+// exactly once, in a fixed order (deterministic, exact fp32 products and fp32 accumulation).
+constexpr int FBK = 32;
+#ifndef FAST_PREFETCH
+#define FAST_PREFETCH 4  // k stages of global loads in flight per thread
+#endif
+template <int R>
+struct FImg {
+  static constexpr int CS = R + 4;             // float4 slots per k-chunk (pad: the 8 chunks' stores spread)
+  static constexpr int F4 = (FBK / 4) * CS;    // float4 slots per image
+  static constexpr int LD = R * FBK / 4 / 256; // float4 global loads per thread per stage
+  static_assert(R * FBK / 4 % 256 == 0, "tile rows x 32 must be a multiple of 1024 floats");
+};
+
+// one operand of one stage: rows r0.., k0.. of a k-contiguous (KC) or row-contiguous source
+template <bool KC, int R>
+__device__ __forceinline__ void fast_gload(const float* __restrict__ X, int64_t ld, int64_t r0, int64_t k0,
+                                           float4 (&v)[FImg<R>::LD]) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < FImg<R>::LD; ++i) {
+    const int f = t + 256 * i;
+    if (KC) {  // [r][k]: 8 threads per row, 128 contiguous bytes
+      const int r = f >> 3, c = f & 7;
+      v[i] = *reinterpret_cast<const float4*>(X + (r0 + r) * ld + k0 + 4 * c);
+    } else {   // [k][r]: R/4 threads per k row
+      const int k = f / (R / 4), r4 = f % (R / 4);
+      v[i] = *reinterpret_cast<const float4*>(X + (k0 + k) * ld + r0 + 4 * r4);
+    }
   }
-  const int64_t step = (ep.kind >= HVAE_EPI_BIAS_GELU_DROP && ep.kind <= HVAE_EPI_DROP_BWD) ? load_step(ep.step_dev) : 0;
-  if (!slab) {
+}
+
+template <bool KC, int R>
+__device__ __forceinline__ void fast_lstore(float4* __restrict__ img, const float4 (&v)[FImg<R>::LD]) {
+  const int t = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < IM; ++i)
-#pragma unroll
-      for (int j = 0; j < JN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
-          const int64_t col = n0 + wn + j * 16 + (lane & 15);
-          if (row >= M || col >= N) continue;
-          float c = alpha * acc[i][j][r];
-          if (beta != 0.f) c += beta * C[row * ldc + col];
-          C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c, C);
-        }
-    return;
+  for (int i = 0; i < FImg<R>::LD; ++i) {
+    const int f = t + 256 * i;
+    if (KC) {
+      const int r = f >> 3, c = f & 7;
+      img[c * FImg<R>::CS + r] = v[i];
+    } else {
+      const int k = f / (R / 4), r4 = f % (R / 4);
+      float* d = reinterpret_cast<float*>(img + (k >> 2) * FImg<R>::CS + 4 * r4) + (k & 3);
+      d[0] = v[i].x;
+      d[4] = v[i].y;
+      d[8] = v[i].z;
+      d[12] = v[i].w;
+    }
   }
-  // ---- split-K: publish the partial tile, the last arrival reduces
+}
+
+template <bool TA, bool TB, int BM, int BN>
+__device__ __forceinline__ void gemm_fast_block(const GemmP& g, unsigned bx, unsigned by, unsigned bz,
+                                                float4* __restrict__ smem) {
+  constexpr int IM = BM / 32, JN = BN / 32;
+  using IA = FImg<BM>;
+  using IB = FImg<BN>;
+  float4* sA[2] = {smem, smem + IA::F4};
+  float4* sB[2] = {smem + 2 * IA::F4, smem + 2 * IA::F4 + IB::F4};
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t m0 = (int64_t)by * BM, n0 = (int64_t)bx * BN;
+  const int64_t kb = (int64_t)bz * g.kps;
+  const int nst = (int)((min(g.K, kb + g.kps) - kb) / FBK);
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  const int q = lane >> 4, c16 = lane & 15;
+  const bool do_rowsum = g.ep.opa_rowsum != nullptr && bx == 0;
+  float rowsum = 0.f;
+
+  f32x4 acc[IM][JN];
 #pragma unroll
   for (int i = 0; i < IM; ++i)
 #pragma unroll
-    for (int j = 0; j < JN; ++j)
+    for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // a ring of FP stages of register-staged global loads (the k range's first FP stages issued at once,
+  // each slot refilled FP stages ahead as soon as it has been copied to LDS)
+  constexpr int FP = FAST_PREFETCH;
+  float4 ra[FP][IA::LD], rb[FP][IB::LD];
+  // A: op(A)[m][k] is A[m][k] (k-contiguous) unless TA; B: op(B)[k][n] is B[n][k] (k-contiguous) if TB
+  auto gload = [&](int st, float4 (&xa)[IA::LD], float4 (&xb)[IB::LD]) {
+    const int64_t k0 = kb + (int64_t)st * FBK;
+    if (TA) fast_gload<false, BM>(g.A, g.lda, m0, k0, xa);
+    else fast_gload<true, BM>(g.A, g.lda, m0, k0, xa);
+    if (TB) fast_gload<true, BN>(g.B, g.ldb, n0, k0, xb);
+    else fast_gload<false, BN>(g.B, g.ldb, n0, k0, xb);
+  };
+  auto lstore = [&](int buf, const float4 (&xa)[IA::LD], const float4 (&xb)[IB::LD]) {
+    if (TA) fast_lstore<false, BM>(sA[buf], xa);
+    else fast_lstore<true, BM>(sA[buf], xa);
+    if (TB) fast_lstore<true, BN>(sB[buf], xb);
+    else fast_lstore<false, BN>(sB[buf], xb);
+  };
+  auto compute = [&](int buf) {
+    const float4* a_ = sA[buf] + wm + c16;
+    const float4* b_ = sB[buf] + wn + c16;
+    if (do_rowsum && t < BM) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
-        const int64_t col = n0 + wn + j * 16 + (lane & 15);
-        if (row < M && col < N) st_shared_f(&slab[((int64_t)bz * M + row) * N + col], acc[i][j][r]);
+      for (int c = 0; c < FBK / 4; ++c) {
+        const float4 x = sA[buf][c * IA::CS + t];
+        rowsum += x.x;
+        rowsum += x.y;
+        rowsum += x.z;
+        rowsum += x.w;
       }
-  const unsigned tile = by * g.gx + bx;
-  if (!last_block_arrives(&tickets[tile], g.gz)) return;
-  // the tile's elements per thread: one coherent load each per split, all in flight together
-  constexpr int Q = BM * BN / 256;
-  const int S = (int)g.gz;
-  float sum[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) sum[q] = 0.f;
-  for (int z = 0; z < S; ++z) {
-    float v[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int e = t + 256 * q;
-      const int64_t row = m0 + e / BN, col = n0 + e % BN;
-      v[q] = (row < M && col < N) ? ld_shared_f(&slab[((int64_t)z * M + row) * N + col]) : 0.f;
     }
 #pragma unroll
-    for (int q = 0; q < Q; ++q) sum[q] += v[q];
-  }
+    for (int j = 0; j < FBK / 16; ++j) {
+      float4 af[IM], bfr[JN];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    const int e = t + 256 * q;
-    const int64_t row = m0 + e / BN, col = n0 + e % BN;
-    if (row >= M || col >= N) continue;
-    float c = alpha * sum[q];
-    if (beta != 0.f) c += beta * C[row * ldc + col];
-    C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c, C);
+      for (int i = 0; i < IM; ++i) af[i] = a_[(4 * j + q) * IA::CS + 16 * i];
+#pragma unroll
+      for (int n = 0; n < JN; ++n) bfr[n] = b_[(4 * j + q) * IB::CS + 16 * n];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+          for (int n = 0; n < JN; ++n)
+            acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i][s], bfr[n][s], acc[i][n], 0, 0, 0);
+    }
+  };
+
+  // stage st: copy slot st % FP to LDS buffer st & 1, barrier, refill the slot with stage st + FP, MFMAs.
+  // LDS buffer b was last read by compute(st - 2), which every wave finished before the barrier of st - 1.
+#pragma unroll
+  for (int u = 0; u < FP; ++u)
+    if (u < nst) gload(u, ra[u], rb[u]);
+  for (int st0 = 0; st0 < nst; st0 += FP) {
+#pragma unroll
+    for (int u = 0; u < FP; ++u) {
+      const int st = st0 + u;
+      if (st < nst) {
+        lstore(st & 1, ra[u], rb[u]);
+        __syncthreads();
+        if (st + FP < nst) gload(st + FP, ra[u], rb[u]);
+        compute(st & 1);
+      }
+    }
   }
-  if (ep.opa_rowsum && bx == 0 && t < BM && m0 + t < M) {
-    float r = 0.f;
-    for (int z = 0; z < S; ++z) r += ld_shared_f(&slab[(int64_t)S * M * N + (int64_t)z * M + m0 + t]);
-    ep.opa_rowsum[m0 + t] = alpha * r;
+  gemm_finish<BM, BN>(g, acc, bx, by, bz, do_rowsum, rowsum);
+}
+
+template <int BM, int BN>
+constexpr int fast_smem_f4() { return 2 * (FImg<BM>::F4 + FImg<BN>::F4); }
+
+template <bool TA, bool TB, int BM, int BN>
+__global__ void __launch_bounds__(256) k_gemm_fast(GemmP g) {
+  __shared__ float4 smem[fast_smem_f4<BM, BN>()];
+  gemm_fast_block<TA, TB, BM, BN>(g, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+// the (dW = dY^T X, dX = dY W) pair of a layer's backward: the weight gradient (long K, split-K) on the
+// fast path in F0 x F0 tiles, the data gradient (short K) on the register-staged kernel in BT1 x BT1 tiles
+template <int F0, int BT1>
+__global__ void __launch_bounds__(256) k_gemm_mixed_pair(GemmP g0, GemmP g1) {
+  constexpr int S0 = fast_smem_f4<F0, F0>() * 4, S1 = gemm_smem_floats<BT1>() * 2;
+  __shared__ __attribute__((aligned(16))) float smem[S0 > S1 ? S0 : S1];
+  const unsigned n0 = g0.gx * g0.gy * g0.gz;
+  unsigned b = blockIdx.x;
+  if (b < n0) {
+    gemm_fast_block<true, false, F0, F0>(g0, b % g0.gx, (b / g0.gx) % g0.gy, b / (g0.gx * g0.gy),
+                                         reinterpret_cast<float4*>(smem));
+  } else {
+    b -= n0;
+    gemm_block<false, false, BT1, BT1>(g1, b % g1.gx, (b / g1.gx) % g1.gy, b / (g1.gx * g1.gy), smem,
+                                       smem + gemm_smem_floats<BT1>());
   }
 }
 
@@ -420,6 +620,42 @@ static int gemm_splits(int64_t M, int64_t N, int64_t K) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
+// ---- fast-path plan: a tile (BM x BN from the instantiated set) and a split count, or none
+struct FastPlan {
+  int bm = 0, bn = 0, splits = 1;
+  int64_t kps = 0;
+};
+// The fast path serves the weight gradients dW = dY^T X (trans_a, K = the batch): split-K over 32-deep
+// stages with four stages of loads in flight beat the register-staged kernel there (B = 4096, MI355X:
+// 384x384x4096 44.8 -> 32.8 us, 768x768x4096 124.6 -> 89.0, 256x512x4096 38.4 -> 27.6;
+// profiles/r02_gemm_fast_sweep.txt), while the short-K batch GEMMs (K = d, H or 2L) stay faster on the
+// register-staged kernel, which issues every k stage's loads at once (4096x384x384 27.3 us against
+// 38.8 at best); so do batches under 1024 (K = B). Tile: 32 x 32 while that gives <= 256 tiles, else 64 x 64.
+// A/B knobs, read at every call: HVAE_GEMM_FAST=0 (register-staged kernel only), HVAE_GEMM_FAST_TILE=32|64,
+// HVAE_GEMM_FAST_SPLITS=s
+static FastPlan fast_plan(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                          const float* B, int64_t ldb, bool /*pair_w*/) {
+  FastPlan f;
+  const char* e = std::getenv("HVAE_GEMM_FAST");
+  if (e && std::atoi(e) == 0) return f;
+  if (!ta || tb) return f;
+  if (K < 1024 || K % FBK || ((uintptr_t)A) % 16 || ((uintptr_t)B) % 16 || lda % 4 || ldb % 4) return f;
+  int bt = cdiv(M, 32) * cdiv(N, 32) <= 256 ? 32 : 64;
+  if (const char* t = std::getenv("HVAE_GEMM_FAST_TILE")) bt = std::atoi(t) == 64 ? 64 : 32;
+  if (M % bt || N % bt) return f;
+  const int64_t tiles = (M / bt) * (N / bt);
+  int64_t s = 1;
+  if (K > 1024) s = std::max<int64_t>(1, std::min<int64_t>((512 + tiles - 1) / tiles, K / 256));
+  if (const char* t = std::getenv("HVAE_GEMM_FAST_SPLITS")) s = std::max(1, std::atoi(t));
+  s = std::min<int64_t>(s, 64);
+  if (s > 1 && tiles > (int64_t)kTicketSlice) s = 1;
+  const int64_t kps = cdiv(cdiv(K, s), FBK) * FBK;
+  f.bm = f.bn = bt;
+  f.splits = (int)cdiv(K, kps);
+  f.kps = kps;
+  return f;
+}
+
 static int colsum_parts(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 64), 64)); }
 
 }  // namespace hvae
@@ -427,14 +663,22 @@ static int colsum_parts(int64_t M) { return (int)std::max<int64_t>(1, std::min<i
 using namespace hvae;
 
 extern "C" size_t hvae_gemm_f32_workspace(int64_t M, int64_t N, int64_t K) {
-  const int s = gemm_splits(M, N, K);
+  int s = gemm_splits(M, N, K);
+  // the fast path's split count (operands assumed aligned; as a pair's weight-gradient half or alone)
+  static const float dummy[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int pw = 0; pw < 2; ++pw)
+    for (int ta = 0; ta < 2; ++ta) {
+      const FastPlan f = fast_plan(ta, false, M, N, K, dummy, 4, dummy, 4, pw);
+      if (f.bm) s = std::max(s, f.splits);
+    }
   return s > 1 ? (size_t)s * (M * N + M) * sizeof(float) : 0;
 }
 
 // Validate one problem and fill its launch record (tile size in *bt).
 static int gemm_setup(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha, const float* A,
                       int64_t lda, const float* B, int64_t ldb, float beta, float* C, int64_t ldc,
-                      const hvae_epilogue* epi, void* ws, size_t ws_bytes, GemmP& g, int& bt) {
+                      const hvae_epilogue* epi, void* ws, size_t ws_bytes, GemmP& g, int& bt,
+                      FastPlan* fp = nullptr, bool pair_w = false) {
   HVAE_REQUIRE(M >= 0 && N >= 0 && K >= 0 && C, "hvae_gemm_f32: bad shape / null C");
   HVAE_REQUIRE(ldc >= N, "hvae_gemm_f32: ldc < N");
   HVAE_REQUIRE(M < (1ll << 31) / 64 * 64 && N < (1ll << 31), "hvae_gemm_f32: too large");
@@ -465,7 +709,9 @@ static int gemm_setup(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
     HVAE_REQUIRE(ep.kind != HVAE_EPI_BIAS_GELU_DROP || ep.pre_out, "hvae_gemm_f32: no pre_out");
     HVAE_REQUIRE(ep.kind != HVAE_EPI_GELU_DROP_BWD || ep.pre_in, "hvae_gemm_f32: no pre_in");
   }
-  int splits = gemm_splits(M, N, K);
+  FastPlan f;
+  if (fp) f = fast_plan(trans_a, trans_b, M, N, K, A, lda, B, ldb, pair_w);
+  int splits = f.bm ? f.splits : gemm_splits(M, N, K);
   if (splits > 1) {
     const int64_t fit = ws ? (int64_t)(ws_bytes / ((size_t)(M * N + M) * sizeof(float))) : 0;
     splits = (int)std::min<int64_t>(splits, fit);
@@ -477,12 +723,18 @@ static int gemm_setup(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
     splits = (int)cdiv(K, kps);
   }
   bt = gemm_tile(M, N, K);
+  if (fp) {
+    f.splits = splits;
+    f.kps = kps;
+    *fp = f;
+  }
   g.M = M; g.N = N; g.K = K; g.kps = (K == 0) ? 0 : kps;
   g.alpha = alpha; g.A = A; g.lda = lda; g.B = B; g.ldb = ldb; g.beta = beta; g.C = C; g.ldc = ldc;
   g.ep = ep;
   g.vec_a = (((uintptr_t)A) % 16 == 0) && (lda % 4 == 0);
   g.vec_b = (((uintptr_t)B) % 16 == 0) && (ldb % 4 == 0);
-  g.gx = (unsigned)cdiv(N, bt); g.gy = (unsigned)cdiv(M, bt); g.gz = (unsigned)std::max(splits, 1);
+  g.gx = (unsigned)cdiv(N, f.bm ? f.bn : bt); g.gy = (unsigned)cdiv(M, f.bm ? f.bm : bt);
+  g.gz = (unsigned)std::max(splits, 1);
   g.slab = splits > 1 ? (float*)ws : nullptr;
   g.tickets = nullptr;
   if (g.slab) {
@@ -503,12 +755,19 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
   }
   GemmP g{};
   int bt = 32;
+  FastPlan f;
   if (int rc = gemm_setup(trans_a, trans_b, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, epi, ws, ws_bytes, g,
-                          bt))
+                          bt, &f))
     return rc;
   hipStream_t st = as_stream(stream);
   dim3 grid(g.gx, g.gy, g.gz);
   ProbeScope probe("gemm", st);
+  if (f.bm) {  // trans_a && !trans_b
+    if (f.bm == 64) k_gemm_fast<true, false, 64, 64><<<grid, 256, 0, st>>>(g);
+    else k_gemm_fast<true, false, 32, 32><<<grid, 256, 0, st>>>(g);
+    HVAE_LAUNCH_CHECK("k_gemm_fast");
+    return HVAE_OK;
+  }
 #define HVAE_GEMM_CALL(TA_, TB_)                                                 \
   (bt == 64 ? (k_gemm_f32<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(g))            \
             : (k_gemm_f32<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(g)))
@@ -539,13 +798,28 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
   }
   GemmP g0{}, g1{};
   int bt0 = 32, bt1 = 32;
+  FastPlan f0, f1;
   if (int rc = gemm_setup(1, 0, w->M, w->N, w->K, w->alpha, w->A, w->lda, w->B, w->ldb, w->beta, w->C, w->ldc,
-                          w->epi, w->ws, w->ws_bytes, g0, bt0))
+                          w->epi, w->ws, w->ws_bytes, g0, bt0, &f0, true))
     return rc;
   if (int rc = gemm_setup(0, 0, x->M, x->N, x->K, x->alpha, x->A, x->lda, x->B, x->ldb, x->beta, x->C, x->ldc,
-                          x->epi, x->ws, x->ws_bytes, g1, bt1))
+                          x->epi, x->ws, x->ws_bytes, g1, bt1, &f1))
     return rc;
   hipStream_t st = as_stream(stream);
+  if (f0.bm || f1.bm) {
+    if (!f0.bm || f1.bm || (g0.slab && g1.slab)) {  // not (fast dW, register-staged dX): two launches
+      if (int rc = gemm_desc(w, stream)) return rc;
+      return gemm_desc(x, stream);
+    }
+    const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
+    ProbeScope probe("gemm", st);
+    if (f0.bm == 64 && bt1 == 64) k_gemm_mixed_pair<64, 64><<<nblk, 256, 0, st>>>(g0, g1);
+    else if (f0.bm == 64) k_gemm_mixed_pair<64, 32><<<nblk, 256, 0, st>>>(g0, g1);
+    else if (bt1 == 64) k_gemm_mixed_pair<32, 64><<<nblk, 256, 0, st>>>(g0, g1);
+    else k_gemm_mixed_pair<32, 32><<<nblk, 256, 0, st>>>(g0, g1);
+    HVAE_LAUNCH_CHECK("k_gemm_mixed_pair");
+    return HVAE_OK;
+  }
   const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
   ProbeScope probe("gemm", st);
   if (bt0 == 64 && bt1 == 64) k_gemm_f32_pair<64, 64><<<nblk, 256, 0, st>>>(g0, g1);

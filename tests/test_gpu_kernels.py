@@ -441,7 +441,9 @@ def test_clip_step_counters(ops, hip_device):
 
 
 @pytest.mark.parametrize("nb,N,lam,hot", [(40, 300, 5.0, 0), (64, 12101, 3.0, 40), (300, 2000, 8.0, 100), (5000, 500, 2.0, 4500),
-                                         (40000, 3000, 1.0, 3000), (40000, 3000, 1.0, 6000)])
+                                         (40000, 3000, 1.0, 3000), (40000, 3000, 1.0, 6000),
+                                         # catalogs past the one-block scan: the look-back scan over 4096-item blocks
+                                         (4096, 100000, 15.0, 300), (2000, 1000003, 15.0, 0)])
 def test_rowgrad_plan_apply_segments(ops, hip_device, nb, N, lam, hot):
     """Segments of every sort path (wave <= 64; bitmap rank for nb <= 32768; beyond that block bitonic
     <= 4096 and selection): plan + apply == dense reference, bitwise == the one-call form, and bitwise
@@ -465,8 +467,10 @@ def test_rowgrad_plan_apply_segments(ops, hip_device, nb, N, lam, hot):
     one = rg.rows[:nu].clone()
     dense = torch.zeros(N, H, device=hip_device)
     ops.rowgrad_to_dense(rg, dense)
-    x = torch.as_tensor(X.toarray(), dtype=torch.float64)
-    assert _maxrel(dense, x.t() @ da.double()) < 1e-5
+    ref = torch.as_tensor(np.asarray(X.T.astype(np.float64) @ da.double().numpy()))  # sparse: N may be 1M
+    assert _maxrel(dense, ref) < 1e-5
+    # slots in ascending item order, one per distinct item of the batch
+    np.testing.assert_array_equal(rg.item_of[:nu].cpu().numpy(), np.unique(X.indices))
     st = stream_of(dad)
     _lib.check(lib().hvae_w1_rowgrad_plan(xd.ref, rg.ref, ptr(rg.ws), rg.ws.numel(), st), "plan")
     _lib.check(lib().hvae_w1_rowgrad_apply(ptr(dad), H, rg.ref, st), "apply")
@@ -480,7 +484,8 @@ def test_rowgrad_plan_apply_segments(ops, hip_device, nb, N, lam, hot):
         assert np.all(cslot[seg[s_]:seg[s_ + 1]] == s_)
     if hot:  # the long segment (its own sort path) against a float64 sum
         s0 = int((rg.item_of[:nu] == 0).nonzero()[0, 0])
-        assert _maxrel(rg.rows[s0], x[:, 0] @ da.double()) < 1e-5
+        col0 = torch.as_tensor(X[:, 0].toarray().ravel(), dtype=torch.float64)
+        assert _maxrel(rg.rows[s0], col0 @ da.double()) < 1e-5
 
 
 # ------------------------------------------------------------------ eval ---

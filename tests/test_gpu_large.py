@@ -125,7 +125,8 @@ def test_decoder_train_full_shape(ops, hip_device, dtype, nb, N, D):
 
 @pytest.mark.timeout(300)
 def test_decoder_d768_versions_agree(ops, hip_device, monkeypatch):
-    """Versions 4 (item-split GEMM1, one barrier per tile) and 3 (item-half softmax ownership) against version 2
+    """Versions 5 (GEMM1 and GEMM2 on different waves), 4 (item-split GEMM1, one barrier per tile) and 3
+    (item-half softmax ownership) against version 2
     (whole-tile softmax in both waves) of the d = 768 bf16 sweep: all round the same bf16 operands (P to bf16
     included); only fp32 summation order differs."""
     nb, N, D = 700, 50_001, 768
@@ -135,12 +136,14 @@ def test_decoder_d768_versions_agree(ops, hip_device, monkeypatch):
     img = ops.decoder_image(E)
     enorm = ops.row_norm_max(img)
     out = {}
-    for name, v3, v4 in (("v4", "1", "1"), ("v3", "1", "0"), ("v2", "0", "0")):
+    for name, v3, v4, v5 in (("v5", "1", "1", "1"), ("v4", "1", "1", "0"), ("v3", "1", "0", "0"),
+                             ("v2", "0", "0", "0")):
         monkeypatch.setenv("HVAE_DEC_V3", v3)
         monkeypatch.setenv("HVAE_DEC_V4", v4)
+        monkeypatch.setenv("HVAE_DEC_V5", v5)
         out[name] = ops.decoder_train(xd, U, img, enorm, E, 1.0 / nb, want_o=True)
     l2, o2, r2, d2 = out["v2"]
-    for name in ("v4", "v3"):
+    for name in ("v5", "v4", "v3"):
         la, oa, ra, da = out[name]
         assert (la - l2).abs().max() < 1e-4, name
         assert _maxrel(oa, o2) < 5e-3 and _maxrel(ra, r2) < 1e-5 and _maxrel(da, d2) < 5e-3, name
