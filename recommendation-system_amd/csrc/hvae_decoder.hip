@@ -2077,6 +2077,311 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   }
 }
 
+// fp8 at d = 768 with version 4's structure (k_dec4_f8): wave (ug, dh) computes the COMPLETE S^T of items
+// 32 dh .. 32 dh + 31 of each 64-item tile over all of D (u over all of D as e4m3: 96 VGPRs, where the
+// DS = 2 ring above holds a D half and exchanges partial scores), so only P crosses LDS: each wave writes its
+// packed e4m3 half and that half's block exponent (the MFMA takes k-block b's scale from lane column + 32 b,
+// so the halves keep their own exponents), double-buffered by tile parity, which leaves one barrier per tile:
+//   [barrier: tile t + 1 landed, P(t) halves published, GEMM2(t - 1) done]
+//   -> GEMM1(t + 1) (12 32x32x64 MFMAs, the LDS-DMA of tile t + 2 one piece per MFMA gap)
+//   -> the own half's max and exponent -> GEMM2(t) (12 MFMAs over both item halves, the 16 exponentials of
+//   tile t + 1 in its gaps) -> P(t + 1) half out.
+// The image, the pieces, the GEMM2 transposed reads, the exponent rule and the fixed offset are k_dec_fp8's.
+#ifndef F8V4_G1_AHEAD
+#define F8V4_G1_AHEAD 2
+#endif
+constexpr int kF8v4PBytes = 1024 + 256;  // per wave and parity: P half (64 lanes x 16 B) + exponent (64 x 4 B)
+constexpr int f8v4_lds_bytes() { return 3 * 64 * 768 + 2 * 4 * kF8v4PBytes + 4 * 256; }
+
+template <bool WITH_O>
+__global__ void __launch_bounds__(256) k_dec4_f8(const float* __restrict__ U, int64_t ldu,
+                                                 const unsigned char* __restrict__ T8, const int* __restrict__ e_exp,
+                                                 const float* __restrict__ e_maxnorm, int64_t nb, int64_t N,
+                                                 int splits, int64_t tiles_per_split, DecOut out) {
+  constexpr int D = 768;
+  constexpr int DW = D / 2;        // GEMM2: dims owned by one wave
+  constexpr int KS = D / 64;       // GEMM1 k-steps over all of D
+  constexpr int DB = DW / 32;      // GEMM2 d-blocks
+  constexpr int TB = f8_tile_bytes<D>();
+  constexpr int PW = TB / 4096;    // 1-KiB LDS-DMA pieces per wave per tile (12)
+  constexpr int NS = 3;
+  static_assert(f8v4_lds_bytes() <= 160 * 1024, "k_dec4_f8 LDS");
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned char* pbuf = lds + NS * TB;                                        // [2 par][4 w][kF8v4PBytes]
+  float* xm = reinterpret_cast<float*>(lds + NS * TB + 2 * 4 * kF8v4PBytes);  // [4 w][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ug = w & 1, dh = w >> 1, pw = w ^ 2;
+  const int dbase = dh * DW;
+  const int split = blockIdx.x % splits;
+  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 64 + ug * 32;
+  const int64_t user = u0 + col;
+  const bool wave_active = u0 < nb;
+  const int64_t ntiles = (N + kF8TI - 1) / kF8TI;
+  const int64_t t_beg = (int64_t)split * tiles_per_split;
+  const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
+  const float emax = *e_maxnorm;  // scalars before any LDS-DMA is in flight
+  const int ke = *e_exp;
+  const int sa = 127 - ke;
+
+  // u over all of D: lane (col, h) holds u[64 ks + 32 h + j], j < 32, as e4m3 of u 2^ku (ku from the row)
+  const float* urow = U + min(user, nb - 1) * ldu + 32 * h;
+  float amax = 0.f, usq = 0.f;
+#pragma unroll 8
+  for (int q4 = 0; q4 < D / 8; ++q4) {
+    const float4 a = *reinterpret_cast<const float4*>(urow + 64 * (q4 >> 3) + 4 * (q4 & 7));
+    amax = fmaxf(amax, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+    usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
+  }
+  amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+  usq += __shfl_xor(usq, 32, 64);
+  int eu = 0;
+  (void)frexpf(amax, &eu);
+  const int ku = amax > 0.f ? min(127, 8 - eu) : 0;
+  const int sbu = 127 - ku;
+  const float qu = ldexpf(1.f, ku);
+  i32x8 uf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int q4 = 0; q4 < 8; ++q4) {
+      const float4 a = *reinterpret_cast<const float4*>(urow + 64 * ks + 4 * q4);
+      uf[ks][q4] = pack_fp8x4(a.x * qu, a.y * qu, a.z * qu, a.w * qu);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+
+  const int voff = w * PW * 1024 + lane * 16;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(T8), (short)0, (int)(ntiles * TB), 0x00020000);
+  const uint32_t ring0 = lds_addr(lds) + (uint32_t)(w * PW * 1024);
+  auto issue_piece = [&](uint32_t soff, int slot_i, int i, bool fresh) {
+    const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
+    if (fresh)
+      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff), "s"(rsrc), "s"(soff + (uint32_t)(i * 1024)) : "memory");
+    else
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :: "s"(lb + (uint32_t)(i * 1024)), "v"(voff), "s"(rsrc), "s"(soff + (uint32_t)(i * 1024)) : "memory");
+  };
+  auto tile_soff = [&](int64_t t) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)TB)); };
+  auto barrier = [&] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // GEMM1 A operand (k-step ks of all of D): item row 32 dh + col, chunks 4 ks + 2 h + {0, 1}
+  const int swc = f8_sw(D, col);  // f8_sw depends on the low 4 bits of the row only
+  const unsigned char* rowA_off = nullptr;
+  const int rowA = (32 * dh + col) * D;
+  auto rdA = [&](const unsigned char* buf, int ks) {
+    const int ch = 4 * ks + 2 * h;
+    const unsigned char* row = buf + rowA;
+    const uint4 x = *reinterpret_cast<const uint4*>(row + 16 * (ch ^ swc));
+    const uint4 y = *reinterpret_cast<const uint4*>(row + 16 * ((ch + 1) ^ swc));
+    i32x8 r;
+    r[0] = (int)x.x; r[1] = (int)x.y; r[2] = (int)x.z; r[3] = (int)x.w;
+    r[4] = (int)y.x; r[5] = (int)y.y; r[6] = (int)y.z; r[7] = (int)y.w;
+    return r;
+  };
+  (void)rowA_off;
+  // GEMM2 A operand (d-block db of this wave's D half): four transposed reads of items f8_item_of(h, 8 c + qq)
+  const int g1 = (lane >> 4) & 1, qq = (lane & 15) >> 1, pp = lane & 1;
+  int trow[4], tsw[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int it = f8_item_of(h, 8 * c + qq);
+    trow[c] = it * D + 8 * pp;
+    tsw[c] = f8_sw(D, it);
+  }
+  auto rdB = [&](const unsigned char* buf, int db) {
+    i32x8 r;
+    const int ch = 2 * (dbase / 32 + db) + g1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+          (__attribute__((address_space(3))) i32x2*)(void*)(buf + trow[c] + 16 * (ch ^ tsw[c])));
+      r[2 * c] = v[0];
+      r[2 * c + 1] = v[1];
+    }
+    return r;
+  };
+  auto gemm1 = [&](const unsigned char* buf, f32x16& sv, auto&& fill) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) sv[r] = 0.f;
+    constexpr int AH = F8V4_G1_AHEAD;
+    i32x8 ra[AH];
+#pragma unroll
+    for (int j = 0; j < AH; ++j) ra[j] = rdA(buf, j);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const i32x8 c = ra[ks % AH];
+      if (ks + AH < KS) ra[ks % AH] = rdA(buf, ks + AH);
+      sv = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, uf[ks], sv, 0, 0, 0, sa, 0, sbu);
+      fill(ks);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  f32x16 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  auto gemm2 = [&](const unsigned char* buf, const i32x8& pf, int sbp, auto&& fill) {
+    if constexpr (WITH_O) {
+      constexpr int AH2 = 2;
+      i32x8 a[AH2];
+#pragma unroll
+      for (int j = 0; j < AH2; ++j) a[j] = rdB(buf, j);
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        const i32x8 c = a[db % AH2];
+        if (db + AH2 < DB) a[db % AH2] = rdB(buf, db + AH2);
+        o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
+        fill(db);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int db = 0; db < DB; ++db) fill(db);
+    }
+  };
+
+  float m = 0.f, mL = 0.f, lsum = 0.f;
+  const float bound = sqrtf(usq) * emax * 1.02f;
+  // own half of tile t: items past N -> -inf; the half's max over its 32 items (every lane of a column)
+  auto half_max = [&](int64_t t, f32x16& sv) {
+    if (t == ntiles - 1 && (N % kF8TI) != 0) {
+      const int lim = (int)(N - t * kF8TI) - 4 * h - 32 * dh;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[r] = ((r & 3) + 8 * (r >> 2) >= lim) ? -INFINITY : sv[r];
+    }
+    const float a0 = fmaxf(fmaxf(sv[0], sv[1]), sv[2]), a1 = fmaxf(fmaxf(sv[3], sv[4]), sv[5]);
+    const float a2 = fmaxf(fmaxf(sv[6], sv[7]), sv[8]), a3 = fmaxf(fmaxf(sv[9], sv[10]), sv[11]);
+    const float a4 = fmaxf(fmaxf(sv[12], sv[13]), fmaxf(sv[14], sv[15]));
+    float mx = fmaxf(fmaxf(fmaxf(a0, a1), a2), fmaxf(a3, a4));
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+    return fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+  };
+  auto tile_exp = [&](float mh) { return max(-119, min(127, (int)ceilf(__builtin_fmaf(mh, kLog2e, -mL)) - 8)); };
+  auto p_slot = [&](int par, int ww) { return pbuf + (par * 4 + ww) * kF8v4PBytes; };
+  int pk[4] = {0, 0, 0, 0}, e_own = 0;  // this wave's P half of the current tile and its exponent
+  auto p_publish = [&](int par) {
+    reinterpret_cast<int4*>(p_slot(par, w))[lane] = make_int4(pk[0], pk[1], pk[2], pk[3]);
+    reinterpret_cast<int*>(p_slot(par, w) + 1024)[lane] = e_own;
+  };
+
+  f32x16 s_nx;
+  if (t_beg < t_end) {
+    for (int i = 0; i < PW; ++i) issue_piece(tile_soff(t_beg), 0, i, i == 0);
+    if (t_beg + 1 < t_end)
+      for (int i = 0; i < PW; ++i) issue_piece(tile_soff(t_beg + 1), 1, i, false);
+    wait_vmcnt<0>();
+  }
+  barrier();
+  float mh = 0.f;
+  if (t_beg < t_end) {
+    gemm1(lds, s_nx, [](int) {});
+    mh = half_max(t_beg, s_nx);
+    if (lane < 32) xm[w * 64 + lane] = mh;
+  }
+  barrier();  // the pair's common offset from the first tile's max over both halves
+  if (t_beg < t_end) {
+    m = fmaxf(fmaxf(mh, xm[pw * 64 + col]), bound - kOffsetSpan);
+    mL = m * kLog2e;
+    e_own = tile_exp(mh);
+    const float cE = mL + (float)e_own;
+    float qsum = 0.f;
+#pragma unroll
+    for (int j4 = 0; j4 < 4; ++j4) {
+      float q[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        q[b] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_nx[4 * j4 + b], kLog2e, -cE));
+        qsum += q[b];
+      }
+      pk[j4] = pack_fp8x4(q[0], q[1], q[2], q[3]);
+    }
+    lsum += ldexpf(qsum, e_own);
+    p_publish(0);
+  }
+  for (int64_t t = t_beg; t < t_end; ++t) {
+    const int li = (int)(t - t_beg);
+    const int cur = li % NS, nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
+    wait_vmcnt<0>();
+    barrier();  // tile t + 1 landed, P(t) halves published, GEMM2(t - 1) done
+    const int4 y = reinterpret_cast<const int4*>(p_slot(par, pw))[lane];
+    const int ey = reinterpret_cast<const int*>(p_slot(par, pw) + 1024)[lane];
+    i32x8 pf;
+    if (dh == 0) {
+      pf[0] = pk[0]; pf[1] = pk[1]; pf[2] = pk[2]; pf[3] = pk[3];
+      pf[4] = y.x; pf[5] = y.y; pf[6] = y.z; pf[7] = y.w;
+    } else {
+      pf[0] = y.x; pf[1] = y.y; pf[2] = y.z; pf[3] = y.w;
+      pf[4] = pk[0]; pf[5] = pk[1]; pf[6] = pk[2]; pf[7] = pk[3];
+    }
+    const int sbp = 127 + (h == dh ? e_own : ey);  // lane half h: k-block h's scale
+    const bool more = t + 1 < t_end;
+    if (more) {
+      const bool dma = t + 2 < t_end;
+      const uint32_t soff_dma = tile_soff(dma ? t + 2 : t);
+      gemm1(lds + nxt * TB, s_nx, [&](int ks) {
+        if (dma) issue_piece(soff_dma, s_dma, ks, ks == 0);
+      });
+      mh = half_max(t + 1, s_nx);
+    }
+    const int e_nx = more ? tile_exp(mh) : 0;
+    const float cE = mL + (float)e_nx;
+    float q[16];
+    float qsum = 0.f;
+    int pk_nx[4];
+    gemm2(lds + cur * TB, pf, sbp, [&](int db) {
+      if (more) {
+#pragma unroll
+        for (int j = (16 * db) / DB; j < (16 * (db + 1)) / DB; ++j) {
+          q[j] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_nx[j], kLog2e, -cE));
+          qsum += q[j];
+          if ((j & 3) == 3) pk_nx[j >> 2] = pack_fp8x4(q[j - 3], q[j - 2], q[j - 1], q[j]);
+        }
+      }
+    });
+    if (more) {
+      lsum += ldexpf(qsum, e_nx);
+      pk[0] = pk_nx[0]; pk[1] = pk_nx[1]; pk[2] = pk_nx[2]; pk[3] = pk_nx[3];
+      e_own = e_nx;
+      p_publish(par ^ 1);
+    }
+  }
+  wait_vmcnt<0>();
+  // l = own half (both lane halves of the column) + the partner's half, in dh order
+  const float lw = lsum + __shfl_xor(lsum, 32, 64);
+  barrier();
+  if (lane < 32) xm[w * 64 + lane] = lw;
+  barrier();
+  const float ltot = dh == 0 ? lw + xm[pw * 64 + col] : xm[pw * 64 + col] + lw;
+  if (!wave_active || t_beg >= t_end || user >= nb) return;
+  if (h == 0 && dh == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
+  const int64_t row = out.direct ? user : (int64_t)split * nb + user;
+  if (h == 0 && dh == 0) {
+    if (out.direct) out.lse[user] = m + logf(ltot);
+    else { out.m[row] = m; out.l[row] = ltot; }
+  }
+  if (WITH_O) {
+    const float sc = out.direct ? 1.0f / ltot : 1.0f;
+#pragma unroll
+    for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
+        *reinterpret_cast<float4*>(out.O + row * D + dd) =
+            make_float4(o[d][4 * g4] * sc, o[d][4 * g4 + 1] * sc, o[d][4 * g4 + 2] * sc, o[d][4 * g4 + 3] * sc);
+      }
+  }
+}
+
 // ------------------------------------------------------------------- f32 ---
 // Same algorithm on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 sums):
 // 4 waves x 16 users, 16-item tiles, LDS rows padded to D+2 floats
@@ -2768,6 +3073,22 @@ static int launch_fp8(const float* U, int64_t ldu, const void* E, const float* e
   return HVAE_OK;
 }
 
+template <bool WO>
+static int launch_fp8_v4(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
+                         const DecPlan& p, DecOut o, hipStream_t st) {
+  constexpr int D = 768, lds = f8v4_lds_bytes();
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec4_f8<WO>, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr_set = true;
+  }
+  const unsigned char* T8 = (const unsigned char*)E + f8_offset_bytes(N, D);
+  const int* ke = (const int*)((const char*)E + f8_tail_offset(N, D));
+  k_dec4_f8<WO><<<(unsigned)p.blocks, 256, lds, st>>>(U, ldu, T8, ke, enorm, nb, N, p.splits, p.tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec4_f8");
+  return HVAE_OK;
+}
+
 template <int D, bool WO>
 static int launch_f32(const float* U, int64_t ldu, const void* E, int64_t nb, int64_t N, const DecPlan& p,
                       DecOut o, hipStream_t st) {
@@ -2791,7 +3112,9 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
       case 128: return launch_fp8<128, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 256: return launch_fp8<256, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 384: return launch_fp8<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
-      case 768: return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+      case 768:  // HVAE_DEC_F8V4=0 keeps the D-split ring (A/B; read at every call)
+        if (env_int("HVAE_DEC_F8V4", 0) != 0) return launch_fp8_v4<WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       default: break;
     }
   } else if (dtype == HVAE_BF16 && p.v5 && D == 768) {
