@@ -143,6 +143,8 @@ class DPExchange:
                 send=torch.zeros(L, dtype=torch.float32, device=dev),
                 recv=torch.zeros(W, L, dtype=torch.float32, device=dev),
                 send_da=torch.zeros(B, H, dtype=torch.float32, device=dev),
+                send_g=torch.zeros(ns, dtype=torch.float32, device=dev),
+                recv_g=torch.zeros(W, ns, dtype=torch.float32, device=dev),
                 recv_da=torch.zeros(W * B, H, dtype=torch.float32, device=dev),
                 rp_u=torch.zeros(W * (B + 1), dtype=torch.int64, device=dev),
                 base=(torch.arange(W, dtype=torch.int64, device=dev) * L + ns + B + 1)[:, None],
@@ -181,6 +183,69 @@ class DPExchange:
             return
         self._all_gather(self.recv.reshape(-1), self.send)
         self._all_gather(self.recv_da, self.send_da)
+
+    # ------------------------------------------- the step in two exchanges ---
+    # The trainer sends the batch CSR before the forward, so that the union batch's row-gradient plan (which
+    # needs the batches only) runs on a side stream beside the forward / decoder, and the small gradients
+    # and da after the backward; only the apply of the union row gradient is left between the second
+    # exchange and Adam. The packets and the results are those of pack / communicate / unpack_merge.
+    def pack_csr(self, x, nb: int, weight: float) -> None:
+        """Device-only: this rank's batch as compact CSR (values * weight), before its forward."""
+        flat = self.send
+        if x is None or nb == 0:
+            flat[self.ns:].zero_()
+            return
+        self.pack_fn(self, x, weight, flat[self.off_rp:self.off_rp + nb + 1].view(torch.int32),
+                     flat[self.off_col:self.off_col + self.cap].view(torch.int32),
+                     flat[self.off_col + self.cap:], self.cap)
+        if nb < self.B:  # a short tail: rows past nb are empty
+            flat[self.off_rp + nb + 1:self.off_rp + self.B + 1].view(torch.int32).copy_(
+                flat[self.off_rp + nb:self.off_rp + nb + 1].view(torch.int32).expand(self.B - nb))
+
+    def pack_grads(self, g_small: torch.Tensor, nb: int, da: torch.Tensor | None, weight: float) -> None:
+        """Device-only: the weighted small gradients and da, after the backward."""
+        torch.mul(g_small.reshape(-1), weight, out=self.send_g)
+        if da is None or nb == 0:
+            self.send_da.zero_()
+            return
+        if nb < self.B:
+            self.send_da[nb:].zero_()
+        if da.data_ptr() != self.send_da.data_ptr():
+            self.send_da[:nb].copy_(da[:nb])
+
+    def communicate_csr(self) -> None:
+        if self.world == 1:
+            self.recv[0].copy_(self.send)
+            return
+        self._all_gather(self.recv.reshape(-1), self.send)
+
+    def communicate_grads(self) -> None:
+        if self.world == 1:
+            self.recv_g[0].copy_(self.send_g)
+            self.recv_da.copy_(self.send_da)
+            return
+        self._all_gather(self.recv_g.reshape(-1), self.send_g)
+        self._all_gather(self.recv_da, self.send_da)
+
+    def merge_plan(self) -> None:
+        """Device-only, on the current stream: the union batch's row-gradient plan from the gathered CSR."""
+        from . import ops
+        W, B = self.world, self.B
+        rp = self.rp_u.view(W, B + 1)
+        rp.copy_(self.recv[:, self.off_rp:self.off_rp + B + 1].view(torch.int32))
+        rp.add_(self.base)
+        flat = self.recv.reshape(-1)
+        self._union = ops.Csr(self.rp_u, flat.view(torch.int32), flat[self.cap:], self.n_items, rows=self.rows_u,
+                              nb=W * B)
+        ops.w1_rowgrad_plan(self._union, self.merged)
+
+    def merge_apply(self, g_small: torch.Tensor):
+        """Device-only: dense gradients <- rank-order sum of the weighted small gradients; the union row
+        gradient <- the apply over the gathered da (after merge_plan)."""
+        from . import ops
+        torch.sum(self.recv_g, dim=0, out=g_small.reshape(-1))
+        ops.w1_rowgrad_apply(self.recv_da, self.merged)
+        return self.merged
 
     def unpack_merge(self, g_small: torch.Tensor):
         """Device-only (graph-capturable): dense gradients <- rank-order sum of the weighted packets; the union

@@ -222,6 +222,7 @@ class _StepBuffers:
         # side-stream GEMMs: their split-K slabs must not alias the main stream's
         self.ws2 = torch.empty_like(self.ws) if ex.two_streams else None
         self.graph = None
+        self.graph_pre = self.graph_up = None  # data parallel: the CSR-packet and update graphs of a step
         self.graph_data = None  # the DeviceData a captured graph reads (held, compared by identity)
 
 
@@ -395,13 +396,16 @@ class FusedTrainer:
         """Enqueue one full step on the current stream (captured into a graph by the caller).
 
         advance > 0 also moves the device batch offset (rows_offset) by that many users. Data parallel:
-        the step's exchange runs between the forward/backward and the update; weight = this rank's share of
-        the union batch.
+        the batch CSR is exchanged before the forward (the union batch's row-gradient plan then runs beside
+        it), the small gradients and da between the backward and the update; weight = this rank's share of the
+        union batch.
         """
         if train and self.dp is not None:
+            self._launch_pack_csr(bf, csr, weight)
+            self.dp.communicate_csr()
             self._launch_fwd_bwd(bf, csr, train, beta, p_drop, ext)
-            self._launch_pack(bf, csr, weight)
-            self._launch_exchange()
+            self._launch_pack_grads(bf, weight)
+            self.dp.communicate_grads()
             self._launch_dp_update(bf, advance)
             return
         self._launch_fwd_bwd(bf, csr, train, beta, p_drop, ext)
@@ -410,20 +414,24 @@ class FusedTrainer:
         elif advance:
             self._advance(advance)
 
-    def _launch_pack(self, bf: _StepBuffers | None, csr: CsrBatch | None, weight: float):
-        """End of a data-parallel forward/backward: this rank's packet (weighted small gradients, its batch
-        as compact CSR, its first-layer pre-activation gradient). bf None: no users in this step."""
+    def _launch_pack_csr(self, bf: _StepBuffers | None, csr: CsrBatch | None, weight: float):
+        """Start of a data-parallel step: this rank's batch as compact CSR (values * weight) into its packet.
+        bf None: no users in this step."""
         if bf is None:
-            self.dp.pack(self.g_small.zero_(), None, 0, None, 0.0)
+            self.dp.pack_csr(None, 0, 0.0)
             return
-        self.dp.pack(self.g_small, C.byref(csr), bf.B, bf.da[0], weight)
+        self.dp.pack_csr(C.byref(csr), bf.B, weight)
 
-    def _launch_exchange(self):
-        """The step's collectives (eager, between the two graphs)."""
-        self.dp.communicate()
+    def _launch_pack_grads(self, bf: _StepBuffers | None, weight: float):
+        """End of a data-parallel forward/backward: the weighted small gradients and the first-layer
+        pre-activation gradient da."""
+        if bf is None:
+            self.dp.pack_grads(self.g_small.zero_(), 0, None, 0.0)
+            return
+        self.dp.pack_grads(self.g_small, bf.B, bf.da[0], weight)
 
     def _launch_dp_update(self, bf: _StepBuffers, advance: int):
-        merged = self.dp.unpack_merge(self.g_small)
+        merged = self.dp.merge_apply(self.g_small)
         self._launch_update(merged, bf, advance)
 
     def _fork(self, src, dst):
@@ -467,13 +475,24 @@ class FusedTrainer:
         ev_plan = None
         dp = self.dp is not None
         if train and dp:
-            # data parallel: no local row gradient (the exchange builds the union's); the batch's W1t rows
-            # replay their deferred steps, found from the CSR entries, before the forward reads them
+            # data parallel: no local row gradient; the union batch's plan (from the CSR packets gathered
+            # before this forward) runs on the plan stream beside it, its apply after the second exchange. The
+            # batch's W1t rows replay their deferred steps, found from the CSR entries, before the forward
+            # reads them
             if self.lazy_adam:
                 cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
                 check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
                                                     ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
                       "adam_lazy_catchup_csr")
+            ps = self.plan_stream if self.plan_stream is not None else side
+            if ps is not main:
+                self._fork(main, ps)
+                with torch.cuda.stream(ps):
+                    self.dp.merge_plan()
+                ev_plan = torch.cuda.Event()
+                ev_plan.record(ps)
+            else:
+                self.dp.merge_plan()
         elif train and self.plan_stream is not None and B >= self.plan_side_min_batch:
             # the batch's W1t rows replay their deferred steps (found from the CSR) before the forward reads
             # them, while the row-gradient plan runs on the plan stream
@@ -747,9 +766,12 @@ class FusedTrainer:
                     self.host_step += 1
                 return False
             self._capture(bf, data, train, beta, p_drop, key)
+        if bf.graph_pre is not None:  # data parallel: the CSR packet, then its exchange
+            bf.graph_pre.replay()
+            self.dp.communicate_csr()
         bf.graph.replay()
-        if bf.graph_up is not None:  # data parallel: the collectives between the two graphs of a step
-            self._launch_exchange()
+        if bf.graph_up is not None:  # data parallel: the gradients' exchange between the step's graphs
+            self.dp.communicate_grads()
             bf.graph_up.replay()
         return True
 
@@ -820,13 +842,19 @@ class FusedTrainer:
             if c:
                 bfc = self._buffers(c, W * cap, True)
                 csr = self._csr(data, c, data.perm, self.boff)
+                self._launch_pack_csr(bfc, csr, c / T)
+            else:
+                self._launch_pack_csr(None, None, 0.0)
+            dp.communicate_csr()
+            if c:
                 self.accum_train.zero_()
                 self._launch_fwd_bwd(bfc, csr, True, beta, p_drop, None)
-                self._launch_pack(bfc, csr, c / T)
+                self._launch_pack_grads(bfc, c / T)
                 sums = sums + self.accum_train.cpu().numpy() * (c / T)
-            else:
-                self._launch_pack(None, None, 0.0)
-            self._launch_exchange()
+            else:  # no users here: the union batch's plan still runs
+                dp.merge_plan()
+                self._launch_pack_grads(None, 0.0)
+            dp.communicate_grads()
             self._launch_dp_update(bf, c)
             self.host_step += 1
         self.flush()
@@ -834,8 +862,9 @@ class FusedTrainer:
         return {"total_loss": tot[0] / n_steps, "recon_loss": tot[1] / n_steps, "kl_loss": tot[2] / n_steps}
 
     def _capture(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float, key):
-        """One graph per step (single GPU); data-parallel: forward/backward + pack, then merge + clip + Adam,
-        with the collectives launched eagerly in between (they stay out of the graphs)."""
+        """One graph per step (single GPU); data-parallel: the CSR packet | forward/backward (the union plan
+        beside it) + the gradient packet | union apply + clip + Adam, with the collectives launched eagerly in
+        between (they stay out of the graphs)."""
         csr = self._csr(data, bf.B, data.perm, self.boff)
         bf.csr_keepalive = csr
         torch.cuda.synchronize(self.device)
@@ -843,15 +872,18 @@ class FusedTrainer:
         if self.dp is None or not train:
             with torch.cuda.graph(g):
                 self._launch(bf, csr, train, beta, p_drop, advance=bf.B)
-            bf.graph_up = None
+            bf.graph_pre = bf.graph_up = None
         else:
+            g0 = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g0):
+                self._launch_pack_csr(bf, csr, key[-1])
             with torch.cuda.graph(g):
                 self._launch_fwd_bwd(bf, csr, train, beta, p_drop, None)
-                self._launch_pack(bf, csr, key[-1])
+                self._launch_pack_grads(bf, key[-1])
             g2 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g2):
                 self._launch_dp_update(bf, bf.B)
-            bf.graph_up = g2
+            bf.graph_pre, bf.graph_up = g0, g2
         bf.graph = g
         bf.graph_key = key
         bf.graph_data = data

@@ -153,6 +153,18 @@ def w1_rowgrad(x: Csr, da: torch.Tensor, rg: RowGradBuffers) -> None:
           "hvae_w1_rowgrad")
 
 
+def w1_rowgrad_plan(x: Csr, rg: RowGradBuffers) -> None:
+    """The plan half of w1_rowgrad (needs the batch only), on the current stream."""
+    check(lib().hvae_w1_rowgrad_plan(x.ref, rg.ref, ptr(rg.ws), rg.ws.numel(),
+                                     torch.cuda.current_stream(rg.rows.device).cuda_stream), "hvae_w1_rowgrad_plan")
+
+
+def w1_rowgrad_apply(da: torch.Tensor, rg: RowGradBuffers) -> None:
+    """The apply half of w1_rowgrad: rows from da over a plan already made."""
+    require_hip(da)
+    check(lib().hvae_w1_rowgrad_apply(ptr(da), da.shape[1], rg.ref, stream_of(da)), "hvae_w1_rowgrad_apply")
+
+
 def rowgrad_to_dense(rg: RowGradBuffers, out: torch.Tensor) -> None:
     """out: zero-filled [N, ld] item-major buffer."""
     check(lib().hvae_rowgrad_to_dense(rg.ref, rg.H, ptr(out), out.stride(0), stream_of(out)),

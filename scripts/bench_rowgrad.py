@@ -1,0 +1,50 @@
+"""Timing of the W1 row-gradient (plan + apply, hvae_w1_rowgrad) for one rank's batch and for the union batch a
+W-rank data-parallel step rebuilds (hvae/dist.py), at the Syn-10M shard's item count.
+
+    python scripts/bench_rowgrad.py [--N 1000000] [--H 512] [--B 4096] [--worlds 1 2 4 8]
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT / "recommendation-system_amd"), str(ROOT / "tests" / "golden")]
+
+import torch  # noqa: E402
+
+from gen import synth_csr  # noqa: E402
+from hvae import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--N", type=int, default=1_000_000)
+    ap.add_argument("--H", type=int, default=512)
+    ap.add_argument("--B", type=int, default=4096)
+    ap.add_argument("--worlds", type=int, nargs="*", default=[1, 2, 4, 8])
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    X = synth_csr(args.B * max(args.worlds), args.N, lam=15.0, seed=0)
+    for W in args.worlds:
+        nb = args.B * W
+        Xb = X[:nb]
+        xd = ops.csr_from_scipy(Xb, dev)
+        da = torch.randn(nb, args.H, device=dev)
+        rg = ops.RowGradBuffers(args.N, args.H, int(Xb.nnz), dev)
+        for _ in range(3):
+            ops.w1_rowgrad(xd, da, rg)
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(args.reps):
+            ops.w1_rowgrad(xd, da, rg)
+        e.record()
+        torch.cuda.synchronize()
+        print(json.dumps({"world": W, "rows": nb, "nnz": int(Xb.nnz), "unique_items": int(rg.n_unique.item()),
+                          "plan_plus_apply_us": round(s.elapsed_time(e) * 1e3 / args.reps, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
