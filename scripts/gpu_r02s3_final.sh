@@ -1,0 +1,21 @@
+# Round-2 final evidence (session 3 tree): every GPU test, smoke, the default bench (Syn-10M shard, bf16, CPU
+# baseline), its rocprofv3 kernel stats and FETCH / WRITE PMC passes, the other bench lines.
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/final3
+mkdir -p $O
+cd $R
+timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 420 python -u bench.py > $O/bench_syn10m.json 2> $O/bench_syn10m.log
+cd /tmp && export TMPDIR=/tmp
+BEN="python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --probe-steps 3"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- $BEN > $O/prof.log 2>&1
+KRX='k_dec4_bf16|k_dec_finalize|k_gemm|k_adam_lazy|k_encoder'
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRX" --output-format csv -d $O/pmc_fetch -o run -- $BEN > $O/pmc_fetch.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRX" --output-format csv -d $O/pmc_write -o run -- $BEN > $O/pmc_write.log 2>&1
+cd $R
+timeout -k 10 420 python -u bench.py --precision fp8 --steps 60 --warmup 5 --probe-steps 5 --no-cpu-baseline > $O/bench_syn10m_fp8.json 2> $O/bench_syn10m_fp8.log
+timeout -k 10 300 python -u bench.py --workload syn1m --steps 200 --warmup 20 --probe-steps 10 > $O/bench_syn1m.json 2> $O/bench_syn1m.log
+timeout -k 10 300 python -u bench.py --workload syn1m --precision fp8 --steps 200 --warmup 20 --probe-steps 10 --no-cpu-baseline > $O/bench_syn1m_fp8.json 2> $O/bench_syn1m_fp8.log
+timeout -k 10 300 python -u bench.py --workload all_beauty --steps 300 --warmup 30 --probe-steps 20 > $O/bench_all_beauty.json 2> $O/bench_all_beauty.log
