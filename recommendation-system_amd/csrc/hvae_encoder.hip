@@ -857,8 +857,12 @@ __global__ void __launch_bounds__(256) k_rg_sort(const int32_t* __restrict__ n_u
 // chunks give ~2K waves): one wave per chunk, lane i
 // holds contribution i of the chunk, NV float4 columns per lane. A run of one
 // segment that is the whole segment is written to its row; a run cut by a chunk
-// edge goes to the chunk's head (run starts the chunk) or tail partial, and
-// k_rg_span adds those up in chunk order. Loads are batched 8 contributions deep.
+// edge goes to the chunk's head (run starts the chunk) or tail partial, stored
+// agent-coherent; the wave then takes a ticket on the segment (fill[s], zero after
+// the plan), and the wave that draws the segment's last ticket adds its chunks'
+// partials up in chunk order (the first chunk's head or tail, then the heads) into
+// the row and re-zeroes the ticket -- the same sums in the same order as a separate
+// pass would, in one launch. Loads are batched 8 contributions deep.
 template <int NV>
 __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_unique,
                                                   const int32_t* __restrict__ seg_off,
@@ -866,7 +870,8 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
                                                   const float* __restrict__ contrib_val,
                                                   const int32_t* __restrict__ contrib_slot,
                                                   const float* __restrict__ da, int64_t H, int CH,
-                                                  float* __restrict__ out_rows, float* __restrict__ part) {
+                                                  float* __restrict__ out_rows, float* __restrict__ part,
+                                                  int32_t* __restrict__ ticket) {
   const int nu = *n_unique;
   const int total = seg_off[nu];
   const int nchunks = (total + CH - 1) / CH;
@@ -907,16 +912,49 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
         }
         if (i == n - 1 || snext != si) {  // end of a run (wave-uniform)
           const int lo = c0 + run_lo, hi = c0 + i + 1;
-          float* dst;
-          if (lo == seg_off[si] && hi == seg_off[si + 1]) dst = out_rows + (int64_t)si * H;
-          else if (run_lo == 0) dst = part + (int64_t)(2 * c) * H;
-          else dst = part + (int64_t)(2 * c + 1) * H;
+          const int beg = seg_off[si], end = seg_off[si + 1];
+          if (lo == beg && hi == end) {
+            float* dst = out_rows + (int64_t)si * H;
 #pragma unroll
-          for (int k = 0; k < NV; ++k) {
-            const int64_t col = 4 * (int64_t)(lane + 64 * k);
-            if (col < H) *reinterpret_cast<float4*>(dst + col) = acc[k];
-            acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int k = 0; k < NV; ++k) {
+              const int64_t col = 4 * (int64_t)(lane + 64 * k);
+              if (col < H) *reinterpret_cast<float4*>(dst + col) = acc[k];
+            }
+          } else {
+            float* dst = part + (int64_t)(run_lo == 0 ? 2 * c : 2 * c + 1) * H;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+              const int64_t col = 4 * (int64_t)(lane + 64 * k);
+              if (col < H) {
+                st_shared_f(dst + col, acc[k].x); st_shared_f(dst + col + 1, acc[k].y);
+                st_shared_f(dst + col + 2, acc[k].z); st_shared_f(dst + col + 3, acc[k].w);
+              }
+            }
+            __builtin_amdgcn_s_waitcnt(0);  // this wave's partial has reached the coherence point
+            const int ca = beg / CH, cb = (end - 1) / CH;
+            int tk = 0;
+            if (lane == 0) tk = __hip_atomic_fetch_add(ticket + si, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tk = __shfl(tk, 0, 64);
+            if (tk == cb - ca) {  // the segment's last chunk to finish: its partials, in chunk order
+              const float* first = part + (int64_t)(2 * ca + (beg % CH == 0 ? 0 : 1)) * H;
+#pragma unroll
+              for (int k = 0; k < NV; ++k) {
+                const int64_t col = 4 * (int64_t)(lane + 64 * k);
+                if (col >= H) continue;
+                float4 sum = make_float4(ld_shared_f(first + col), ld_shared_f(first + col + 1),
+                                         ld_shared_f(first + col + 2), ld_shared_f(first + col + 3));
+                for (int cc = ca + 1; cc <= cb; ++cc) {
+                  const float* pc = part + (int64_t)(2 * cc) * H + col;
+                  sum.x += ld_shared_f(pc); sum.y += ld_shared_f(pc + 1);
+                  sum.z += ld_shared_f(pc + 2); sum.w += ld_shared_f(pc + 3);
+                }
+                *reinterpret_cast<float4*>(out_rows + (int64_t)si * H + col) = sum;
+              }
+              if (lane == 0) __hip_atomic_store(ticket + si, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
           }
+#pragma unroll
+          for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
           run_lo = i + 1;
         }
       }
@@ -972,30 +1010,6 @@ __global__ void __launch_bounds__(256) k_rg_apply_seg(const int32_t* __restrict_
     for (int k = 0; k < NV; ++k) {
       const int64_t col = 4 * (int64_t)(lane + 64 * k);
       if (col < H) *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + col) = acc[k];
-    }
-  }
-}
-
-// Segments cut by chunk edges: first chunk's partial (head if the segment starts the
-// chunk, else tail) + the head partials of the following chunks, in chunk order.
-__global__ void __launch_bounds__(256) k_rg_span(const int32_t* __restrict__ n_unique,
-                                                 const int32_t* __restrict__ seg_off, int64_t H, int CH,
-                                                 const float* __restrict__ part, float* __restrict__ out_rows) {
-  const int nu = *n_unique;
-  const int lane = threadIdx.x & 63;
-  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
-  for (int s = gw; s < nu; s += nw) {
-    const int beg = seg_off[s], end = seg_off[s + 1];
-    const int ca = beg / CH, cb = (end - 1) / CH;
-    if (ca == cb) continue;
-    const float* first = part + (int64_t)(2 * ca + (beg % CH == 0 ? 0 : 1)) * H;
-    for (int64_t col = 4 * lane; col < H; col += 256) {
-      float4 acc = *reinterpret_cast<const float4*>(first + col);
-      for (int c = ca + 1; c <= cb; ++c) {
-        const float4 p = *reinterpret_cast<const float4*>(part + (int64_t)(2 * c) * H + col);
-        acc.x += p.x; acc.y += p.y; acc.z += p.z; acc.w += p.w;
-      }
-      *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + col) = acc;
     }
   }
 }
@@ -1226,10 +1240,8 @@ extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowg
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(rg->cap, ch), 4), 4096));
   HVAE_NV_DISPATCH(H, (k_rg_apply<NV><<<grid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
                                                             rg->contrib_val, rg->contrib_slot, da, H, ch, rg->rows,
-                                                            rg->part)));
+                                                            rg->part, rg->fill)));
   HVAE_LAUNCH_CHECK("k_rg_apply");
-  k_rg_span<<<rg_grid(rg), 256, 0, st>>>(rg->n_unique, rg->seg_off, H, ch, rg->part, rg->rows);
-  HVAE_LAUNCH_CHECK("k_rg_span");
   return HVAE_OK;
 }
 

@@ -30,7 +30,9 @@ def _maxrel(a, b):
 
 # ------------------------------------------------------------------ GEMM ---
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (7, 13, 5), (64, 64, 64), (130, 67, 300), (37, 384, 4096),
-                                   (384, 384, 4096), (4096, 128, 512)])
+                                   (384, 384, 4096), (4096, 128, 512),
+                                   # weight-gradient fast path (trans_a, K >= 1024): 32- and 64-square tiles
+                                   (768, 768, 4096), (256, 64, 2048)])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 def test_gemm_f32(ops, hip_device, M, N, K, ta, tb):
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
@@ -80,7 +82,7 @@ def test_gemm_tn_bias_rowsum(ops, hip_device, M, N, K):
 
 
 @pytest.mark.parametrize("B,M,N,Kx", [(64, 384, 384, 384), (4096, 256, 512, 256), (64, 384, 128, 384),
-                                     (50, 70, 33, 45)])
+                                     (50, 70, 33, 45), (4096, 768, 768, 768), (2048, 768, 128, 768)])
 def test_gemm_pair_equals_two_launches(ops, hip_device, B, M, N, Kx):
     """hvae_gemm_f32_pair (dW = dY^T X with the bias gradient, and dX = dY W in one launch) is bitwise the
     two hvae_gemm_f32 launches it replaces, including split-K on the weight gradient at large B."""
