@@ -24,6 +24,8 @@
 // and left to the caller's exact path.
 #include <climits>
 
+#include <cstdlib>
+
 #include "hvae_common.h"
 
 namespace hvae {
@@ -68,6 +70,7 @@ struct TkScanArgs {
   int nseg;            // segments per user: splits * 8 (wave_users 0) or splits * 2 (wave_users 1)
   int wave_users;      // 1: a block's 4 waves take 4 user groups over the same tiles (E read once per block
                        // from L2, the repeats served by the CU's L1); 0: one user group, waves split the tiles
+  int tau_mask;        // other waves' bounds are read every tau_mask + 1 tiles (a power of two minus one)
 };
 
 __device__ __forceinline__ int tk_ku(const TkScanArgs& a, int64_t r) {
@@ -229,12 +232,15 @@ struct TkSelect {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the h == 0 lane's writes land before the pair reads
     const float root = ku > 0 ? hp[0] : -INFINITY;
+    // a tighter own bound is published without waiting for the atomic's return; other waves' bounds are read
+    // every tau_mask + 1 tiles (a returned atomic holds the wave for a device round trip). A stale bound only
+    // loosens the filter, so neither needs ordering.
     if (live && root - eps > tau) {
       tau = root - eps;
-      tau = fmaxf(tau, tk_unord(atomicMax(a.g_tau + user, tk_ord(tau))));
-    } else if ((j & 7) == 7 && live) {
-      tau = fmaxf(tau, tk_unord(atomicMax(a.g_tau + user, INT_MIN)));  // other waves' bounds
+      __hip_atomic_fetch_max(a.g_tau + user, tk_ord(tau), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (live && (j & a.tau_mask) == a.tau_mask)
+      tau = fmaxf(tau, tk_unord(atomicMax(a.g_tau + user, INT_MIN)));  // other waves' bounds
     if (live) {
       const float thr = tau - eps;
 #pragma unroll
@@ -590,6 +596,14 @@ extern "C" size_t hvae_topk_fused_workspace(int64_t R, int64_t N, int64_t D, int
   return 256 + (size_t)R * 8 + (size_t)R * nseg * 4 + (size_t)R * nseg * kTkSegCap * 4 + (size_t)R * kTkSeed * 4;
 }
 
+// HVAE_TK_TAU_PERIOD (A/B, read at every call; a power of two): tiles between reads of the other waves' bounds
+static int tk_tau_mask() {
+  const char* e = std::getenv("HVAE_TK_TAU_PERIOD");
+  int p = e ? std::atoi(e) : 8;
+  if (p < 1 || (p & (p - 1)) != 0) p = 8;
+  return p - 1;
+}
+
 extern "C" int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, const float* E32,
                                const float* e32_maxnorm, int64_t N, int64_t D, const hvae_csr_batch* exclude,
                                int64_t R, int64_t K, int32_t* idx, float* val, int32_t* flag, void* ws,
@@ -618,7 +632,7 @@ extern "C" int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, 
   TkScanArgs sa{U, ldu, static_cast<const bf16_t*>(E_bf16), e32_maxnorm, R, N,
                 exclude ? exclude->row_ptr : nullptr, exclude ? exclude->rows : nullptr,
                 exclude ? exclude->rows_offset : nullptr, (int)K, splits, cdiv(cdiv(N, 32), splits), g_tau, g_eps,
-                seed, cand, cnt, nseg, wu};
+                seed, cand, cnt, nseg, wu, tk_tau_mask()};
   const int64_t ntiles = cdiv(N, 32);
   const int nsample = (int)std::min<int64_t>(ntiles, kTkSeedTiles);
   const int64_t stride = std::max<int64_t>(1, ntiles / nsample);

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--neg99-users", type=int, default=4096)
     ap.add_argument("--skip-matrix", action="store_true")
+    ap.add_argument("--probes", nargs="*", default=None, help="only these score arms (topk_fused, ...)")
     args = ap.parse_args()
     from gen import synth_csr
     from hvae import ops
@@ -83,6 +84,8 @@ def main():
 
     arms = [("topk_fused", run_fused), ("topk_fused_global_scan", run_fused_global)] + \
         ([] if args.skip_matrix else [("topk_matrix", run_matrix)])
+    if args.probes:
+        arms = [a for a in arms if a[0] in args.probes]
     res = {}
     rows = [batch_rows() for _ in range(args.reps)]  # the same batches for every arm
     for name, fn in arms:
