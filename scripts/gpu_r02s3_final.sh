@@ -2,7 +2,7 @@
 # baseline), its rocprofv3 kernel stats and FETCH / WRITE PMC passes, the other bench lines.
 set -e
 R=$GRAFT_REPO_ROOT
-O=$R/gpurun_out/final3
+O=$R/gpurun_out/${FINAL_DIR:-final3}
 mkdir -p $O
 cd $R
 timeout -k 10 700 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
