@@ -1198,6 +1198,15 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
 // NW waves per block = NW / 2 user groups x 2 D halves (NW = 8: two waves per SIMD, <= 256 registers each --
 // d = 384, where u over all of D takes 96 VGPRs and O's half 96 AGPRs). A D half that is not a whole number of
 // 128-column segments (d = 384) owns every other 32-column d-block instead (block 2 db + dh).
+// GEMM1's MFMA row block b (rows 4 b .. 4 b + 3 of the 16x16x32 A operand, lanes c16 = 4 b ..) reads own-item
+// block dec4_rowblk(b) = 0, 2, 3, 1 of the tile half. In the image's chunk XOR (d2_off) the natural order puts
+// the two 4-row blocks of each ds_read_b128 lane group on the same banks (2-way: SQ_LDS_BANK_CONFLICT 0.33 of
+// the sweep's LDS cycles); with this map every group's 16 lanes read 16 distinct 16-B bank slots.
+#ifndef DEC4_ROWMAP
+#define DEC4_ROWMAP 0x1320
+#endif
+__host__ __device__ constexpr int dec4_rowblk(int b) { return (DEC4_ROWMAP >> (4 * b)) & 3; }
+
 __host__ __device__ constexpr int d4_lds_bytes(int D, int NW) {
   return 3 * ((D / 128) * 8192) + 2 * (NW / 2) * 32 * 80 + NW * 64 * 4;
 }
@@ -1224,7 +1233,8 @@ __global__ void __launch_bounds__(64 * NW) k_dec4_bf16(const float* __restrict__
   float* xm = reinterpret_cast<float*>(lds + NS * TB + 2 * NUG * 32 * PST);  // [NW w][64]: max / sum exchange
 
   const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
-  const int c16 = lane & 15, g = lane >> 4;  // GEMM1 layout: users c16 + 16 nb, items 4 g .. 4 g + 3
+  // GEMM1 layout: users c16 + 16 nb; MFMA rows 4 g .. 4 g + 3 are own items 4 gi .. 4 gi + 3 (row map below)
+  const int c16 = lane & 15, g = lane >> 4, gi = dec4_rowblk(g);
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ug = w & (NUG - 1), dh = w / NUG, pw = w ^ NUG;
   const int split = blockIdx.x % splits;
@@ -1299,8 +1309,9 @@ __global__ void __launch_bounds__(64 * NW) k_dec4_bf16(const float* __restrict__
     asm volatile("" ::: "memory");
   };
 
-  // GEMM1: S^T[16 own items][32 users] over all of D; A = image rows 16 dh + c16, chunk 4 ks + g
-  const int r1 = 16 * dh + c16;
+  // GEMM1: S^T[16 own items][32 users] over all of D; A = image row 16 dh + 4 dec4_rowblk(c16 >> 2) + (c16 & 3),
+  // chunk 4 ks + g
+  const int r1 = 16 * dh + 4 * dec4_rowblk(c16 >> 2) + (c16 & 3);
   const int laneA = ((r1 >> 3) << 11) + ((r1 & 7) << 6) + ((g ^ ((r1 >> 2) & 3)) << 4);
   auto gemm1 = [&](const unsigned char* buf, f32x4 (&s)[2], auto&& fill) {
 #pragma unroll
@@ -1370,16 +1381,16 @@ __global__ void __launch_bounds__(64 * NW) k_dec4_bf16(const float* __restrict__
     }
   };
   // P rows: pbuf[par][ug][user][PST]; own half at k-step dh; lane's items 4 g .. 4 g + 3 -> positions
-  // 16 dh + 8 (g & 1) + 4 (g >> 1)
+  // 16 dh + 8 (gi & 1) + 4 (gi >> 1)
   auto p_row = [&](int par, int uu) { return pbuf + ((par * NUG + ug) * 32 + uu) * PST; };
-  const int ppos = 2 * (16 * dh + 8 * (g & 1) + 4 * (g >> 1));
+  const int ppos = 2 * (16 * dh + 8 * (gi & 1) + 4 * (gi >> 1));
 
   float m[2] = {0.f, 0.f}, mL[2] = {0.f, 0.f}, lsum[2] = {0.f, 0.f};
   f32x4 s_nx[2];
   // tail: own items 16 dh + 4 g + i of tile t past N leave the softmax
   auto mask_tail = [&](f32x4 (&s)[2], int64_t t) {
     if (t == ntiles - 1 && (N % kBfTI) != 0) {
-      const int lim = (int)(N - t * kBfTI) - 16 * dh - 4 * g;
+      const int lim = (int)(N - t * kBfTI) - 16 * dh - 4 * gi;
 #pragma unroll
       for (int n2 = 0; n2 < 2; ++n2)
 #pragma unroll

@@ -25,3 +25,24 @@ def test_gemm2_item_map_covers_the_tile():
     """Element j of lane half h of the GEMM2 operand covers each of the 64 items of a tile exactly once."""
     items = sorted(fb.f8_item_of(h, j) for h in range(2) for j in range(32))
     assert items == list(range(64))
+
+
+def test_dec4_bf16_reads_conflict_free():
+    """bf16 version-4 sweep (k_dec4_bf16, d = 768): with DEC4_ROWMAP's row map GEMM1's ds_read_b128, GEMM2's
+    ds_read_b64_tr_b16 and the P reads all hit distinct banks; the natural row order was 2-way on GEMM1
+    (SQ_LDS_BANK_CONFLICT 8.3e8 -> 6.4e7 per launch on MI355X, profiles/r02s3_pmc_dec4_lds.txt)."""
+    import check_dec4_banks as db
+    assert db.worst_conflicts(0x1320) == (1, 1, 1)
+    assert db.worst_conflicts(0x3210)[0] == 2
+
+
+def test_dec4_row_map_is_a_permutation():
+    """Each wave half's 16 MFMA rows read 16 distinct own items, and lane block g's S^T rows are the items the
+    kernel's P positions and tail mask assume (4 dec4_rowblk(g) + r)."""
+    import check_dec4_banks as db
+    for dh in range(2):
+        rows, held = db.gemm1_rows(0x1320, dh)
+        assert sorted(rows) == list(range(16 * dh, 16 * dh + 16))
+        assert sorted(i for g in range(4) for i in held[g]) == list(range(16 * dh, 16 * dh + 16))
+        for g in range(4):  # MFMA output row 4 g + r is A row 4 g + r
+            assert held[g] == rows[4 * g: 4 * g + 4]
