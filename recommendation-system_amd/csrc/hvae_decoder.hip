@@ -1188,7 +1188,7 @@ __global__ void __launch_bounds__(256) k_dec3_bf16(const float* __restrict__ U, 
 #define DEC4_DMA 0  // LDS-DMA pieces: 0 = in GEMM1's gaps, 1 = in GEMM2's, 2 = half in each
 #endif
 // timing ablations (A/B builds only, results invalid): 1 = no LDS-DMA / vmcnt waits in the loop,
-// 2 = no barrier in the loop, 3 = no exponentials / P stores
+// 2 = no barrier in the loop, 3 = no exponentials / P stores, 4 = LDS-DMA issued but never waited for in the loop
 #ifndef DEC4_ABL
 #define DEC4_ABL 0
 #endif
@@ -1439,7 +1439,7 @@ __global__ void __launch_bounds__(64 * NW) k_dec4_bf16(const float* __restrict__
     const int li = (int)(t - t_beg);
     const int cur = li % NS, nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
     // [t]: tile t + 1 has landed, P(t) halves are published (the xm reads of the prologue are done)
-    if (DEC4_ABL != 1) wait_vmcnt<0>();
+    if (DEC4_ABL != 1 && DEC4_ABL != 4) wait_vmcnt<0>();
     if (DEC4_ABL != 2) barrier();
     const int64_t t_dma = min(t + 2, t_end - 1);
     const uint32_t soff_dma = tile_soff(t_dma);

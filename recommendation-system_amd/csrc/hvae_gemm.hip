@@ -357,10 +357,13 @@ __device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned
 // operands with ld % 4 == 0 -- the batch GEMMs of the train step at B = 4096 or 64): no bounds checks,
 // one barrier per 32-deep k stage, the next stage's global loads in flight under the current stage's
 // MFMAs, and 128-bit fragment reads. Both operands are staged into the same LDS image whatever their
-// memory order: [8 k-chunks][R rows (+4 pad)][4 k], so a lane (row r, k-group q) reads four consecutive
-// k of its row with one ds_read_b128 (16 lanes read 256 contiguous bytes: conflict-free). k-contiguous
-// sources ([r][k]) are copied 16 B at a time; r-contiguous ones ([k][r]) are transposed in the store
-// (4 ds_write_b32 per float4).
+// memory order: [8 k-chunks][R rows][4 k], so a lane (row r, k-group q) reads four consecutive k of its
+// row with one ds_read_b128. k-contiguous sources ([r][k]) are copied 16 B at a time; r-contiguous ones
+// ([k][r], the fast path's operands) are transposed in the store (4 ds_write_b32 per float4).
+// Banks (scripts/check_gemm_banks.py): a chunk stride of R rows (a multiple of 16 float4) keeps the q = 1
+// lanes of each ds_read_b128 lane group ({0-3, 12-15, 20-27}, ...) off the q = 0 lanes' banks, and row r
+// sits in slot r ^ ((r >> 3) & 3) of its chunk, so the four rows a store lane holds land on 16 distinct
+// banks across a 16-row half-wave. FAST_LAYOUT 0 is the first image (R + 4 stride, no swizzle).
 // MFMA order: the 16x16x4 MFMA (s) of 16-k group j sums k = 16 j + 4 q + s over the lane groups q,
 // so the four k of a lane's float4 feed four consecutive MFMAs. Each k still enters the accumulator
 // exactly once, in a fixed order (deterministic, exact fp32 products and fp32 accumulation).
@@ -368,9 +371,13 @@ constexpr int FBK = 32;
 #ifndef FAST_PREFETCH
 #define FAST_PREFETCH 4  // k stages of global loads in flight per thread
 #endif
+#ifndef FAST_LAYOUT
+#define FAST_LAYOUT 1
+#endif
 template <int R>
 struct FImg {
-  static constexpr int CS = R + 4;             // float4 slots per k-chunk (pad: the 8 chunks' stores spread)
+  static constexpr int CS = FAST_LAYOUT ? R : R + 4;  // float4 slots per k-chunk
+  static __device__ __forceinline__ int slot(int r) { return FAST_LAYOUT ? r ^ ((r >> 3) & 3) : r; }
   static constexpr int F4 = (FBK / 4) * CS;    // float4 slots per image
   static constexpr int LD = R * FBK / 4 / 256; // float4 global loads per thread per stage
   static_assert(R * FBK / 4 % 256 == 0, "tile rows x 32 must be a multiple of 1024 floats");
@@ -402,14 +409,14 @@ __device__ __forceinline__ void fast_lstore(float4* __restrict__ img, const floa
     const int f = t + 256 * i;
     if (KC) {
       const int r = f >> 3, c = f & 7;
-      img[c * FImg<R>::CS + r] = v[i];
+      img[c * FImg<R>::CS + FImg<R>::slot(r)] = v[i];
     } else {
       const int k = f / (R / 4), r4 = f % (R / 4);
-      float* d = reinterpret_cast<float*>(img + (k >> 2) * FImg<R>::CS + 4 * r4) + (k & 3);
-      d[0] = v[i].x;
-      d[4] = v[i].y;
-      d[8] = v[i].z;
-      d[12] = v[i].w;
+      float* d = reinterpret_cast<float*>(img + (k >> 2) * FImg<R>::CS) + (k & 3);
+      d[4 * FImg<R>::slot(4 * r4)] = v[i].x;
+      d[4 * FImg<R>::slot(4 * r4 + 1)] = v[i].y;
+      d[4 * FImg<R>::slot(4 * r4 + 2)] = v[i].z;
+      d[4 * FImg<R>::slot(4 * r4 + 3)] = v[i].w;
     }
   }
 }
@@ -456,12 +463,12 @@ __device__ __forceinline__ void gemm_fast_block(const GemmP& g, unsigned bx, uns
     else fast_lstore<false, BN>(sB[buf], xb);
   };
   auto compute = [&](int buf) {
-    const float4* a_ = sA[buf] + wm + c16;
-    const float4* b_ = sB[buf] + wn + c16;
+    const float4* a_ = sA[buf];
+    const float4* b_ = sB[buf];
     if (do_rowsum && t < BM) {
 #pragma unroll
       for (int c = 0; c < FBK / 4; ++c) {
-        const float4 x = sA[buf][c * IA::CS + t];
+        const float4 x = sA[buf][c * IA::CS + IA::slot(t)];
         rowsum += x.x;
         rowsum += x.y;
         rowsum += x.z;
@@ -472,9 +479,9 @@ __device__ __forceinline__ void gemm_fast_block(const GemmP& g, unsigned bx, uns
     for (int j = 0; j < FBK / 16; ++j) {
       float4 af[IM], bfr[JN];
 #pragma unroll
-      for (int i = 0; i < IM; ++i) af[i] = a_[(4 * j + q) * IA::CS + 16 * i];
+      for (int i = 0; i < IM; ++i) af[i] = a_[(4 * j + q) * IA::CS + IA::slot(wm + c16 + 16 * i)];
 #pragma unroll
-      for (int n = 0; n < JN; ++n) bfr[n] = b_[(4 * j + q) * IB::CS + 16 * n];
+      for (int n = 0; n < JN; ++n) bfr[n] = b_[(4 * j + q) * IB::CS + IB::slot(wn + c16 + 16 * n)];
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll

@@ -46,3 +46,15 @@ def test_dec4_row_map_is_a_permutation():
         assert sorted(i for g in range(4) for i in held[g]) == list(range(16 * dh, 16 * dh + 16))
         for g in range(4):  # MFMA output row 4 g + r is A row 4 g + r
             assert held[g] == rows[4 * g: 4 * g + 4]
+
+
+@pytest.mark.parametrize("R", [32, 64])
+def test_gemm_fast_image(R):
+    """f32 GEMM fast path (hvae_gemm.hip FImg, FAST_LAYOUT 1): every (k, row) slot of a stage is stored once,
+    the fragment reads are conflict-free and the transposing stores at most 2-way (the first image: 2-way reads,
+    4- and 8-way stores)."""
+    import check_gemm_banks as gb
+    assert gb.covers(R, 1)
+    st, rd = gb.worst_conflicts(R, 1)
+    assert rd == 1 and st <= 2
+    assert gb.worst_conflicts(R, 0) == ((4, 2) if R == 32 else (8, 2))
