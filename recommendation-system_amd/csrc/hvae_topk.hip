@@ -34,6 +34,9 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 constexpr int kTkHeap = 256;    // per-user heap capacity (K_u <= 256)
+// LDS heaps of one wave's 32 users sit cap + 1 floats apart, so that the same slot of every user's heap is on a
+// different bank (a stride of cap floats put the 32 lanes' root reads on one bank: 32-way conflicts every tile)
+constexpr int kTkHeapPad = 1;
 constexpr int kTkSegCap = 256;  // candidates per (user, wave instance, lane half)
 constexpr int kTkMaxCand = 4096;
 constexpr int kTkMaxSeen = 2048;
@@ -275,7 +278,8 @@ __global__ void __launch_bounds__(256) k_topk_scan(TkScanArgs a) {
   const int ku = live ? min(tk_ku(a, user), kTkHeap) : 0;  // K_u > kTkHeap: flagged by k_topk_select
   const float eps = sc.eps;
 
-  TkSelect sel(a, heap_lds + (size_t)(w * 32 + (lane & 31)) * kTkHeap, kTkHeap, user, live, h, eps, ku, sgw);
+  TkSelect sel(a, heap_lds + (size_t)(w * 32 + (lane & 31)) * (kTkHeap + kTkHeapPad), kTkHeap, user, live, h, eps, ku,
+               sgw);
   for (int64_t j = 0; j < nw; ++j) {
     const int64_t t = t0 + tw + ts * j;
     sel.consume(a, sc.score(a, t), t, j);
@@ -288,7 +292,7 @@ __global__ void __launch_bounds__(256) k_topk_scan(TkScanArgs a) {
 // ---- LDS-staged scan (D a multiple of 128): a block's 4 waves take 4 groups of 32 users over the same tiles;
 // each 32-item E tile arrives once per block by LDS-DMA (three-slot ring, the decoder's image and piece map,
 // one barrier per tile) and the 32x32x16 A operands are ds_read_b128 row reads of it. Per-user heaps of up to
-// kTkHeapL tile maxima (a user with K_u beyond it keeps the seed / other waves' bound, which is still valid).
+// tkl_heap - 1 tile maxima (a user with K_u beyond it keeps the seed / other waves' bound, which is still valid).
 // ring slots and heap capacity per D (LDS: slots x the tile + 4 waves x 32 users x the heap): d = 768 keeps two
 // slots (the next tile's DMA overlaps the current tile's MFMAs) so that K_u up to 64 keeps its heap
 template <int D>
@@ -310,7 +314,7 @@ __device__ __forceinline__ void tk_wait_vmcnt() {
 template <int D>
 __global__ void __launch_bounds__(256) k_topk_scan_lds(TkScanArgs a) {
   constexpr int NSEG = D / 128, TB = NSEG * 8192, PW = NSEG * 8 / 4, NS = tkl_ns<D>(), KS = D / 16;
-  constexpr int HC = tkl_heap<D>();
+  constexpr int HC = tkl_heap<D>() - 1;  // heap capacity = stride: odd, so the 32 users' slots fall on 32 banks
   static_assert(D % 128 == 0 && tkl_lds_bytes<D>() <= 160 * 1024, "k_topk_scan_lds shape");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   float* heaps = reinterpret_cast<float*>(lds + NS * TB);
@@ -638,7 +642,7 @@ extern "C" int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, 
   const int64_t stride = std::max<int64_t>(1, ntiles / nsample);
   const unsigned groups = (unsigned)cdiv(R, 32);  // the seed pass: one block per 32 users
   const unsigned blocks = (unsigned)(cdiv(R, wu ? 128 : 32) * splits);
-  const size_t lds = (size_t)4 * 32 * kTkHeap * 4;
+  const size_t lds = (size_t)4 * 32 * (kTkHeap + kTkHeapPad) * 4;
 #define TK_SCAN_LDS(DD)                                                                                 \
   {                                                                                                       \
     constexpr int DL = DD % 128 == 0 ? DD : 128;                                                          \
