@@ -2924,9 +2924,10 @@ static bool v3_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V3", 
 static bool v4_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V4", 1) != 0; }
 // HVAE_DEC_V4_384=1 runs version 4 with 8 waves at D = 384 (large batches) instead of version 2's DS = 1 sweep
 static bool v4_384(int64_t D, int64_t nb) { return D == 384 && nb > 64 && env_int("HVAE_DEC_V4_384", 0) != 0; }
-// HVAE_DEC_V5=1 runs version 5 (hvae_decoder5.hip: producer / consumer waves, two per SIMD) at D = 768
-// (A/B; read at every plan)
-static bool v5_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V5", 0) != 0; }
+// version 5 (hvae_decoder5.hip: producer / consumer waves, two per SIMD) runs the bf16 sweep at D = 768 since
+// both use the conflict-free GEMM1 row map (2.5 % under version 4 at the Syn-10M shard); HVAE_DEC_V5=0 runs
+// version 4 (A/B; read at every plan)
+static bool v5_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V5", 1) != 0; }
 int dec5_launch(bool with_o, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                 int splits, int64_t tiles_per_split, int64_t blocks, int* flag, float* m, float* l, float* O,
                 float* lse, int direct, hipStream_t st);

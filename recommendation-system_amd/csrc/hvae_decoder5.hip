@@ -29,6 +29,13 @@
 #include "hvae_common.h"
 
 namespace hvae {
+// GEMM1 row map (version 4's DEC4_ROWMAP): MFMA row block b reads own-item block dec5_rowblk(b) of a tile half,
+// which makes every ds_read_b128 lane group of the 16x16x32 A operand conflict-free in the image's chunk XOR
+#ifndef DEC5_ROWMAP
+#define DEC5_ROWMAP 0x1320
+#endif
+__device__ __forceinline__ constexpr int dec5_rowblk(int b) { return (DEC5_ROWMAP >> (4 * b)) & 3; }
+
 namespace dec5 {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -71,7 +78,7 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #define DEC5_G1_AHEAD 2  // GEMM1 A operand k-steps in flight
 #endif
 #ifndef DEC5_DMA_B
-#define DEC5_DMA_B 0  // of each (ug, dh)'s 12 LDS-DMA pieces per tile, how many the consumer wave issues
+#define DEC5_DMA_B 6  // of each (ug, dh)'s 12 LDS-DMA pieces per tile, how many the consumer wave issues
 #endif
 
 constexpr int D = 768;
@@ -170,11 +177,13 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
       v += __shfl_xor(v, 32, 64);
       bound = sqrtf(v) * emax * 1.02f;
     }
-    // GEMM1: S^T[32 items][16 users] over all of D, item halves ih: A = image rows 16 ih + c16, chunk 4 ks + g
+    // GEMM1: S^T[32 items][16 users] over all of D, item halves ih: A = image row 16 ih + 4 dec5_rowblk(c16 >> 2)
+    // + (c16 & 3) (version 4's conflict-free row map), chunk 4 ks + g
     int laneA[2];
+    const int gi = dec5_rowblk(g);  // MFMA rows 4 g .. 4 g + 3 hold items 4 gi .. 4 gi + 3 of each half
 #pragma unroll
     for (int ih = 0; ih < 2; ++ih) {
-      const int r1 = 16 * ih + c16;
+      const int r1 = 16 * ih + 4 * dec5_rowblk(c16 >> 2) + (c16 & 3);
       laneA[ih] = ((r1 >> 3) << 11) + ((r1 & 7) << 6) + ((g ^ ((r1 >> 2) & 3)) << 4);
     }
     auto gemm1 = [&](const unsigned char* buf, f32x4 (&s)[2], auto&& fill) {
@@ -207,7 +216,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
       if (t == ntiles - 1 && (N % kTI) != 0) {
 #pragma unroll
         for (int ih = 0; ih < 2; ++ih) {
-          const int lim = (int)(N - t * kTI) - 16 * ih - 4 * g;
+          const int lim = (int)(N - t * kTI) - 16 * ih - 4 * gi;
 #pragma unroll
           for (int r = 0; r < 4; ++r) s[ih][r] = r >= lim ? -INFINITY : s[ih][r];
         }
@@ -223,7 +232,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
           pv[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_nx[ih][r], kLog2e, -mL));
           lsum += pv[r];
         }
-        *reinterpret_cast<uint2*>(prow + 2 * (16 * ih + 8 * (g & 1) + 4 * (g >> 1))) =
+        *reinterpret_cast<uint2*>(prow + 2 * (16 * ih + 8 * (gi & 1) + 4 * (gi >> 1))) =
             make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
       }
     };

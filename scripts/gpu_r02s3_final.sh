@@ -11,7 +11,7 @@ timeout -k 10 420 python -u bench.py > $O/bench_syn10m.json 2> $O/bench_syn10m.l
 cd /tmp && export TMPDIR=/tmp
 BEN="python3 $R/bench.py --steps 20 --warmup 3 --no-cpu-baseline --probe-steps 3"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- $BEN > $O/prof.log 2>&1
-KRX='k_dec4_bf16|k_dec_finalize|k_gemm|k_adam_lazy|k_encoder'
+KRX='k_dec5_bf16|k_dec4_bf16|k_dec_finalize|k_gemm|k_adam_lazy|k_encoder'
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$KRX" --output-format csv -d $O/pmc_fetch -o run -- $BEN > $O/pmc_fetch.log 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRX" --output-format csv -d $O/pmc_write -o run -- $BEN > $O/pmc_write.log 2>&1
 cd $R
