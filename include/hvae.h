@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define HVAE_ABI_VERSION 1
+#define HVAE_ABI_VERSION 2
 
 enum {
   HVAE_OK = 0,
@@ -186,6 +186,9 @@ typedef struct hvae_epilogue {
                           /* of a Linear alongside its weight gradient dY^T X       */
   const float* aux;       /* REPARAM_BWD: eps [M, N]                                */
   float aux_scale;        /* REPARAM_BWD: KL gradient scale beta / B               */
+  const float* aux_scale_dev; /* REPARAM_BWD: if non-NULL, the device scalar that   */
+                          /* replaces aux_scale (an annealed beta / B written by    */
+                          /* hvae_anneal_beta earlier on the stream)                */
 } hvae_epilogue;
 int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K, float alpha,
                   const float* A, int64_t lda, const float* B, int64_t ldb, float beta, float* C,
@@ -224,10 +227,21 @@ int hvae_reparam_kl_fwd(const float* mu, const float* logvar, int64_t ld, int64_
                         int train, const float* eps_in, uint64_t seed, const int64_t* step_dev,
                         float* z, float* eps_out, float* kl_rows, void* stream);
 /* dmu = dz + kl_scale * mu ; dlv = dz * eps * 0.5 exp(0.5 lv) + kl_scale * 0.5 (exp(lv) - 1)
- * with kl_scale = beta / nb (dz may be NULL: KL-only gradient). */
+ * with kl_scale = beta / nb (dz may be NULL: KL-only gradient); kl_scale_dev (nullable) is a
+ * device scalar that replaces kl_scale (hvae_anneal_beta's out2[1]). */
 int hvae_reparam_kl_bwd(const float* dz, const float* mu, const float* logvar, int64_t ld,
-                        const float* eps, int64_t nb, int64_t L, float kl_scale, int train,
-                        float* dmu, float* dlogvar, int64_t ld_out, void* stream);
+                        const float* eps, int64_t nb, int64_t L, float kl_scale, const float* kl_scale_dev,
+                        int train, float* dmu, float* dlogvar, int64_t ld_out, void* stream);
+/* AnnealedVAE's KL-weight schedule (src/ml/model.py:312-334) on the device, so that an
+ * annealed epoch replays one captured step: with s = *anneal_step,
+ *   beta = s >= anneal_steps ? beta_max : beta_min + (s / anneal_steps) (beta_max - beta_min)
+ * in double, as the reference's Python floats (get_current_beta); out2[0] = (float) beta,
+ * out2[1] = (float)(beta / nb) (the KL gradient scale); then *anneal_step = s + 1
+ * (step_annealing, src/ml/train.py:74-76). One launch per train step, before the kernels
+ * that read out2 (hvae_decoder_train's beta_dev, the REPARAM_BWD epilogue's aux_scale_dev,
+ * hvae_reparam_kl_bwd's kl_scale_dev). */
+int hvae_anneal_beta(int64_t* anneal_step, double beta_min, double beta_max, int64_t anneal_steps, int64_t nb,
+                     float* out2, void* stream);
 
 /* -------------------------------------------------- decoder (K7, K8, K10) -- */
 /* Streaming decoder over all N items, scores never stored:
@@ -268,11 +282,13 @@ int hvae_row_norm_max(int dtype, const void* E, int64_t N, int64_t D, float* out
  * loss and of d(u) against the fp32 E32 (see hvae_decoder_bwd). nb = x->nb,
  * N = x->n_items. O may be NULL (kept internal); dU NULL => loss only.
  * If loss3 != NULL the last finalize block also does hvae_loss_finalize
- * (recon_rows, kl_rows, beta -> loss3, accum3) with the same arithmetic. */
+ * (recon_rows, kl_rows, beta -> loss3, accum3) with the same arithmetic; beta_dev
+ * (nullable) is a device scalar that replaces beta (hvae_anneal_beta's out2[0]). */
 int hvae_decoder_train(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                        const float* E32, const hvae_csr_batch* x, int64_t D, float grad_scale, float* lse,
-                       float* O, float* recon_rows, float* dU, const float* kl_rows, float beta, float* loss3,
-                       double* accum3, void* ws, size_t ws_bytes, void* stream);
+                       float* O, float* recon_rows, float* dU, const float* kl_rows, float beta,
+                       const float* beta_dev, float* loss3, double* accum3, void* ws, size_t ws_bytes,
+                       void* stream);
 /* Sparse half of the loss and of d(u), in fp32 against the fp32 E:
  *   recon_rows[b] = n_b * lse[b] - sum_{j in row b} x_bj (u_b . E_j),  n_b = sum_j x_bj
  *   dU[b,:]       = grad_scale * (n_b * O[b,:] - sum_{j in row b} x_bj E_j)

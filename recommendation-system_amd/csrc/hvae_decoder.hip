@@ -2564,7 +2564,8 @@ struct FinArgs {
   const int32_t* rows; const int64_t* rows_offset;    // CSR batch (nullable row_ptr => no sparse terms)
   float scale;
   float* lse_out; float* O_out; float* recon_rows; float* dU;
-  const float* kl_rows; float beta; float* loss3; double* accum3; unsigned* ticket;  // fused loss (optional)
+  const float* kl_rows; float beta; const float* beta_dev; float* loss3; double* accum3;  // fused loss (optional)
+  unsigned* ticket;
 };
 
 constexpr int kFinEB = 16;  // CSR entries per batch of the finalize's sparse-term loads
@@ -2769,7 +2770,7 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     }
   }
   if (a.loss3 && last_block_arrives(a.ticket, gridDim.x))
-    loss_block_reduce(a.recon_rows, true, a.kl_rows, a.nb, a.beta, a.loss3, a.accum3);
+    loss_block_reduce(a.recon_rows, true, a.kl_rows, a.nb, a.beta_dev ? *a.beta_dev : a.beta, a.loss3, a.accum3);
 }
 
 // Exact recompute of one user flagged by k_dec_bf16 (its max score sits more
@@ -3256,7 +3257,8 @@ extern "C" size_t hvae_decoder_workspace(int dtype, int64_t nb, int64_t N, int64
 static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                        const float* E32, const hvae_csr_batch* x, int64_t nb, int64_t N, int64_t D, float scale,
                        float* lse, float* O, float* recon_rows, float* dU, const float* kl_rows, float beta,
-                       float* loss3, double* accum3, void* ws, size_t ws_bytes, hipStream_t st) {
+                       const float* beta_dev, float* loss3, double* accum3, void* ws, size_t ws_bytes,
+                       hipStream_t st) {
   HVAE_REQUIRE(dtype == HVAE_BF16 || dtype == HVAE_F32 || dtype == HVAE_FP8, "hvae decoder: bad dtype");
   HVAE_REQUIRE(U && E && lse && N > 0 && D > 0 && ldu >= D, "hvae decoder: bad args");
   HVAE_REQUIRE(dtype == HVAE_F32 || e_maxnorm, "hvae decoder: bf16 / fp8 need e_maxnorm");
@@ -3324,7 +3326,7 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   a.dU = dU;
   if (loss3) {
     HVAE_REQUIRE(x && recon_rows && kl_rows, "hvae_decoder_train: fused loss needs recon_rows and kl_rows");
-    a.kl_rows = kl_rows; a.beta = beta; a.loss3 = loss3; a.accum3 = accum3;
+    a.kl_rows = kl_rows; a.beta = beta; a.beta_dev = beta_dev; a.loss3 = loss3; a.accum3 = accum3;
     if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   }
   ProbeScope probe("decoder_finalize", st);
@@ -3338,17 +3340,17 @@ extern "C" int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const vo
                                 int64_t nb, int64_t N, int64_t D, float* lse, float* O, void* ws,
                                 size_t ws_bytes, void* stream) {
   return decoder_run(dtype, U, ldu, E, e_maxnorm, nullptr, nullptr, nb, N, D, 0.f, lse, O, nullptr, nullptr,
-                     nullptr, 0.f, nullptr, nullptr, ws, ws_bytes, as_stream(stream));
+                     nullptr, 0.f, nullptr, nullptr, nullptr, ws, ws_bytes, as_stream(stream));
 }
 
 extern "C" int hvae_decoder_train(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                                   const float* E32, const hvae_csr_batch* x, int64_t D, float grad_scale,
                                   float* lse, float* O, float* recon_rows, float* dU, const float* kl_rows,
-                                  float beta, float* loss3, double* accum3, void* ws, size_t ws_bytes,
-                                  void* stream) {
+                                  float beta, const float* beta_dev, float* loss3, double* accum3, void* ws,
+                                  size_t ws_bytes, void* stream) {
   HVAE_REQUIRE(x && recon_rows, "hvae_decoder_train: needs the CSR batch and recon_rows");
   return decoder_run(dtype, U, ldu, E, e_maxnorm, E32, x, x->nb, x->n_items, D, grad_scale, lse, O, recon_rows, dU,
-                     kl_rows, beta, loss3, accum3, ws, ws_bytes, as_stream(stream));
+                     kl_rows, beta, beta_dev, loss3, accum3, ws, ws_bytes, as_stream(stream));
 }
 
 extern "C" int hvae_decoder_bwd(const hvae_csr_batch* x, const float* U, int64_t ldu, const float* E32,

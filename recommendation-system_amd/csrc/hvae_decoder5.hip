@@ -80,6 +80,29 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #ifndef DEC5_DMA_B
 #define DEC5_DMA_B 6  // of each (ug, dh)'s 12 LDS-DMA pieces per tile, how many the consumer wave issues
 #endif
+// Timing-ablation builds only (scripts/build_variant5.sh; outputs invalid by construction), a bit mask:
+// 1 no LDS-DMA pieces in the loop (and no vmcnt waits), 2 no per-tile barrier, 4 no exponentials / P out,
+// 8 GEMM1 A operands not re-read from LDS, 16 GEMM2 E^T operands not re-read, 32 no GEMM1 MFMAs,
+// 64 no GEMM2 MFMAs
+#ifndef DEC5_ABL
+#define DEC5_ABL 0
+#endif
+// A/B placement of the LDS-DMA pieces: producer piece i at GEMM1 k-step DEC5_PDMA_AT + 2 i, consumer piece i at
+// GEMM2 MFMA DEC5_CDMA_AT + 2 i
+#ifndef DEC5_PDMA_AT
+#define DEC5_PDMA_AT 1
+#endif
+#ifndef DEC5_CDMA_AT
+#define DEC5_CDMA_AT 0
+#endif
+// DEC5_RSTAGE=1 (A/B): the producer stages its 12 - DEC5_DMA_B pieces of its (ug, dh) through registers (buffer_load_dwordx4
+// to VGPRs one tile ahead, ds_write_b128 into the image after the barrier that frees the slot) instead of LDS-DMA
+#ifndef DEC5_RSTAGE
+#define DEC5_RSTAGE 0
+#endif
+#ifndef DEC5_DMA_BURST
+#define DEC5_DMA_BURST 0  // A/B: each wave issues its pieces back to back at its first DMA slot
+#endif
 
 constexpr int D = 768;
 constexpr int NS = 3;                    // tile slots
@@ -125,16 +148,24 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(E), (short)0, (int)(N * D * 2), 0x00020000);
   const uint32_t ring0 = lds_addr(lds) + (uint32_t)(q * PW * 1024);
+#ifndef DEC5_DMA_NT
+#define DEC5_DMA_NT 0  // A/B: non-temporal cache policy on the LDS-DMA pieces
+#endif
+#if DEC5_DMA_NT
+#define DEC5_POL " nt"
+#else
+#define DEC5_POL ""
+#endif
   auto issue_piece = [&](uint32_t soff, int slot_i, int i, bool fresh) {
     const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
     const int p = q * PW + i;
     const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
     const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
     if (fresh)
-      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen" DEC5_POL " lds"
                    :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
     else
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen" DEC5_POL " lds"
                    :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
   };
   auto tile_soff = [&](int64_t t) {
@@ -203,9 +234,14 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const bf16x8 c0 = a[ks % AH][0], c1 = a[ks % AH][1];
-        if (ks + AH < KS) { a[ks % AH][0] = rdA(0, ks + AH); a[ks % AH][1] = rdA(1, ks + AH); }
-        s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c0, uf[ks], s[0], 0, 0, 0);
-        s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c1, uf[ks], s[1], 0, 0, 0);
+        if (!(DEC5_ABL & 8) && ks + AH < KS) { a[ks % AH][0] = rdA(0, ks + AH); a[ks % AH][1] = rdA(1, ks + AH); }
+        if (!(DEC5_ABL & 32)) {
+          s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c0, uf[ks], s[0], 0, 0, 0);
+          s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c1, uf[ks], s[1], 0, 0, 0);
+        } else {
+          s[0][0] += (float)c0[0] * (float)uf[ks][0];
+          s[1][0] += (float)c1[0] * (float)uf[ks][0];
+        }
         fill(ks);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -236,11 +272,27 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
             make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
       }
     };
+#if DEC5_RSTAGE
+    uint4 stg[PA > 0 ? PA : 1];
+    auto rs_load = [&](int64_t tt, int i) {
+      const int p = q * PW + i;
+      const uint32_t so = tile_soff(tt) + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
+      const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
+      stg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, (int)so, 0));
+    };
+    auto rs_write = [&](int slot_i, int i) {
+      *reinterpret_cast<uint4*>(lds + slot_i * TB + q * PW * 1024 + i * 1024 + lane * 16) = stg[i];
+    };
+#endif
     if (t_beg < t_end) {
       for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg), 0, i, i == 0);
       if (t_beg + 1 < t_end)
         for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg + 1), 1, i, false);
       wait_vmcnt<0>();
+#if DEC5_RSTAGE
+      if (t_beg + 2 < t_end)
+        for (int i = 0; i < PA; ++i) rs_load(t_beg + 2, i);
+#endif
     }
     barrier();  // [P0] tiles t_beg (and t_beg + 1) landed (consumers' pieces too)
     if (t_beg < t_end) {
@@ -259,16 +311,33 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     for (int64_t t = t_beg; t < t_end; ++t) {
       const int li = (int)(t - t_beg);
       const int nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
-      wait_vmcnt<0>();
-      barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
+#if !DEC5_RSTAGE
+      if (!(DEC5_ABL & 1)) wait_vmcnt<0>();
+#endif
+      if (!(DEC5_ABL & 2)) barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
       if (t + 1 < t_end) {
-        const bool dma = t + 2 < t_end;
+        const bool dma = !(DEC5_ABL & 1) && t + 2 < t_end;
+#if DEC5_RSTAGE
+        const bool ld3 = t + 3 < t_end;
+        gemm1(lds + nxt * TB, s_nx, [&](int ks) {
+          if (dma && ks < PA) rs_write(s_dma, ks);  // tile t + 2, loaded one iteration ago
+          if (ld3 && ks >= KS - PA) rs_load(t + 3, ks - (KS - PA));
+        });
+#else
         const uint32_t soff_dma = tile_soff(dma ? t + 2 : t);
         gemm1(lds + nxt * TB, s_nx, [&](int ks) {
-          if (dma && (ks & 1) == 1 && ks / 2 < PA) issue_piece(soff_dma, s_dma, ks / 2, ks == 1);
+#if DEC5_DMA_BURST
+          if (dma && ks == DEC5_PDMA_AT)
+            for (int i = 0; i < PA; ++i) issue_piece(soff_dma, s_dma, i, i == 0);
+#else
+          const int kk = ks - DEC5_PDMA_AT;
+          if (dma && kk >= 0 && (kk & 1) == 0 && kk / 2 < PA) issue_piece(soff_dma, s_dma, kk / 2, kk == 0);
+#endif
         });
+#endif
         mask_tail(s_nx, t + 1);
-        p_out(par ^ 1);
+        if (!(DEC5_ABL & 4)) p_out(par ^ 1);
+        else lsum += s_nx[0][0] + s_nx[1][0];
       }
     }
     wait_vmcnt<0>();
@@ -313,11 +382,14 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
 #pragma unroll
       for (int i = 0; i < 2 * DB; ++i) {
         const std::array<s16x4, 2> c = n[i % BH];
-        if (i + BH < 2 * DB) n[i % BH] = rdT(buf, i + BH);
+        if (!(DEC5_ABL & 16) && i + BH < 2 * DB) n[i % BH] = rdT(buf, i + BH);
         const s16x8 a = {c[0][0], c[0][1], c[0][2], c[0][3], c[1][0], c[1][1], c[1][2], c[1][3]};
-        o[i % DB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
-                                                           __builtin_bit_cast(bf16x8, i < DB ? pf0 : pf1), o[i % DB],
-                                                           0, 0, 0);
+        if (!(DEC5_ABL & 64))
+          o[i % DB] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                             __builtin_bit_cast(bf16x8, i < DB ? pf0 : pf1), o[i % DB],
+                                                             0, 0, 0);
+        else
+          o[i % DB][0] += (float)__builtin_bit_cast(bf16x8, a)[0];
         fill(i);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -339,16 +411,23 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   for (int64_t t = t_beg; t < t_end; ++t) {
     const int li = (int)(t - t_beg);
     const int cur = li % NS, s_dma = (li + 2) % NS, par = li & 1;
-    if constexpr (PB > 0) wait_vmcnt<0>();
-    barrier();  // [L]
+    if constexpr (PB > 0) if (!(DEC5_ABL & 1)) wait_vmcnt<0>();
+    if (!(DEC5_ABL & 2)) barrier();  // [L]
     // P(t) in GEMM2's B layout: user col, positions 8 h .. 8 h + 7 of k-steps 0 and 1
     const uint4 pf0 = *reinterpret_cast<const uint4*>(p_row(par, col) + 16 * h);
     const uint4 pf1 = *reinterpret_cast<const uint4*>(p_row(par, col) + 32 + 16 * h);
-    const bool dma = t + 2 < t_end;
+    const bool dma = !(DEC5_ABL & 1) && t + 2 < t_end;
     const uint32_t soff_dma = tile_soff(dma ? t + 2 : t);
     gemm2(lds + cur * TB, pf0, pf1, [&](int i) {
+      const int ii = i - DEC5_CDMA_AT;
+#if DEC5_DMA_BURST
       if constexpr (PB > 0)
-        if (dma && (i & 1) == 0 && i / 2 < PB) issue_piece(soff_dma, s_dma, PA + i / 2, i == 0);
+        if (dma && ii == 0)
+          for (int k = 0; k < PB; ++k) issue_piece(soff_dma, s_dma, PA + k, k == 0);
+#else
+      if constexpr (PB > 0)
+        if (dma && ii >= 0 && (ii & 1) == 0 && ii / 2 < PB) issue_piece(soff_dma, s_dma, PA + ii / 2, ii == 0);
+#endif
     });
   }
   if constexpr (PB > 0) wait_vmcnt<0>();

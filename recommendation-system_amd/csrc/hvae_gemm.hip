@@ -52,6 +52,7 @@ struct EpiArgs {
   float* opa_rowsum;  // [M]: sum_k op(A)[m, k] (bias gradient alongside dY^T X)
   const float* aux;   // REPARAM_BWD: eps [M, N]
   float aux_scale;    // REPARAM_BWD: beta / B
+  const float* aux_scale_dev;  // REPARAM_BWD: device beta / B (annealed schedule) or NULL
 };
 
 __device__ __forceinline__ float epi_apply(const EpiArgs& ep, int64_t step, int64_t row, int64_t col,
@@ -60,8 +61,9 @@ __device__ __forceinline__ float epi_apply(const EpiArgs& ep, int64_t step, int6
     case HVAE_EPI_REPARAM_BWD: {  // c = dz; same arithmetic as k_reparam_kl_bwd
       const float m = ep.pre_in[row * ldc + col], v = ep.pre_in[row * ldc + N + col];
       const float gz = ep.train ? c * ep.aux[row * N + col] * 0.5f * expf(0.5f * v) : 0.f;
-      C[row * ldc + N + col] = gz + ep.aux_scale * 0.5f * (expf(v) - 1.f);
-      return c + ep.aux_scale * m;
+      const float ks = ep.aux_scale_dev ? *ep.aux_scale_dev : ep.aux_scale;
+      C[row * ldc + N + col] = gz + ks * 0.5f * (expf(v) - 1.f);
+      return c + ks * m;
     }
     case HVAE_EPI_BIAS:
       return c + ep.bias[col];
@@ -709,6 +711,7 @@ static int gemm_setup(int trans_a, int trans_b, int64_t M, int64_t N, int64_t K,
     ep.opa_rowsum = epi->opa_rowsum;
     ep.aux = epi->aux;
     ep.aux_scale = epi->aux_scale;
+    ep.aux_scale_dev = epi->aux_scale_dev;
     HVAE_REQUIRE(ep.kind >= 0 && ep.kind <= HVAE_EPI_REPARAM_BWD, "hvae_gemm_f32: bad epilogue");
     HVAE_REQUIRE(ep.kind != HVAE_EPI_REPARAM_BWD || (ep.pre_in && (ep.aux || !ep.train) && ldc >= 2 * N),
                  "hvae_gemm_f32: REPARAM_BWD needs heads (pre_in), eps (aux) and ldc >= 2N");

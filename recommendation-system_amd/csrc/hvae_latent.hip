@@ -42,10 +42,11 @@ __global__ void __launch_bounds__(256) k_reparam_kl_fwd(const float* __restrict_
 __global__ void k_reparam_kl_bwd(const float* __restrict__ dz, const float* __restrict__ mu,
                                  const float* __restrict__ lv, int64_t ld,
                                  const float* __restrict__ eps, int64_t nb, int64_t L,
-                                 float kl_scale, int train, float* __restrict__ dmu,
-                                 float* __restrict__ dlv, int64_t ldo) {
+                                 float kl_scale_h, const float* __restrict__ kl_scale_dev, int train,
+                                 float* __restrict__ dmu, float* __restrict__ dlv, int64_t ldo) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= nb * L) return;
+  const float kl_scale = kl_scale_dev ? *kl_scale_dev : kl_scale_h;
   const int64_t b = i / L, l = i % L;
   const float m = mu[b * ld + l], v = lv[b * ld + l];
   const float g = dz ? dz[i] : 0.f;
@@ -127,14 +128,37 @@ extern "C" int hvae_reparam_kl_fwd(const float* mu, const float* logvar, int64_t
 }
 
 extern "C" int hvae_reparam_kl_bwd(const float* dz, const float* mu, const float* logvar, int64_t ld,
-                                   const float* eps, int64_t nb, int64_t L, float kl_scale, int train,
-                                   float* dmu, float* dlogvar, int64_t ld_out, void* stream) {
+                                   const float* eps, int64_t nb, int64_t L, float kl_scale,
+                                   const float* kl_scale_dev, int train, float* dmu, float* dlogvar,
+                                   int64_t ld_out, void* stream) {
   HVAE_REQUIRE(mu && logvar && dmu && dlogvar && ld >= L && ld_out >= L, "hvae_reparam_kl_bwd: bad args");
   HVAE_REQUIRE(!(train && dz) || eps, "hvae_reparam_kl_bwd: train backward needs eps");
   if (nb == 0) return HVAE_OK;
   k_reparam_kl_bwd<<<(unsigned)cdiv(nb * L, 256), 256, 0, as_stream(stream)>>>(
-      dz, mu, logvar, ld, eps, nb, L, kl_scale, train, dmu, dlogvar, ld_out);
+      dz, mu, logvar, ld, eps, nb, L, kl_scale, kl_scale_dev, train, dmu, dlogvar, ld_out);
   HVAE_LAUNCH_CHECK("k_reparam_kl_bwd");
+  return HVAE_OK;
+}
+
+// AnnealedVAE.get_current_beta + step_annealing (src/ml/model.py:312-327) for one train step, in double as
+// the reference's Python floats; contraction off so that beta_min + progress * span rounds as Python does
+__global__ void k_anneal_beta(int64_t* __restrict__ anneal_step, double beta_min, double beta_max,
+                              int64_t anneal_steps, int64_t nb, float* __restrict__ out2) {
+#pragma clang fp contract(off)
+  if (threadIdx.x != 0) return;
+  const int64_t s = *anneal_step;
+  const double beta = s >= anneal_steps ? beta_max
+                                        : beta_min + ((double)s / (double)anneal_steps) * (beta_max - beta_min);
+  out2[0] = (float)beta;
+  out2[1] = (float)(beta / (double)nb);
+  *anneal_step = s + 1;
+}
+
+extern "C" int hvae_anneal_beta(int64_t* anneal_step, double beta_min, double beta_max, int64_t anneal_steps,
+                                int64_t nb, float* out2, void* stream) {
+  HVAE_REQUIRE(anneal_step && out2 && nb > 0 && anneal_steps >= 0, "hvae_anneal_beta: bad args");
+  k_anneal_beta<<<1, 64, 0, as_stream(stream)>>>(anneal_step, beta_min, beta_max, anneal_steps, nb, out2);
+  HVAE_LAUNCH_CHECK("k_anneal_beta");
   return HVAE_OK;
 }
 

@@ -19,7 +19,8 @@
 //   k_topk_select      one block per user: exact fp32 rescore of the candidates against fp32 E (the score the
 //                      reference ranks), seen items dropped, bitonic sort by (score desc, item desc) -- the order
 //                      hvae_topk uses -- and the first K out.
-// eps_u = ||u|| max||E|| (2^-8 + 2^-17 + 4 D 2^-24) x 1.02 (bf16 rounding of u and E, fp32 accumulation on both
+// eps_u = ||u|| max||E|| (2^-7 + 2^-16 + 4 D 2^-24) x 1.02 (bf16 rounding of u and E, each off by up to 2^-8
+// relative, so a product by up to 2^-7 + 2^-16; fp32 accumulation on both
 // sides). Users whose candidate lists overflow (or that have fewer than K unseen items, or K_u > 256) are flagged
 // and left to the caller's exact path.
 #include <climits>
@@ -116,7 +117,7 @@ struct TkScorer {
         __builtin_amdgcn_sched_barrier(0);
       }
     usq += __shfl_xor(usq, 32, 64);
-    eps = sqrtf(usq) * (*a.e_maxnorm) * (0x1p-8f + 0x1p-17f + 4.0f * D * 0x1p-24f) * 1.02f;
+    eps = sqrtf(usq) * (*a.e_maxnorm) * (0x1p-7f + 0x1p-16f + 4.0f * D * 0x1p-24f) * 1.02f;
   }
 
   // S~^T of tile t: lane (col = user, h) holds items 32 t + (r & 3) + 8 (r >> 2) + 4 h; past N: -inf
@@ -345,7 +346,7 @@ __global__ void __launch_bounds__(256) k_topk_scan_lds(TkScanArgs a) {
     __builtin_amdgcn_sched_barrier(0);  // a few k-steps' loads in flight, not all (register peak)
   }
   usq += __shfl_xor(usq, 32, 64);
-  const float eps = sqrtf(usq) * emax * (0x1p-8f + 0x1p-17f + 4.0f * D * 0x1p-24f) * 1.02f;
+  const float eps = sqrtf(usq) * emax * (0x1p-7f + 0x1p-16f + 4.0f * D * 0x1p-24f) * 1.02f;
   const int ku = live ? tk_ku(a, user) : 0;
 
   // LDS-DMA (the decoder's version-2 image: 8-row x 32-column subtiles, 2-bit chunk XOR)
@@ -355,8 +356,12 @@ __global__ void __launch_bounds__(256) k_topk_scan_lds(TkScanArgs a) {
     const int row = 8 * pb + ((lane >> 2) & 7);
     vlane[pb] = ((lane >> 2) & 7) * (D * 2) + 64 * (lane >> 5) + 16 * ((lane & 3) ^ ((row >> 2) & 3));
   }
-  const __amdgpu_buffer_rsrc_t rsrc =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.E), (short)0, (int)(a.N * D * 2), 0x00020000);
+  // the resource covers this split's items only (its extent is a 32-bit byte count: a whole E of more than
+  // 2^31 bytes would wrap, and the bounds check would then read real items as zeros); tile offsets are split-relative
+  const int64_t i_end = min(a.N, t1 * 32);
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.E) + t0 * 32 * D, (short)0, (int)(i_end > t0 * 32 ? (i_end - t0 * 32) * D * 2 : 0),
+      0x00020000);
   const uint32_t ring0 = tk_lds_addr(lds) + (uint32_t)(w * PW * 1024);
   auto issue_pieces = [&](uint32_t soff, int slot_i, int i0, int i1, bool fresh) {
     const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
@@ -373,7 +378,9 @@ __global__ void __launch_bounds__(256) k_topk_scan_lds(TkScanArgs a) {
                      :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
     }
   };
-  auto tile_soff = [&](int64_t t) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(32 * D * 2))); };
+  auto tile_soff = [&](int64_t t) {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)((t - t0) * (int64_t)(32 * D * 2)));
+  };
   auto barrier = [&] {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -580,11 +587,15 @@ static int tk_wave_users() {  // HVAE_TOPK_WAVE_USERS=0 selects the tile-split m
   return (v && *v) ? (atoi(v) != 0) : 1;
 }
 
-static int tk_splits(int64_t R, int64_t N, int wave_users) {
+// a split's bf16 slice of E must stay below 2^31 bytes (the LDS scan's buffer resource extent is 32-bit)
+constexpr int64_t kTkSplitBytes = (int64_t)1 << 30;
+
+static int tk_splits(int64_t R, int64_t N, int64_t D, int wave_users) {
   const int64_t groups = std::max<int64_t>(1, cdiv(R, wave_users ? 128 : 32));  // R = 0: a workspace query
   const int64_t tiles = cdiv(N, 32);
   int64_t s = std::max<int64_t>(1, cdiv(256, groups));  // ~256 blocks (one per CU: 128 KiB of heaps each)
   s = std::min<int64_t>(s, std::max<int64_t>(1, tiles / (wave_users ? 4 : 16)));  // >= 4 tiles per wave
+  s = std::max<int64_t>(s, cdiv(tiles * 32 * D * 2, kTkSplitBytes));  // large E: enough splits for the extent
   s = std::min<int64_t>(s, wave_users ? 512 : 128);  // nseg <= 1024
   return (int)s;
 }
@@ -595,7 +606,7 @@ using namespace hvae;
 
 extern "C" size_t hvae_topk_fused_workspace(int64_t R, int64_t N, int64_t D, int64_t K) {
   const int wu = tk_lds_scan(D) ? 1 : tk_wave_users();
-  const int s = tk_splits(R, N, wu);
+  const int s = tk_splits(R, N, D, wu);
   const size_t nseg = (size_t)s * (wu ? 2 : 8);
   return 256 + (size_t)R * 8 + (size_t)R * nseg * 4 + (size_t)R * nseg * kTkSegCap * 4 + (size_t)R * kTkSeed * 4;
 }
@@ -623,8 +634,10 @@ extern "C" int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, 
   hipStream_t st = as_stream(stream);
   const bool lds_scan = tk_lds_scan(D);
   const int wu = lds_scan ? 1 : tk_wave_users();
-  const int splits = tk_splits(R, N, wu);
+  const int splits = tk_splits(R, N, D, wu);
   const int nseg = splits * (wu ? 2 : 8);
+  HVAE_REQUIRE(!lds_scan || cdiv(cdiv(N, 32), splits) * 32 * D * 2 < ((int64_t)1 << 31),
+               "hvae_topk_fused: a split of E exceeds 2^31 bytes");
   unsigned char* p = static_cast<unsigned char*>(ws);
   int* g_tau = reinterpret_cast<int*>(p + 256);
   float* g_eps = reinterpret_cast<float*>(g_tau + R);

@@ -15,6 +15,7 @@ import torch
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("HVAE_LIB", _HERE / "libhvae.so"))
 
+ABI_VERSION = 2  # include/hvae.h HVAE_ABI_VERSION
 HVAE_OK = 0
 HVAE_F32 = 0
 HVAE_BF16 = 1
@@ -59,7 +60,7 @@ class Epilogue(C.Structure):
     _fields_ = [
         ("kind", cint), ("bias", vp), ("pre_out", vp), ("pre_in", vp), ("p_drop", f32),
         ("drop_mult", vp), ("seed", u64), ("step_dev", vp), ("tag", u32), ("train", cint),
-        ("opa_rowsum", vp), ("aux", vp), ("aux_scale", f32),
+        ("opa_rowsum", vp), ("aux", vp), ("aux_scale", f32), ("aux_scale_dev", vp),
     ]
 
 
@@ -105,7 +106,8 @@ SIGNATURES = {
     "hvae_colsum": (cint, [vp, i64, i64, i64, f32, vp, vp, sz, vp]),
     "hvae_colsum_workspace": (sz, [i64, i64]),
     "hvae_reparam_kl_fwd": (cint, [vp, vp, i64, i64, i64, cint, vp, u64, vp, vp, vp, vp, vp]),
-    "hvae_reparam_kl_bwd": (cint, [vp, vp, vp, i64, vp, i64, i64, f32, cint, vp, vp, i64, vp]),
+    "hvae_reparam_kl_bwd": (cint, [vp, vp, vp, i64, vp, i64, i64, f32, vp, cint, vp, vp, i64, vp]),
+    "hvae_anneal_beta": (cint, [vp, f64, f64, i64, i64, vp, vp]),
     "hvae_decoder_image_bytes": (sz, [cint, i64, i64]),
     "hvae_decoder_image": (cint, [cint, vp, i64, i64, vp, vp]),
     "hvae_decoder_fwd": (cint, [cint, vp, i64, vp, vp, i64, i64, i64, vp, vp, vp, sz, vp]),
@@ -114,7 +116,7 @@ SIGNATURES = {
     "hvae_row_norm_max": (cint, [cint, vp, i64, i64, vp, vp]),
     "hvae_decoder_bwd": (cint, [P(CsrBatch), vp, i64, vp, i64, vp, vp, f32, vp, vp, vp]),
     "hvae_decoder_train": (cint, [cint, vp, i64, vp, vp, vp, P(CsrBatch), i64, f32, vp, vp, vp, vp, vp, f32, vp,
-                                  vp, vp, sz, vp]),
+                                  vp, vp, vp, sz, vp]),
     "hvae_nll_rows_fwd": (cint, [vp, i64, vp, i64, i64, i64, vp, vp, vp]),
     "hvae_nll_rows_bwd": (cint, [vp, i64, vp, i64, vp, i64, i64, f32, vp, i64, vp]),
     "hvae_loss_finalize": (cint, [vp, vp, i64, f32, vp, vp, vp]),
@@ -162,8 +164,8 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        if L.hvae_version() != 1:
-            raise RuntimeError(f"libhvae ABI version {L.hvae_version()} != 1")
+        if L.hvae_version() != ABI_VERSION:
+            raise RuntimeError(f"libhvae ABI version {L.hvae_version()} != {ABI_VERSION}")
         _lib = L
     return _lib
 

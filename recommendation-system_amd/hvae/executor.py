@@ -275,6 +275,11 @@ class FusedTrainer:
         self.norm = torch.zeros(1, device=device)
         self.coef = torch.ones(1, device=device)
         self.accum_train = torch.zeros(3, dtype=torch.float64, device=device)
+        # annealed beta (AnnealedVAE): the schedule's step counter and (beta, beta / B) of the current step, both
+        # on the device, so an annealed epoch replays one captured step (hvae_anneal_beta)
+        self.anneal_dev = torch.zeros(1, dtype=torch.int64, device=device)
+        self.beta_dev = torch.zeros(2, device=device)
+        self._anneal = None  # (beta_min, beta_max, anneal_steps) while an annealed train epoch runs
         self.accum_val = torch.zeros(3, dtype=torch.float64, device=device)
         self.host_step = 0
         # ---- frozen embeddings: fp32 (sparse terms, eval) + bf16 copy (decoder MFMA)
@@ -303,6 +308,7 @@ class FusedTrainer:
             raise ValueError(f"precision must be 'bf16', 'fp8' or 'fp32', got {precision!r}")
         self.precision = precision
         self.enorm = ops.row_norm_max(self.E_dec)
+        self._e_version = model.item_embeddings._version
         self._bufs: dict[tuple, _StepBuffers] = {}
         self._views()
         self.dp = None
@@ -369,6 +375,21 @@ class FusedTrainer:
                       "projection_layer.3.bias"):
                 self.P[n] = V(f, n)
                 self.G[n] = V(self.g_small, n, base)
+
+    def sync_embeddings(self):
+        """E is frozen, but load_state_dict / copy_ may still write new values into the module's buffer (a
+        checkpoint of another embedding file): bring the fp32 copy, the decoder image and max||E|| up to date in
+        place, so captured graphs keep their pointers. Cheap when nothing changed (a version compare)."""
+        E = self.model.item_embeddings
+        if E._version == self._e_version and E.data_ptr() == self.E32.data_ptr():
+            return
+        with torch.no_grad():
+            if E.data_ptr() != self.E32.data_ptr():
+                self.E32.copy_(E.detach())
+            if isinstance(self.E_dec, ops.DecoderImage):
+                self.E_dec.refresh(self.E32)
+            ops.row_norm_max(self.E_dec, out=self.enorm)
+        self._e_version = E._version
 
     def grad_of(self, name: str) -> torch.Tensor:
         """Current gradient of a small parameter (after the last step)."""
@@ -474,6 +495,12 @@ class FusedTrainer:
 
         ev_plan = None
         dp = self.dp is not None
+        anneal = self._anneal if train else None
+        beta_dev = None
+        if anneal is not None:  # this step's (beta, beta / B) from the device schedule counter, which it advances
+            beta_dev = self.beta_dev
+            check(L_.hvae_anneal_beta(ptr(self.anneal_dev), anneal[0], anneal[1], anneal[2], B, ptr(beta_dev), st),
+                  "anneal_beta")
         if train and dp:
             # data parallel: no local row gradient; the union batch's plan (from the CSR packets gathered
             # before this forward) runs on the plan stream beside it, its apply after the second exchange. The
@@ -551,8 +578,8 @@ class FusedTrainer:
         # decoder sweep + finalize (split merge, sparse loss terms, du) + the batch loss means, one call
         check(L_.hvae_decoder_train(self.dec_dtype, ptr(bf.u), d, ptr(self.E_dec), ptr(self.enorm), ptr(self.E32),
                                     csr_ref, d, 1.0 / B, ptr(bf.lse), None, ptr(bf.recon_rows),
-                                    ptr(bf.dU) if train else None, ptr(bf.kl_rows), beta, ptr(bf.loss3), ptr(accum),
-                                    ws, wsn, st), "decoder_train")
+                                    ptr(bf.dU) if train else None, ptr(bf.kl_rows), beta, ptr(beta_dev),
+                                    ptr(bf.loss3), ptr(accum), ws, wsn, st), "decoder_train")
         if not train:
             return
         # ----------------------------------------------------- backward ---
@@ -583,13 +610,14 @@ class FusedTrainer:
                       G["projection_layer.3.bias"], (B, d, d, ptr(bf.dU), d, ptr(Wb), d, ptr(bf.dp1), d), epi3)
             # dz = dp1 Wa with the reparameterisation + KL backward as its epilogue -> dheads = [dmu | dlogvar]
             epi_r = Epilogue(_lib.EPI_REPARAM_BWD, None, None, ptr(bf.heads), 0.0, None, 0, None, 0, tr, None,
-                             ptr(bf.eps), beta / B)
+                             ptr(bf.eps), beta / B, ptr(beta_dev[1:]) if beta_dev is not None else None)
             layer_bwd((d, Lt, B, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt),
                       G["projection_layer.0.bias"], (B, Lt, d, ptr(bf.dp1), d, ptr(Wa), Lt, ptr(bf.dheads), 2 * Lt),
                       epi_r)
         else:
             dmu, dlv = bf.dheads, bf.dheads[:, Lt:]
-            check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B, tr,
+            check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B,
+                                         ptr(beta_dev[1:]) if beta_dev is not None else None, tr,
                                          ptr(dmu), ptr(dlv), 2 * Lt, st), "reparam_kl_bwd")
         layer_bwd((2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl), self.gb_heads,
                   (B, Hl, 2 * Lt, ptr(bf.dheads), 2 * Lt, ptr(self.W_heads), Hl, ptr(bf.dh[-1]), Hl))
@@ -679,6 +707,7 @@ class FusedTrainer:
 
         Data parallel (train): every rank calls it together with its own rows; weight = this rank's share of
         the union batch (default 1 / world: equal batches)."""
+        self.sync_embeddings()
         cap = int(data.row_ptr[-1].item()) if rows is None else data.max_batch_nnz(B)
         dp = self.dp if train else None
         if dp is not None:
@@ -703,15 +732,45 @@ class FusedTrainer:
                   max_batches: int | None = None) -> dict:
         """Iterate the dataset in batches (DataLoader semantics: shuffle, drop_last=False).
 
-        beta_fn(step_index) -> beta; a constant beta lets every full batch replay one graph.
+        beta_fn(step_index) -> beta; a constant beta (ConstBeta) or the annealed schedule evaluated on the device
+        (AnnealedBeta) lets every full batch replay one graph.
         Returns the mean of the per-batch losses (VAETrainer.train_epoch's metric).
         """
         n = int(data.users.numel())
         if n == 0:
             return {"total_loss": float("nan"), "recon_loss": float("nan"), "kl_loss": float("nan")}
-        if train and self.dp is not None:
-            return self._run_epoch_dp(data, batch_size, shuffle, beta_fn, p_drop, drop_last, generator,
-                                      max_batches)
+        self.sync_embeddings()
+        anneal = getattr(beta_fn, "anneal", None) if train else None
+        if anneal is not None:
+            self.anneal_dev.fill_(int(beta_fn.model.current_step))
+        self._anneal = anneal
+        try:
+            if train and self.dp is not None:
+                out, steps = self._run_epoch_dp(data, batch_size, shuffle, beta_fn, p_drop, drop_last, generator,
+                                                max_batches)
+            else:
+                out, steps = self._run_epoch_local(data, batch_size, shuffle, beta_fn, p_drop, train, drop_last,
+                                                   generator, max_batches)
+        finally:
+            self._anneal = None
+        if anneal is not None:  # the host mirror of the device schedule counter (AnnealedVAE.step_annealing)
+            beta_fn.model.current_step += steps
+        return out
+
+    @staticmethod
+    def _step_beta(beta_fn, const_beta, anneal, i: int):
+        """The beta argument of step i: the constant, a placeholder when the device schedule supplies it, or
+        beta_fn(i) (a host schedule: eager steps)."""
+        if const_beta is not None:
+            return const_beta
+        return 0.0 if anneal is not None else beta_fn(i)
+
+    def _run_epoch_local(self, data: DeviceData, batch_size: int, shuffle: bool, beta_fn, p_drop: float,
+                         train: bool, drop_last: bool, generator, max_batches) -> tuple[dict, int]:
+        n = int(data.users.numel())
+        if not train and self.dp is not None and data.users_host is not None:
+            return self._run_eval_sharded(data, batch_size, shuffle, beta_fn, p_drop, drop_last, generator,
+                                          max_batches)
         if shuffle:
             order = _sampler_order(n, generator, self.device)
             data.perm.copy_(data.users[order.to(self.device)])
@@ -731,26 +790,74 @@ class FusedTrainer:
             n_full, tail = min(n_full, max_batches), 0
         n_batches = n_full + (1 if tail else 0)
         const_beta = getattr(beta_fn, "constant", None)
+        anneal = self._anneal
         B = batch_size
         for bi in range(n_full):
-            beta = beta_fn(bi)
+            beta = self._step_beta(beta_fn, const_beta, anneal, bi)
             bf = self._buffers(B, data.max_batch_nnz(B), train)
-            if self.use_graphs and const_beta is not None:
-                if not self._replay(bf, data, train, beta, p_drop, bi, (beta, p_drop) + self._hyper()):
+            if self.use_graphs and (const_beta is not None or anneal is not None):
+                if not self._replay(bf, data, train, beta, p_drop, bi, (beta, anneal, p_drop) + self._hyper()):
                     continue
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
             if train:
                 self.host_step += 1
         if tail:
-            beta = beta_fn(n_full)
+            beta = self._step_beta(beta_fn, const_beta, anneal, n_full)
             bf = self._buffers(tail, data.max_batch_nnz(tail), train)
             self._launch(bf, self._csr(data, tail, data.perm, self.boff), train, beta, p_drop, advance=tail)
             if train:
                 self.host_step += 1
         self.flush()
         sums = accum.cpu().tolist()  # the one host sync of the epoch
-        return {"total_loss": sums[0] / n_batches, "recon_loss": sums[1] / n_batches, "kl_loss": sums[2] / n_batches}
+        return ({"total_loss": sums[0] / n_batches, "recon_loss": sums[1] / n_batches,
+                 "kl_loss": sums[2] / n_batches}, n_batches if train else 0)
+
+    def _run_eval_sharded(self, data: DeviceData, B: int, shuffle: bool, beta_fn, p_drop: float, drop_last: bool,
+                          generator, max_batches) -> tuple[dict, int]:
+        """Data-parallel validation (VAETrainer.validate under torchrun): the epoch's batches -- the ones a single
+        GPU would form, in its order -- are dealt round-robin over the ranks (batch i to rank i mod W), each rank
+        runs its own through the same captured eval step, and the per-batch loss sums are all-reduced. Every
+        batch is the single-GPU batch, so the result is the single-GPU validation loss up to the order of the
+        fp64 sum over batches."""
+        dp, W, r = self.dp, self.dp.world, self.dp.rank
+        users = data.users_host
+        n = len(users)
+        order = users[_sampler_order(n, generator, self.device).cpu().numpy()] if shuffle else users
+        n_full, tail = divmod(n, B)
+        if drop_last:
+            tail = 0
+        if max_batches is not None:
+            n_full, tail = min(n_full, max_batches), 0
+        n_batches = n_full + (1 if tail else 0)
+        mine_full = list(range(r, n_full, W))
+        mine_tail = bool(tail) and n_full % W == r
+        parts = [order[i * B:(i + 1) * B] for i in mine_full] + ([order[n_full * B:n_full * B + tail]] if mine_tail
+                                                                   else [])
+        if parts:
+            mine = np.concatenate(parts).astype(np.int32)
+            data.perm[:len(mine)].copy_(torch.as_tensor(mine).to(self.device))
+        self.accum_val.zero_()
+        self.boff.zero_()
+        self.flush()  # the forward reads W1t rows that no catch-up precedes
+        const_beta = getattr(beta_fn, "constant", None)
+        for k, bi in enumerate(mine_full):
+            beta = const_beta if const_beta is not None else beta_fn(bi)
+            bf = self._buffers(B, data.max_batch_nnz(B), False)
+            if self.use_graphs and const_beta is not None:
+                if not self._replay(bf, data, False, beta, p_drop, k, (beta, None, p_drop) + self._hyper()):
+                    continue
+            else:
+                self._launch(bf, self._csr(data, B, data.perm, self.boff), False, beta, p_drop, advance=B)
+        if mine_tail:
+            beta = const_beta if const_beta is not None else beta_fn(n_full)
+            bf = self._buffers(tail, data.max_batch_nnz(tail), False)
+            self._launch(bf, self._csr(data, tail, data.perm, self.boff), False, beta, p_drop, advance=tail)
+        tot = dp.all_reduce(self.accum_val.cpu().numpy())  # the batches' losses summed over the ranks
+        if n_batches == 0:
+            return {"total_loss": float("nan"), "recon_loss": float("nan"), "kl_loss": float("nan")}, 0
+        return {"total_loss": tot[0] / n_batches, "recon_loss": tot[1] / n_batches,
+                "kl_loss": tot[2] / n_batches}, 0
 
     def _replay(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float, bi: int,
                 key) -> bool:
@@ -786,7 +893,7 @@ class FusedTrainer:
         return hit[1]
 
     def _run_epoch_dp(self, data: DeviceData, B: int, shuffle: bool, beta_fn, p_drop: float, drop_last: bool,
-                      generator, max_batches) -> dict:
+                      generator, max_batches) -> tuple[dict, int]:
         """A data-parallel training epoch (hvae/dist.py). data.dp_global: every rank holds every user and takes
         its slice of each global batch of a permutation drawn from the shared seed; otherwise the ranks'
         datasets are their own shards, which must have equal sizes."""
@@ -820,14 +927,16 @@ class FusedTrainer:
         n_steps = n_full + (1 if sum(counts) else 0)
         self._check_steps(n_steps + 1)
         const_beta = getattr(beta_fn, "constant", None)
+        anneal = self._anneal
         cap = self._dp_cap(data, B)
         if n_full:
             dp.plan(B, cap)
         for bi in range(n_full):
-            beta = beta_fn(bi)
+            beta = self._step_beta(beta_fn, const_beta, anneal, bi)
             bf = self._buffers(B, W * cap, True)
-            if self.use_graphs and const_beta is not None:
-                if not self._replay(bf, data, True, beta, p_drop, bi, (beta, p_drop) + self._hyper() + (cap, 1.0 / W)):
+            if self.use_graphs and (const_beta is not None or anneal is not None):
+                if not self._replay(bf, data, True, beta, p_drop, bi,
+                                    (beta, anneal, p_drop) + self._hyper() + (cap, 1.0 / W)):
                     continue
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), True, beta, p_drop, advance=B,
@@ -836,7 +945,7 @@ class FusedTrainer:
         sums = self.accum_train.cpu().numpy() / W  # the union batch's loss = mean of equal shares
         if sum(counts):  # the last, partial global batch: eager, every rank takes part (possibly with no users)
             T, c, Bt = sum(counts), counts[r], max(counts)
-            beta = beta_fn(n_full)
+            beta = self._step_beta(beta_fn, const_beta, anneal, n_full)
             dp.plan(Bt, cap)
             bf = self._buffers(Bt, W * cap, True)
             if c:
@@ -851,15 +960,18 @@ class FusedTrainer:
                 self._launch_fwd_bwd(bfc, csr, True, beta, p_drop, None)
                 self._launch_pack_grads(bfc, c / T)
                 sums = sums + self.accum_train.cpu().numpy() * (c / T)
-            else:  # no users here: the union batch's plan still runs
+            else:  # no users here: the union batch's plan still runs (and the schedule counter advances)
                 dp.merge_plan()
                 self._launch_pack_grads(None, 0.0)
+                if anneal is not None:
+                    ops.counter_add(self.anneal_dev, 1)
             dp.communicate_grads()
             self._launch_dp_update(bf, c)
             self.host_step += 1
         self.flush()
         tot = dp.all_reduce(sums)  # the union batches' losses summed over the steps
-        return {"total_loss": tot[0] / n_steps, "recon_loss": tot[1] / n_steps, "kl_loss": tot[2] / n_steps}
+        return ({"total_loss": tot[0] / n_steps, "recon_loss": tot[1] / n_steps, "kl_loss": tot[2] / n_steps},
+                n_steps)
 
     def _capture(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float, key):
         """One graph per step (single GPU); data-parallel: the CSR packet | forward/backward (the union plan
@@ -899,3 +1011,21 @@ class ConstBeta:
 
     def __call__(self, _i):
         return self.constant
+
+
+class AnnealedBeta:
+    """AnnealedVAE's linear KL-weight schedule (reference src/ml/model.py:312-334) for a fused epoch.
+
+    run_epoch evaluates it on the device (hvae_anneal_beta: one launch per train step that reads and advances a
+    device copy of model.current_step), so annealed epochs replay one captured step like constant-beta ones, and
+    then advances model.current_step by the steps it ran. Called directly (eager steps over other iterables) it is
+    the reference's _compute_loss order: the current beta, then step_annealing()."""
+
+    def __init__(self, model):
+        self.model = model
+        self.anneal = (float(model.beta_min), float(model.beta_max), int(model.anneal_steps))
+
+    def __call__(self, _i):
+        b = self.model.get_current_beta()
+        self.model.step_annealing()
+        return b

@@ -207,9 +207,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor | None = None, alph
 
 
 def epilogue(kind, bias=None, pre_out=None, pre_in=None, p_drop=0.0, drop_mult=None, seed=0, step=None,
-             tag=0, train=False, opa_rowsum=None, aux=None, aux_scale=0.0) -> Epilogue:
+             tag=0, train=False, opa_rowsum=None, aux=None, aux_scale=0.0, aux_scale_dev=None) -> Epilogue:
     return Epilogue(kind, ptr(bias), ptr(pre_out), ptr(pre_in), float(p_drop), ptr(drop_mult), int(seed), ptr(step),
-                    int(tag), int(train), ptr(opa_rowsum), ptr(aux), float(aux_scale))
+                    int(tag), int(train), ptr(opa_rowsum), ptr(aux), float(aux_scale), ptr(aux_scale_dev))
 
 
 def colsum(x: torch.Tensor, out: torch.Tensor | None = None, beta=0.0):
@@ -239,13 +239,13 @@ def reparam_kl_fwd(mu, logvar, train: bool, seed: int, step=None, eps_in=None):
     return z, eps, kl_rows
 
 
-def reparam_kl_bwd(dz, mu, logvar, eps, kl_scale: float, train: bool, dmu=None, dlv=None):
+def reparam_kl_bwd(dz, mu, logvar, eps, kl_scale: float, train: bool, dmu=None, dlv=None, kl_scale_dev=None):
     nb, L = mu.shape
     if dmu is None:
         dmu = torch.empty(nb, L, device=mu.device)
         dlv = torch.empty(nb, L, device=mu.device)
     check(lib().hvae_reparam_kl_bwd(ptr(dz), ptr(mu), ptr(logvar), mu.stride(0), ptr(eps), nb, L, float(kl_scale),
-                                    int(train), ptr(dmu), ptr(dlv), dmu.stride(0), stream_of(mu)),
+                                    ptr(kl_scale_dev), int(train), ptr(dmu), ptr(dlv), dmu.stride(0), stream_of(mu)),
           "hvae_reparam_kl_bwd")
     return dmu, dlv
 
@@ -270,6 +270,15 @@ class DecoderImage:
         self.bf16 = self.buf[: self.N * self.D * 2].view(torch.bfloat16).view(self.N, self.D)
         self.device = E32.device
 
+    def refresh(self, E32: torch.Tensor) -> None:
+        """Rewrite the image from new values of E in place (same shape; captured graphs keep their pointers)."""
+        require_hip(E32)
+        if tuple(E32.shape) != (self.N, self.D):
+            raise ValueError(f"refresh: E shape {tuple(E32.shape)} != image shape {(self.N, self.D)}")
+        E32 = E32.contiguous()
+        check(lib().hvae_decoder_image(self.dtype, ptr(E32), self.N, self.D, ptr(self.buf), stream_of(E32)),
+              "hvae_decoder_image")
+
     def data_ptr(self) -> int:
         return self.buf.data_ptr()
 
@@ -287,12 +296,13 @@ def _dec_operand(E):
     return _lib.HVAE_F32, E.shape[0], E
 
 
-def row_norm_max(E) -> torch.Tensor:
-    """max_i ||E_i|| of an fp32 / bf16 [N, D] matrix or of a DecoderImage's bf16 values (device scalar)."""
+def row_norm_max(E, out: torch.Tensor | None = None) -> torch.Tensor:
+    """max_i ||E_i|| of an fp32 / bf16 [N, D] matrix or of a DecoderImage's bf16 values (device scalar; written
+    into `out` when given)."""
     if isinstance(E, DecoderImage):
         E = E.bf16
     require_hip(E)
-    out = torch.empty(1, device=E.device)
+    out = torch.empty(1, device=E.device) if out is None else out
     dtype = _lib.HVAE_BF16 if E.dtype == torch.bfloat16 else _lib.HVAE_F32
     check(lib().hvae_row_norm_max(dtype, ptr(E), E.shape[0], E.shape[1], ptr(out), stream_of(E)),
           "hvae_row_norm_max")
@@ -353,7 +363,7 @@ def decoder_train(x: Csr, U, E, enorm, E32, grad_scale: float, want_du: bool = T
     ws = workspace(U.device, lib().hvae_decoder_workspace(dtype, nb, N, D))
     check(lib().hvae_decoder_train(dtype, ptr(U), U.stride(0), ptr(Eh), ptr(enorm), ptr(E32), x.ref, D,
                                    float(grad_scale), ptr(lse), ptr(O), ptr(recon_rows), ptr(dU), ptr(kl_rows),
-                                   float(beta), ptr(loss3), ptr(accum3), ptr(ws), ws.numel(), stream_of(U)),
+                                   float(beta), None, ptr(loss3), ptr(accum3), ptr(ws), ws.numel(), stream_of(U)),
           "hvae_decoder_train")
     return lse, O, recon_rows, dU
 

@@ -186,8 +186,11 @@ class HybridVAE(nn.Module):
         E = self.item_embeddings.detach()
         d = E.shape[1]
         if k <= 256 and d in (64, 128, 256, 384, 512, 768) and k <= E.shape[0]:
-            key = (E.data_ptr(), E.shape)
-            cache = getattr(self, "_topk_cache", None)
+            # the bf16 image and max||E|| are cached for a frozen E; the key carries the tensor's version, which
+            # load_state_dict / copy_ bump. A trainable E is written in place by libhvae's Adam (no version bump),
+            # so its image is rebuilt on every call
+            key = (E.data_ptr(), tuple(E.shape), self.item_embeddings._version)
+            cache = None if getattr(self, "item_embeddings_trainable", False) else getattr(self, "_topk_cache", None)
             if cache is None or cache[0] != key:
                 E32 = E.contiguous()
                 cache = (key, E32, ops.decoder_image(E32), ops.row_norm_max(E32))

@@ -26,7 +26,7 @@ from torch.utils.data import DataLoader, Dataset, RandomSampler
 from hvae import io as hio
 from hvae import ops
 from hvae.dist import init_from_env, is_main
-from hvae.executor import ConstBeta, DeviceData, FusedTrainer
+from hvae.executor import AnnealedBeta, ConstBeta, DeviceData, FusedTrainer
 
 from ..config import config
 from ..preprocessing.embeddings import load_embeddings
@@ -245,15 +245,12 @@ class VAETrainer:
         logger.info(f"Trainer on {device}, {sum(p.numel() for p in model.parameters()):,} params, "
                     f"decoder {self.fused.precision if self.fused is not None else 'module path (trainable E)'}")
 
-    # beta of one training batch (reference: _compute_loss, train.py:71-79)
+    # beta of one training batch (reference: _compute_loss, train.py:71-79): AnnealedVAE's schedule runs on the
+    # device inside the captured step (AnnealedBeta), so annealed epochs replay one graph like constant-beta ones
     def _beta_fn(self):
         m = self.model
         if hasattr(m, "compute_loss"):
-            def fn(_i):
-                b = m.get_current_beta()
-                m.step_annealing()
-                return b
-            return fn
+            return AnnealedBeta(m)
         return ConstBeta(m.beta)
 
     def _run_module(self, loader, train: bool) -> dict[str, float]:
@@ -433,7 +430,12 @@ def train_hybrid_vae(
     val_loader = DataLoader(UserInteractionDataset(val_matrix, val_users),
                             batch_size=batch_size, shuffle=False, num_workers=0)
 
-    anneal_steps = int(len(train_loader) * epochs * 0.5)
+    # the reference's len(train_loader) * epochs * 0.5 counts optimizer steps; under data parallelism one step covers
+    # batch_size x world users, so the schedule counts the global steps (ceil(n / (B W)) per epoch), and the
+    # annealed beta of step s is the single-GPU value at batch size B W
+    world = torch.distributed.get_world_size(group) if group is not None else 1
+    steps_per_epoch = -(-len(train_users) // (batch_size * world)) if world > 1 else len(train_loader)
+    anneal_steps = int(steps_per_epoch * epochs * 0.5)
     model = create_hybrid_vae(n_items=n_items, item_embeddings=embeddings, latent_dim=latent_dim,
                               hidden_dims=hidden_dims, dropout=dropout, beta=beta, use_annealing=use_annealing,
                               anneal_steps=anneal_steps)

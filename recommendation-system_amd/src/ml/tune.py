@@ -3,8 +3,8 @@
 Same search space, flags, outputs (models/grid_search_results.json with the "best_config" that
 `make train-best` reads) and selection rule (best NDCG@10 on the validation split, 1 + 99
 negatives) as the reference (tune.py:35-360). Every configuration trains through the fused HIP
-train step (hvae.executor.FusedTrainer via VAETrainer: one graph replay per batch, annealed beta
-stepped per batch) and is scored by the device evaluator's batched candidate ranking, instead of
+train step (hvae.executor.FusedTrainer via VAETrainer: one graph replay per batch, the annealed
+beta computed on the device by the replayed step itself) and is scored by the device evaluator's batched candidate ranking, instead of
 the reference's per-row densifying loader and per-user Python loop.
 """
 from __future__ import annotations

@@ -200,3 +200,34 @@ def test_lazy_adam_is_bitwise_dense(hip_device, wd, plan_side, monkeypatch):
     (ra, va, fa, ma, sa), (rb, vb, fb, mb, sb) = outs
     assert ra == rb and va == vb
     assert torch.equal(fa, fb) and torch.equal(ma, mb) and torch.equal(sa, sb)
+
+
+def test_annealed_epoch_graph_is_bitwise_eager(hip_device):
+    """AnnealedVAE (reference src/ml/model.py:295-334, stepped once per train batch, src/ml/train.py:74-76): the
+    schedule evaluated on the device inside the captured step (AnnealedBeta -> hvae_anneal_beta) replays one graph
+    per batch and gives bit for bit the epochs of the eager step fed the host's Python-float beta per batch."""
+    from hvae.executor import AnnealedBeta, FusedTrainer
+    from src.ml.model import create_hybrid_vae
+    X = synth_csr(300, 500, seed=3)
+    E = synth_embeddings(500, 128, seed=4)
+    outs = []
+    for arm in ("graph", "eager", "host"):
+        torch.manual_seed(0)
+        model = create_hybrid_vae(500, E, latent_dim=64, hidden_dims=[128], dropout=0.3, beta=0.2,
+                                  use_annealing=True, anneal_steps=7).to(hip_device)
+        fused = FusedTrainer(model, hip_device, precision="bf16", seed=1234, use_graphs=(arm == "graph"))
+        data = fused.device_data(X, list(range(300)))
+        gen = torch.Generator().manual_seed(5)
+        if arm == "host":  # a plain schedule callable: eager steps, beta passed from the host per batch
+            def beta_fn(_i, m=model):
+                b = m.get_current_beta()
+                m.step_annealing()
+                return b
+        else:
+            beta_fn = AnnealedBeta(model)
+        r = [fused.run_epoch(data, 64, True, beta_fn, 0.3, generator=gen) for _ in range(2)]
+        outs.append((r, fused.flat.clone(), model.current_step))
+    (ra, fa, sa), (rb, fb, sb), (rc, fc, sc) = outs
+    assert sa == sb == sc == 10  # 5 batches per epoch (the last one short) x 2 epochs, past anneal_steps = 7
+    assert ra == rb == rc
+    assert torch.equal(fa, fb) and torch.equal(fa, fc)
