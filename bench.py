@@ -145,7 +145,7 @@ def cpu_baseline(w: dict, X, E, seconds: float, threads: int | None = None) -> d
             t_load += t1 - t0
             t_step += t2 - t1
 
-    warm = 1 if B * w["items"] > 1e8 else 2  # the Syn-10M shape takes seconds per step
+    warm = 3  # 3 warm-up steps, then >= 20 steps or >= 60 s
     for i in range(warm):
         one(i, False)
     n, t0 = 0, time.perf_counter()
@@ -153,13 +153,14 @@ def cpu_baseline(w: dict, X, E, seconds: float, threads: int | None = None) -> d
         one(n + warm, True)
         n += 1
         el = time.perf_counter() - t0
-        if (el >= seconds and n >= 3) or n >= 5000:
+        if n >= 20 or el >= seconds:
             break
     return {"value": round(n * B / (t_load + t_step), 2), "unit": "users/s", "cores": threads, "kind": "port",
             "step_only": round(n * B / t_step, 2), "loader_only": round(n * B / t_load, 2),
             "cpu_model": model, "host_cpus_usable": cores,
-            "sample": f"{n} steps x {B} users of the same synthetic workload (per-row densifying loader + "
-                      f"fwd/bwd/clip/Adam in series), {el:.1f} s, torch fp32 on {threads} CPU threads"}
+            "sample": f"{warm} warm-up + {n} timed steps x {B} users of the same synthetic workload (per-row "
+                      f"densifying loader + fwd/bwd/clip/Adam in series), {el:.1f} s timed, torch fp32 on {threads} "
+                      f"CPU threads"}
 
 
 # kernel families the library's probe can bracket (ProbeScope names in csrc/)
@@ -224,7 +225,8 @@ def main():
     ap.add_argument("--workload", default="syn10m", choices=sorted(WORKLOADS))
     ap.add_argument("--batch-size", type=int, default=None)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8", "fp32"])
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
+                    help="CPU baseline: time >= 20 steps or this many seconds, whichever comes first (SURVEY §8d)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe-steps", type=int, default=50)
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
@@ -364,7 +366,8 @@ def main():
             "vs_baseline": None,
             "dtype": args.precision,
             "data": "synthetic (Zipf(0.8) items, 5+Poisson rows, L2-normalised random E; random-init weights)",
-            "config": {"workload": args.workload, "users": w["users"], "items": w["items"], "emb_dim": D,
+            "config": {"workload": args.workload, "users": w["users"], "users_resident": int(len(users)),
+                       "items": w["items"], "emb_dim": D,
                        "latent": w["latent"], "hidden": w["hidden"], "global_batch": B * world,
                        "batch_per_gpu": B, "parallelism": f"dp{world}", "decoder": args.precision},
             "roofline": roofline,

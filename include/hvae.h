@@ -390,10 +390,12 @@ int hvae_counters_add(int64_t* a, int64_t da, int64_t* b, int64_t db, void* stre
 /* No reference counterpart (the reference trainer is single-device). One rank's share of a
  * data-parallel step: its batch x compacted into row_ptr_out[0..nb] (int32 offsets from 0; [nb] = nnz),
  * col_out[0..cap) and vals_out[0..cap) = scale * vals. Ranks all-gather these packets with their da [nb, H]
- * and rebuild the union batch's first-layer row gradient with hvae_w1_rowgrad (hvae/dist.py). Entries at
- * or past cap are dropped (size cap from the host CSR: the batch's largest possible nnz). */
+ * and rebuild the union batch's first-layer row gradient with hvae_w1_rowgrad (hvae/dist.py). cap is sized
+ * from the host CSR (the batch's largest possible nnz); a batch with more entries keeps its first cap (row
+ * pointers clamped, so the packet stays a valid CSR) and sets *overflow = 1 (nullable), on which the host
+ * raises. */
 int hvae_csr_batch_pack(const hvae_csr_batch* x, float scale, int32_t* row_ptr_out, int32_t* col_out,
-                        float* vals_out, int64_t cap, void* stream);
+                        float* vals_out, int64_t cap, int32_t* overflow, void* stream);
 
 /* ------------------------------------------------------------ eval (K16) -- */
 /* scores[r, c] = U[user_row[r], :] . E32[cand[r, c], :]   (fp32)

@@ -11,6 +11,7 @@
 #include <stdint.h>
 #include <stddef.h>
 #include <math.h>
+#include <stdlib.h>
 
 #include "../../include/hvae.h"
 
@@ -58,6 +59,21 @@ static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream
 // different streams (the nodes of one captured graph) never share one.
 constexpr int kTicketPool = 1 << 16, kTicketSlice = 256;
 unsigned* ticket_slice();  // nullptr (error set) on failure
+
+// A/B knobs (HVAE_DEC_*, HVAE_TOPK_*, HVAE_TK_*, HVAE_GEMM_* in the environment) are read only by variant builds
+// compiled with -DHVAE_AB=1 (scripts/build_ab.sh -> build_var/libhvae_ab.so); the product library ignores the
+// environment and always runs its defaults.
+#ifndef HVAE_AB
+#define HVAE_AB 0
+#endif
+static inline const char* ab_getenv(const char* name) {
+#if HVAE_AB
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // Partials exchanged between the blocks of one launch go through agent-coherent
 // (sc1) stores and loads: they bypass the per-XCD L2s that plain accesses may

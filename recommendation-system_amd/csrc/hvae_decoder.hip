@@ -108,6 +108,7 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14));
 }
 
+#if HVAE_AB  // version 1 (transposed-copy sweep): A/B builds only (scripts/build_ab.sh)
 template <int D, bool WITH_O>
 __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, int64_t ldu,
                                                   const bf16_t* __restrict__ E, const bf16_t* __restrict__ Et,
@@ -324,6 +325,8 @@ __global__ void __launch_bounds__(256) k_dec_bf16(const float* __restrict__ U, i
     }
   }
 }
+
+#endif  // HVAE_AB
 
 // ------------------------------------------------------- bf16, version 2 ---
 // One row-major E image per tile (no transposed copy): GEMM1 reads its rows with
@@ -727,6 +730,7 @@ __global__ void __launch_bounds__(64 * NW) k_dec2_bf16(const float* __restrict__
   }
 }
 
+#if HVAE_AB  // versions 3 and 4: A/B builds only (scripts/build_ab.sh); version 5 is the d = 768 sweep
 // ------------------------------------------------------- bf16, version 3 ---
 // D = 768 (Syn-10M), the version-2 D split with the softmax owned by halves. Version 2 at D = 768 adds the
 // pair's whole partial S^T tiles through LDS and both waves of a user group run the full softmax: its loop
@@ -1510,6 +1514,8 @@ __global__ void __launch_bounds__(64 * NW) k_dec4_bf16(const float* __restrict__
   }
 }
 
+#endif  // HVAE_AB
+
 // ------------------------------------------------------------------- fp8 ---
 // The same sweep on the block-scaled fp8 MFMA (v_mfma_scale_f32_32x32x64_f8f6f4, OCP e4m3 operands,
 // twice the bf16 rate; BASELINE configs[4]). Both products carry exact power-of-two scales:
@@ -2088,6 +2094,7 @@ __global__ void __launch_bounds__(256) k_dec_fp8(const float* __restrict__ U, in
   }
 }
 
+#if HVAE_AB  // the fp8 sweep with version 4's structure: A/B builds only (it tied with the ring)
 // fp8 at d = 768 with version 4's structure (k_dec4_f8): wave (ug, dh) computes the COMPLETE S^T of items
 // 32 dh .. 32 dh + 31 of each 64-item tile over all of D (u over all of D as e4m3: 96 VGPRs, where the
 // DS = 2 ring above holds a D half and exchanges partial scores), so only P crosses LDS: each wave writes its
@@ -2392,6 +2399,8 @@ __global__ void __launch_bounds__(256) k_dec4_f8(const float* __restrict__ U, in
       }
   }
 }
+
+#endif  // HVAE_AB
 
 // ------------------------------------------------------------------- f32 ---
 // Same algorithm on v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 sums):
@@ -2895,18 +2904,21 @@ struct DecPlan {
   int64_t upb;
 };
 
+// A/B switches (environment, read at plan time) exist only in variant builds (-DHVAE_AB=1, scripts/build_ab.sh);
+// the product library runs one sweep per (dtype, D): bf16 version 2 at D <= 384, version 5 at D = 768, the fp8
+// ring, the fp32 sweep.
+#if HVAE_AB
 static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return (v && *v) ? atoi(v) : dflt;
 }
 
 // HVAE_DEC_V1=1 selects the version-1 bf16 sweep (transposed image copy), HVAE_DEC_SPLITS=k forces k item splits
-// (both for A/B measurements; read once per process).
 static bool dec_use_v1() {
   static const int v = env_int("HVAE_DEC_V1", 0);
   return v != 0;
 }
-static int dec_forced_splits() { return env_int("HVAE_DEC_SPLITS", 0); }  // read at every plan (A/B)
+static int dec_forced_splits() { return env_int("HVAE_DEC_SPLITS", 0); }
 
 static int dec_forced_ds() {
   static const int v = env_int("HVAE_DEC_DS", 0);
@@ -2917,6 +2929,13 @@ static int dec_forced_nw() {
   static const int v = env_int("HVAE_DEC_NW", 0);
   return v;
 }
+#else
+static bool dec_use_v1() { return false; }
+static int dec_forced_splits() { return 0; }
+static int dec_forced_ds() { return 0; }
+static int dec_forced_nw() { return 0; }
+static int env_int(const char*, int dflt) { return dflt; }
+#endif
 
 static bool v2_supported(int64_t D) { return D == 64 || D == 128 || D == 256 || D == 384 || D == 768; }
 // HVAE_DEC_V3=0 keeps the version-2 sweep at D = 768 (A/B; read at every plan, so a test can switch it)
@@ -2964,7 +2983,8 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   if (p.v2 && D <= 384 && (dec_forced_ds() == 1 || dec_forced_ds() == 2)) p.ds = dec_forced_ds();
   p.nw = p.v2 && p.ds == 2 && nb > 64 && D <= 384 ? 8 : 4;
   if (p.v2 && p.ds == 2 && D <= 384 && (dec_forced_nw() == 4 || dec_forced_nw() == 8)) p.nw = dec_forced_nw();
-  p.upb = bf ? (p.v4 && D == 384 ? 128 : p.v3 ? 64 : p.v2 ? 32 * p.nw / p.ds : kBfUsersPerBlock) : kF32UsersPerBlock;
+  p.upb = bf ? (p.v4 && D == 384 ? 128 : (p.v3 || p.v5) ? 64 : p.v2 ? 32 * p.nw / p.ds : kBfUsersPerBlock)
+             : kF32UsersPerBlock;
   const int64_t ti = bf ? kBfTI : kF32TI;
   const int64_t target = bf ? 256 : 512;
   const int64_t nub = cdiv(nb, p.upb), tiles = cdiv(N, ti);
@@ -2993,6 +3013,7 @@ static size_t dec_ws_bytes(int splits, int64_t nb, int64_t D) {
          (size_t)nb * D * sizeof(float);
 }
 
+#if HVAE_AB
 template <int D, bool WO>
 static int launch_bf16(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                        const DecPlan& p, DecOut o, hipStream_t st) {
@@ -3008,6 +3029,7 @@ static int launch_bf16(const float* U, int64_t ldu, const void* E, const float* 
   HVAE_LAUNCH_CHECK("k_dec_bf16");
   return HVAE_OK;
 }
+#endif  // HVAE_AB
 
 template <int D, int DS, int NW, bool WO>
 static int launch_bf16_v2_nw(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
@@ -3034,6 +3056,7 @@ static int launch_bf16_v2(const float* U, int64_t ldu, const void* E, const floa
   return launch_bf16_v2_nw<D, DS, 4, WO>(U, ldu, E, enorm, nb, N, p, o, st);
 }
 
+#if HVAE_AB
 template <int D, bool WO>
 static int launch_bf16_v3(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                           const DecPlan& p, DecOut o, hipStream_t st) {
@@ -3049,7 +3072,9 @@ static int launch_bf16_v3(const float* U, int64_t ldu, const void* E, const floa
   HVAE_LAUNCH_CHECK("k_dec3_bf16");
   return HVAE_OK;
 }
+#endif  // HVAE_AB
 
+#if HVAE_AB
 template <int D, bool WO>
 static int launch_bf16_v4(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                           const DecPlan& p, DecOut o, hipStream_t st) {
@@ -3067,6 +3092,7 @@ static int launch_bf16_v4(const float* U, int64_t ldu, const void* E, const floa
   HVAE_LAUNCH_CHECK("k_dec4_bf16");
   return HVAE_OK;
 }
+#endif  // HVAE_AB
 
 template <int D, bool WO>
 static int launch_fp8(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
@@ -3086,6 +3112,7 @@ static int launch_fp8(const float* U, int64_t ldu, const void* E, const float* e
   return HVAE_OK;
 }
 
+#if HVAE_AB
 template <bool WO>
 static int launch_fp8_v4(const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                          const DecPlan& p, DecOut o, hipStream_t st) {
@@ -3101,6 +3128,7 @@ static int launch_fp8_v4(const float* U, int64_t ldu, const void* E, const float
   HVAE_LAUNCH_CHECK("k_dec4_f8");
   return HVAE_OK;
 }
+#endif  // HVAE_AB
 
 template <int D, bool WO>
 static int launch_f32(const float* U, int64_t ldu, const void* E, int64_t nb, int64_t N, const DecPlan& p,
@@ -3125,20 +3153,24 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
       case 128: return launch_fp8<128, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 256: return launch_fp8<256, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 384: return launch_fp8<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
-      case 768:  // HVAE_DEC_F8V4=0 keeps the D-split ring (A/B; read at every call)
+      case 768:
+#if HVAE_AB  // HVAE_DEC_F8V4=1 runs the version-4 structure instead of the D-split ring
         if (env_int("HVAE_DEC_F8V4", 0) != 0) return launch_fp8_v4<WO>(U, ldu, E, enorm, nb, N, p, o, st);
+#endif
         return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       default: break;
     }
   } else if (dtype == HVAE_BF16 && p.v5 && D == 768) {
     return dec5_launch(WO, U, ldu, E, enorm, nb, N, p.splits, p.tiles_per_split, p.blocks, o.flag, o.m, o.l, o.O,
                        o.lse, o.direct, st);
+#if HVAE_AB
   } else if (dtype == HVAE_BF16 && p.v4 && D == 768) {
     return launch_bf16_v4<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
   } else if (dtype == HVAE_BF16 && p.v4 && D == 384) {
     return launch_bf16_v4<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
   } else if (dtype == HVAE_BF16 && p.v3 && D == 768) {
     return launch_bf16_v3<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+#endif
   } else if (dtype == HVAE_BF16 && p.v2) {
     if (p.ds == 1) {
       switch (D) {
@@ -3154,10 +3186,13 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
         case 128: return launch_bf16_v2<128, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
         case 256: return launch_bf16_v2<256, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
         case 384: return launch_bf16_v2<384, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+#if HVAE_AB
         case 768: return launch_bf16_v2<768, 2, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+#endif
         default: break;
       }
     }
+#if HVAE_AB
   } else if (dtype == HVAE_BF16) {
     switch (D) {
       case 64: return launch_bf16<64, WO>(U, ldu, E, enorm, nb, N, p, o, st);
@@ -3166,7 +3201,8 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
       case 384: return launch_bf16<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       default: break;
     }
-  } else {
+#endif
+  } else if (dtype != HVAE_BF16) {
     switch (D) {
       case 32: return launch_f32<32, WO>(U, ldu, E, nb, N, p, o, st);
       case 64: return launch_f32<64, WO>(U, ldu, E, nb, N, p, o, st);

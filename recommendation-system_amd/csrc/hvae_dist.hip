@@ -20,7 +20,10 @@ constexpr int kPackThreads = 1024;
 constexpr int kPackMaxRows = 1 << 20;
 
 // row_ptr_out[0..nb] = exclusive prefix sums of the batch's row lengths (one block)
-__global__ void __launch_bounds__(kPackThreads) k_pack_rowptr(hvae_csr_batch x, int32_t* __restrict__ row_ptr_out) {
+// (clamped to cap, with *overflow = 1, when the batch holds more than cap entries: the packet stays a valid CSR
+// of the entries it kept, and the host raises on the flag)
+__global__ void __launch_bounds__(kPackThreads) k_pack_rowptr(hvae_csr_batch x, int32_t* __restrict__ row_ptr_out,
+                                                              int64_t cap, int32_t* __restrict__ overflow) {
   __shared__ int32_t wsum[kPackThreads / 64];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int64_t per = (x.nb + kPackThreads - 1) / kPackThreads;
@@ -44,18 +47,18 @@ __global__ void __launch_bounds__(kPackThreads) k_pack_rowptr(hvae_csr_batch x, 
   for (int j = 0; j < w; ++j) base += wsum[j];
   int32_t run = base + incl - mine;
   for (int64_t b = r0; b < r1; ++b) {  // second pass over the thread's rows (L1/L2-warm)
-    row_ptr_out[b] = run;
+    row_ptr_out[b] = (int32_t)min((int64_t)run, cap);
     run += row_len(b);
   }
   if (tid == kPackThreads - 1) {
     int32_t tot = 0;
     for (int j = 0; j < kPackThreads / 64; ++j) tot += wsum[j];
-    row_ptr_out[x.nb] = tot;
+    row_ptr_out[x.nb] = (int32_t)min((int64_t)tot, cap);
+    if (tot > cap && overflow) *overflow = 1;
   }
 }
 
-// the entries: one wave per batch row, lanes over the row's entries (coalesced); entries at or past cap are
-// dropped (row_ptr_out[nb] still reports the batch's nnz)
+// the entries: one wave per batch row, lanes over the row's entries (coalesced), up to the row's clamped end
 __global__ void __launch_bounds__(256) k_pack_entries(hvae_csr_batch x, const int32_t* __restrict__ row_ptr_out,
                                                       float scale, int32_t* __restrict__ col_out,
                                                       float* __restrict__ vals_out, int64_t cap) {
@@ -79,13 +82,13 @@ __global__ void __launch_bounds__(256) k_pack_entries(hvae_csr_batch x, const in
 using namespace hvae;
 
 extern "C" int hvae_csr_batch_pack(const hvae_csr_batch* x, float scale, int32_t* row_ptr_out, int32_t* col_out,
-                                   float* vals_out, int64_t cap, void* stream) {
+                                   float* vals_out, int64_t cap, int32_t* overflow, void* stream) {
   HVAE_REQUIRE(x && x->row_ptr && x->col_idx && x->vals && row_ptr_out && cap >= 0 && (cap == 0 || (col_out && vals_out)),
                "hvae_csr_batch_pack: bad args");
   HVAE_REQUIRE(x->nb >= 0 && x->nb <= kPackMaxRows,
                "hvae_csr_batch_pack: nb = %lld over %d", (long long)x->nb, kPackMaxRows);
   hipStream_t st = as_stream(stream);
-  k_pack_rowptr<<<1, kPackThreads, 0, st>>>(*x, row_ptr_out);
+  k_pack_rowptr<<<1, kPackThreads, 0, st>>>(*x, row_ptr_out, cap, overflow);
   HVAE_LAUNCH_CHECK("k_pack_rowptr");
   if (x->nb > 0) {
     k_pack_entries<<<(unsigned)cdiv(x->nb, 4), 256, 0, st>>>(*x, row_ptr_out, scale, col_out, vals_out, cap);

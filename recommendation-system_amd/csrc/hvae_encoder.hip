@@ -933,7 +933,9 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
             __builtin_amdgcn_s_waitcnt(0);  // this wave's partial has reached the coherence point
             const int ca = beg / CH, cb = (end - 1) / CH;
             int tk = 0;
-            if (lane == 0) tk = __hip_atomic_fetch_add(ticket + si, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // acq_rel: every chunk's release publishes its partial before its ticket, and the last taker's acquire
+            // orders its partial loads after all of them (HIP memory model, agent scope)
+            if (lane == 0) tk = __hip_atomic_fetch_add(ticket + si, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
             tk = __shfl(tk, 0, 64);
             if (tk == cb - ca) {  // the segment's last chunk to finish: its partials, in chunk order
               const float* first = part + (int64_t)(2 * ca + (beg % CH == 0 ? 0 : 1)) * H;

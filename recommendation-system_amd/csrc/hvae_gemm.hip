@@ -602,7 +602,7 @@ __global__ void k_colsum_final(const float* __restrict__ part, int64_t P, int64_
 // HVAE_GEMM_TILE64_MIN (A/B knob, read once): the 64x64-tile count from which 64x64 tiles are used.
 static int64_t tile64_min() {
   static const int64_t v = [] {
-    const char* e = std::getenv("HVAE_GEMM_TILE64_MIN");
+    const char* e = ab_getenv("HVAE_GEMM_TILE64_MIN");
     return e ? std::max<int64_t>(1, std::atoll(e)) : (int64_t)512;
   }();
   return v;
@@ -645,17 +645,17 @@ struct FastPlan {
 static FastPlan fast_plan(bool ta, bool tb, int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                           const float* B, int64_t ldb, bool /*pair_w*/) {
   FastPlan f;
-  const char* e = std::getenv("HVAE_GEMM_FAST");
+  const char* e = ab_getenv("HVAE_GEMM_FAST");
   if (e && std::atoi(e) == 0) return f;
   if (!ta || tb) return f;
   if (K < 1024 || K % FBK || ((uintptr_t)A) % 16 || ((uintptr_t)B) % 16 || lda % 4 || ldb % 4) return f;
   int bt = cdiv(M, 32) * cdiv(N, 32) <= 256 ? 32 : 64;
-  if (const char* t = std::getenv("HVAE_GEMM_FAST_TILE")) bt = std::atoi(t) == 64 ? 64 : 32;
+  if (const char* t = ab_getenv("HVAE_GEMM_FAST_TILE")) bt = std::atoi(t) == 64 ? 64 : 32;
   if (M % bt || N % bt) return f;
   const int64_t tiles = (M / bt) * (N / bt);
   int64_t s = 1;
   if (K > 1024) s = std::max<int64_t>(1, std::min<int64_t>((512 + tiles - 1) / tiles, K / 256));
-  if (const char* t = std::getenv("HVAE_GEMM_FAST_SPLITS")) s = std::max(1, std::atoi(t));
+  if (const char* t = ab_getenv("HVAE_GEMM_FAST_SPLITS")) s = std::max(1, std::atoi(t));
   s = std::min<int64_t>(s, 64);
   if (s > 1 && tiles > (int64_t)kTicketSlice) s = 1;
   const int64_t kps = cdiv(cdiv(K, s), FBK) * FBK;

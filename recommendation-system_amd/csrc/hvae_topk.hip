@@ -578,12 +578,12 @@ __global__ void __launch_bounds__(256) k_topk_select(TkSelArgs a) {
 }
 
 static int tk_lds_scan(int64_t D) {  // HVAE_TOPK_LDS=0 keeps the global-load scan (A/B)
-  const char* v = getenv("HVAE_TOPK_LDS");
+  const char* v = ab_getenv("HVAE_TOPK_LDS");
   return D % 128 == 0 && ((v && *v) ? (atoi(v) != 0) : 1);
 }
 
 static int tk_wave_users() {  // HVAE_TOPK_WAVE_USERS=0 selects the tile-split mapping (A/B)
-  const char* v = getenv("HVAE_TOPK_WAVE_USERS");
+  const char* v = ab_getenv("HVAE_TOPK_WAVE_USERS");
   return (v && *v) ? (atoi(v) != 0) : 1;
 }
 
@@ -613,7 +613,7 @@ extern "C" size_t hvae_topk_fused_workspace(int64_t R, int64_t N, int64_t D, int
 
 // HVAE_TK_TAU_PERIOD (A/B, read at every call; a power of two): tiles between reads of the other waves' bounds
 static int tk_tau_mask() {
-  const char* e = std::getenv("HVAE_TK_TAU_PERIOD");
+  const char* e = ab_getenv("HVAE_TK_TAU_PERIOD");
   int p = e ? std::atoi(e) : 8;
   if (p < 1 || (p & (p - 1)) != 0) p = 8;
   return p - 1;

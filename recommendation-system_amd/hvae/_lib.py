@@ -143,7 +143,7 @@ SIGNATURES = {
     "hvae_read_interactions": (cint, [C.c_char_p, C.c_char_p, i64, i64, C.c_char_p, i64, i64, cint,
                                       P(HostCsr)]),
     "hvae_host_csr_free": (None, [P(HostCsr)]),
-    "hvae_csr_batch_pack": (cint, [P(CsrBatch), f32, vp, vp, vp, i64, vp]),
+    "hvae_csr_batch_pack": (cint, [P(CsrBatch), f32, vp, vp, vp, i64, vp, vp]),
 }
 
 _lib = None

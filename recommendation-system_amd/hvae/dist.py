@@ -105,8 +105,17 @@ class DPExchange:
         self.merge_fn = merge_fn or _hip_merge
         self.make_merged = make_merged or _hip_make_merged
         self.B = self.cap = 0
+        # set by hvae_csr_batch_pack when a batch held more entries than its packet's cap (checked by check())
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
         self._plans: dict = {}
         self._merged: dict = {}
+
+    def check(self) -> None:
+        """Raise if any packet since the last check dropped entries (its cap, sized from the host CSR, was
+        exceeded): the union row gradient of that step would be wrong. One host read, at epoch end."""
+        if int(self.overflow.item()):
+            self.overflow.zero_()
+            raise RuntimeError("data-parallel packet overflow: a batch held more CSR entries than its cap")
 
     # ----------------------------------------------------------- collectives ---
     def _stage(self, t: torch.Tensor) -> torch.Tensor:
@@ -269,7 +278,8 @@ def _hip_make_merged(n_items, H, cap, device):
 def _hip_pack(ex: DPExchange, x, weight, rp_out, col_out, val_out, cap):
     from ._lib import check, lib, ptr
     check(lib().hvae_csr_batch_pack(x, float(weight), ptr(rp_out), ptr(col_out), ptr(val_out), cap,
-                                    torch.cuda.current_stream(ex.device).cuda_stream), "hvae_csr_batch_pack")
+                                    ptr(ex.overflow), torch.cuda.current_stream(ex.device).cuda_stream),
+          "hvae_csr_batch_pack")
 
 
 def _hip_merge(ex: DPExchange, row_ptr, col_idx, vals, rows, nb, da, out):

@@ -725,6 +725,8 @@ class FusedTrainer:
         if train:
             self.host_step += 1
             self.flush()
+            if dp is not None:
+                dp.check()
         return bf.loss3
 
     def run_epoch(self, data: DeviceData, batch_size: int, shuffle: bool, beta_fn, p_drop: float,
@@ -853,7 +855,7 @@ class FusedTrainer:
             beta = const_beta if const_beta is not None else beta_fn(n_full)
             bf = self._buffers(tail, data.max_batch_nnz(tail), False)
             self._launch(bf, self._csr(data, tail, data.perm, self.boff), False, beta, p_drop, advance=tail)
-        tot = dp.all_reduce(self.accum_val.cpu().numpy())  # the batches' losses summed over the ranks
+        tot = dp.all_reduce(self.accum_val.cpu().numpy()).tolist()  # the batches' losses summed over the ranks
         if n_batches == 0:
             return {"total_loss": float("nan"), "recon_loss": float("nan"), "kl_loss": float("nan")}, 0
         return {"total_loss": tot[0] / n_batches, "recon_loss": tot[1] / n_batches,
@@ -969,7 +971,9 @@ class FusedTrainer:
             self._launch_dp_update(bf, c)
             self.host_step += 1
         self.flush()
-        tot = dp.all_reduce(sums)  # the union batches' losses summed over the steps
+        dp.check()
+        tot = dp.all_reduce(sums).tolist()  # the union batches' losses summed over the steps (Python floats:
+        # the metrics go into checkpoints, which load with weights_only=True)
         return ({"total_loss": tot[0] / n_steps, "recon_loss": tot[1] / n_steps, "kl_loss": tot[2] / n_steps},
                 n_steps)
 

@@ -276,7 +276,7 @@ class VAETrainer:
                     loss, recon, kl = vae_loss_function(recon_x, x, mu, logvar, self.model.beta)
             tot += np.array([loss.item(), recon.item(), kl.item()])
             n += 1
-        return {"total_loss": tot[0] / n, "recon_loss": tot[1] / n, "kl_loss": tot[2] / n}
+        return {"total_loss": float(tot[0] / n), "recon_loss": float(tot[1] / n), "kl_loss": float(tot[2] / n)}
 
     def _run(self, loader, train: bool) -> dict[str, float]:
         if self.fused is None:
@@ -303,7 +303,7 @@ class VAETrainer:
             loss3 = self.fused.step_batch(data, None, x.shape[0], beta_fn(i), p_drop, train=train)
             tot += np.array(loss3.tolist())
             n += 1
-        return {"total_loss": tot[0] / n, "recon_loss": tot[1] / n, "kl_loss": tot[2] / n}
+        return {"total_loss": float(tot[0] / n), "recon_loss": float(tot[1] / n), "kl_loss": float(tot[2] / n)}
 
     def train_epoch(self, loader) -> dict[str, float]:
         self.model.train()

@@ -32,7 +32,7 @@ def main():
                                                           "batch's sparse terms) instead of hvae_decoder_fwd")
     ap.add_argument("--probe", default="decoder_sweep", choices=["decoder_sweep", "decoder_finalize"])
     ap.add_argument("--ab", nargs="*", default=[], help="A/B arms in one process: each arm a comma list of "
-                    "ENV=VAL settings read by the library at plan time (e.g. HVAE_DEC_V3=0), timed in "
+                    "ENV=VAL settings read by the A/B library (HVAE_LIB=build_var/libhvae_ab.so; e.g. HVAE_DEC_V3=0), timed in "
                     "interleaved rounds")
     ap.add_argument("--rounds", type=int, default=3)
     args = ap.parse_args()

@@ -1,0 +1,99 @@
+"""Checks of the A/B variant kernels (not collected by default: no test_ prefix).
+
+The product libhvae.so runs one sweep per (dtype, d) and ignores the environment. The retired variants -- bf16
+versions 2, 3 and 4 at d = 768 beside version 5, the fp8 sweep with version 4's structure (k_dec4_f8) beside
+the D-split ring -- build only with -DHVAE_AB=1 (`make -C recommendation-system_amd lib-ab` ->
+build_var/libhvae_ab.so), where HVAE_DEC_* select them at plan time. tests/test_gpu_ab_variant.py runs this file
+in a subprocess with HVAE_LIB pointing at that build, so the variants keep their parity checks without being
+shipped.
+"""
+import os
+import sys
+from pathlib import Path
+
+import pytest
+import torch
+
+HERE = Path(__file__).resolve().parent
+for _p in (str(HERE.parent / "recommendation-system_amd"), str(HERE.parent), str(HERE / "golden"), str(HERE)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+from gen import synth_csr, synth_embeddings  # noqa: E402
+
+pytestmark = pytest.mark.skipif(not os.environ.get("HVAE_LIB", "").endswith("libhvae_ab.so"),
+                                reason="runs against the A/B variant build only (tests/test_gpu_ab_variant.py)")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="module")
+def ops(dev):
+    from hvae import ops
+    return ops
+
+
+def _maxrel(a, b):
+    a = a.detach().double()
+    b = b.detach().double().to(a.device)
+    return float((a - b).abs().max() / max(b.abs().max().item(), 1e-30))
+
+
+def test_decoder_d768_versions_agree(ops, dev, monkeypatch):
+    """Versions 5 (GEMM1 and GEMM2 on different waves, the product sweep), 4 (item-split GEMM1, one barrier
+    per tile) and 3 (item-half softmax ownership) against version 2 (whole-tile softmax in both waves) of the
+    d = 768 bf16 sweep: all round the same bf16 operands (P to bf16 included); only fp32 summation order
+    differs."""
+    nb, N, D = 700, 50_001, 768
+    g = torch.Generator(device=dev).manual_seed(11)
+    E = torch.randn(N, D, device=dev, generator=g)
+    E /= E.norm(dim=1, keepdim=True)
+    U = torch.randn(nb, D, device=dev, generator=g)
+    U *= 4.0 / U.norm(dim=1, keepdim=True)
+    X = synth_csr(nb, N, lam=15.0, seed=3)
+    xd = ops.csr_from_scipy(X, dev)
+    img = ops.decoder_image(E)
+    enorm = ops.row_norm_max(img)
+    out = {}
+    for name, v3, v4, v5 in (("v5", "1", "1", "1"), ("v4", "1", "1", "0"), ("v3", "1", "0", "0"),
+                             ("v2", "0", "0", "0")):
+        monkeypatch.setenv("HVAE_DEC_V3", v3)
+        monkeypatch.setenv("HVAE_DEC_V4", v4)
+        monkeypatch.setenv("HVAE_DEC_V5", v5)
+        out[name] = ops.decoder_train(xd, U, img, enorm, E, 1.0 / nb, want_o=True)
+    l2, o2, r2, d2 = out["v2"]
+    for name in ("v5", "v4", "v3"):
+        la, oa, ra, da = out[name]
+        assert (la - l2).abs().max() < 1e-4, name
+        assert _maxrel(oa, o2) < 5e-3 and _maxrel(ra, r2) < 1e-5 and _maxrel(da, d2) < 5e-3, name
+
+
+@pytest.mark.parametrize("nb,N", [(64, 2000), (300, 5001), (7, 100), (130, 4000)])
+def test_decoder_fp8_v4_structure(ops, dev, nb, N, monkeypatch):
+    """k_dec4_f8 (HVAE_DEC_F8V4=1) against float64 on the quantised operands, inside the e4m3 envelope of
+    tests/test_gpu_fp8.py, and its fused train form equal to its fwd + bwd."""
+    from test_gpu_fp8 import _image, _o_envelope, _quantised
+    D = 768
+    monkeypatch.setenv("HVAE_DEC_F8V4", "1")
+    E = torch.as_tensor(synth_embeddings(N, D, seed=N))
+    g = torch.Generator().manual_seed(nb)
+    U = torch.randn(nb, D, generator=g) * 3.0
+    img = _image(ops, E.to(dev))
+    enorm = ops.row_norm_max(img)
+    lse, O = ops.decoder_fwd(U.to(dev), img, enorm)
+    Eq, Uq, _ = _quantised(E, U)
+    S = Uq.double() @ Eq.double().t()
+    lse_ref = torch.logsumexp(S, 1)
+    O_ref = torch.softmax(S, 1) @ Eq.double()
+    assert (lse.double().cpu() - lse_ref).abs().max() < 2e-4 * max(1.0, lse_ref.abs().max().item())
+    assert ((O.double().cpu() - O_ref).abs() <= _o_envelope(S, Eq)).all()
+    X = synth_csr(nb, N, lam=5.0, seed=nb + N)
+    xd = ops.csr_from_scipy(X, dev)
+    lse_t, O_t, rr, dU = ops.decoder_train(xd, U.to(dev), img, enorm, E.to(dev), 1.0 / nb, want_o=True)
+    rr_b, dU_b = ops.decoder_bwd(xd, U.to(dev), E.to(dev), lse, O, 1.0 / nb)
+    assert torch.equal(lse_t, lse) and torch.equal(O_t, O) and torch.equal(rr, rr_b) and torch.equal(dU, dU_b)
