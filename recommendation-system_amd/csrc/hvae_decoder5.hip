@@ -103,6 +103,9 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #ifndef DEC5_DMA_BURST
 #define DEC5_DMA_BURST 0  // A/B: each wave issues its pieces back to back at its first DMA slot
 #endif
+#ifndef DEC5_PRIO
+#define DEC5_PRIO 0  // A/B: static s_setprio 1 before the loop for 1 the consumer waves (4..7), 2 the producers
+#endif
 
 constexpr int D = 768;
 constexpr int NS = 3;                    // tile slots
@@ -177,6 +180,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     asm volatile("" ::: "memory");
   };
   auto p_row = [&](int par, int uu) { return pbuf + ((par * 2 + ug) * 32 + uu) * PST; };
+  if ((DEC5_PRIO == 1 && role == 1) || (DEC5_PRIO == 2 && role == 0)) __builtin_amdgcn_s_setprio(1);
 
   if (role == 0) {
     // ------------------------------------------------------------------ producer ---
