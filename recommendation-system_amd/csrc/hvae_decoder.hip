@@ -2951,6 +2951,9 @@ static bool v5_supported(int64_t D) { return D == 768 && env_int("HVAE_DEC_V5", 
 int dec5_launch(bool with_o, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                 int splits, int64_t tiles_per_split, int64_t blocks, int* flag, float* m, float* l, float* O,
                 float* lse, int direct, hipStream_t st);
+int dec5_f8_launch(bool with_o, const float* U, int64_t ldu, const unsigned char* T8, const int* ke,
+                   const float* enorm, int64_t nb, int64_t N, int splits, int64_t tiles_per_split, int64_t blocks,
+                   int* flag, float* m, float* l, float* O, float* lse, int direct, hipStream_t st);
 
 static void dec_set_splits(DecPlan& p, int64_t tiles, int64_t s) {
   s = std::max<int64_t>(1, std::min<int64_t>(s, std::min<int64_t>(tiles, kMaxSplits)));
@@ -3154,10 +3157,13 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
       case 256: return launch_fp8<256, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 384: return launch_fp8<384, WO>(U, ldu, E, enorm, nb, N, p, o, st);
       case 768:
-#if HVAE_AB  // HVAE_DEC_F8V4=1 runs the version-4 structure instead of the D-split ring
+#if HVAE_AB  // HVAE_DEC_F8V4=1 runs the version-4 structure, HVAE_DEC_F8V5=0 the D-split ring
         if (env_int("HVAE_DEC_F8V4", 0) != 0) return launch_fp8_v4<WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        if (env_int("HVAE_DEC_F8V5", 1) == 0) return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
 #endif
-        return launch_fp8<768, WO>(U, ldu, E, enorm, nb, N, p, o, st);
+        return dec5_f8_launch(WO, U, ldu, (const unsigned char*)E + f8_offset_bytes(N, 768),
+                              (const int*)((const char*)E + f8_tail_offset(N, 768)), enorm, nb, N, p.splits,
+                              p.tiles_per_split, p.blocks, o.flag, o.m, o.l, o.O, o.lse, o.direct, st);
       default: break;
     }
   } else if (dtype == HVAE_BF16 && p.v5 && D == 768) {

@@ -103,6 +103,12 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #ifndef DEC5_DMA_BURST
 #define DEC5_DMA_BURST 0  // A/B: each wave issues its pieces back to back at its first DMA slot
 #endif
+#ifndef DEC5_BFREE
+#define DEC5_BFREE 0  // A/B: branch-free LDS-DMA issue in the loop
+#endif
+#ifndef DEC5_P32
+#define DEC5_P32 0  // A/B: producers of 32 users over one item half (GEMM1 reads each tile twice, not four times)
+#endif
 #ifndef DEC5_PRIO
 #define DEC5_PRIO 0  // A/B: static s_setprio 1 before the loop for 1 the consumer waves (4..7), 2 the producers
 #endif
@@ -182,6 +188,157 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   auto p_row = [&](int par, int uu) { return pbuf + ((par * 2 + ug) * 32 + uu) * PST; };
   if ((DEC5_PRIO == 1 && role == 1) || (DEC5_PRIO == 2 && role == 0)) __builtin_amdgcn_s_setprio(1);
 
+  if (DEC5_P32 && role == 0) {
+    // ------------------------------------------------------- producer, 32 users (A/B) ---
+    // producer q = (ug, ih) owns item half ih of every tile for all 32 users of ug (version 4's GEMM1: U over
+    // all of D for 32 users in 192 VGPRs, one A read per k-step serving both 16-user halves), so the producers
+    // read each tile twice from LDS instead of four times; the first tile's max crosses once between the two
+    // producers of a user group (xmax), and l = l(half 0) + l(half 1) at the end
+    const int ih = dh;
+    float* xmax = xm + 128;  // [4 producers][32 users]
+    const float emax = *e_maxnorm;
+    bf16x8 uf[2][KS];  // GEMM1's B operand: lane holds U[u0 + 16 uh + c16][32 ks + 8 g .. + 7]
+    float bound[2];
+#pragma unroll
+    for (int uh = 0; uh < 2; ++uh) {
+      const int64_t ub = u0 + 16 * uh + c16;
+      const int64_t ur = ub < nb ? ub : nb - 1;  // rows past nb load row nb - 1, zeroed
+      const float keep = ub < nb ? 1.f : 0.f;
+      float usq = 0.f;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const float* up = U + ur * ldu + 32 * ks + 8 * g;
+        if (ks > 0) asm volatile("" : "+v"(up) : "v"(uf[uh][ks - 1]));  // one k-step's loads live at a time
+        float4 a = *reinterpret_cast<const float4*>(up);
+        float4 b = *reinterpret_cast<const float4*>(up + 4);
+        a.x *= keep; a.y *= keep; a.z *= keep; a.w *= keep;
+        b.x *= keep; b.y *= keep; b.z *= keep; b.w *= keep;
+        usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w) + (b.x * b.x + b.y * b.y) + (b.z * b.z + b.w * b.w);
+        uf[uh][ks] = bf16x8{(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w,
+                            (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
+      }
+      usq += __shfl_xor(usq, 16, 64);
+      usq += __shfl_xor(usq, 32, 64);
+      bound[uh] = sqrtf(usq) * emax * 1.02f;
+    }
+    const int gi = dec5_rowblk(g);  // MFMA rows 4 g .. 4 g + 3 hold items 4 gi .. 4 gi + 3 of the half
+    const int r1 = 16 * ih + 4 * dec5_rowblk(c16 >> 2) + (c16 & 3);
+    const int laneA = ((r1 >> 3) << 11) + ((r1 & 7) << 6) + ((g ^ ((r1 >> 2) & 3)) << 4);
+    auto gemm1 = [&](const unsigned char* buf, f32x4 (&s)[2], auto&& fill) {
+#pragma unroll
+      for (int uh = 0; uh < 2; ++uh)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) s[uh][r] = 0.f;
+      auto rdA = [&](int ks) {
+        return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(buf + laneA + ((ks >> 2) << 13) +
+                                                                         ((ks & 3) << 9)));
+      };
+      constexpr int AH = DEC5_G1_AHEAD;
+      bf16x8 a[AH];
+#pragma unroll
+      for (int j = 0; j < AH; ++j) a[j] = rdA(j);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 c = a[ks % AH];
+        if (ks + AH < KS) a[ks % AH] = rdA(ks + AH);
+        s[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c, uf[0][ks], s[0], 0, 0, 0);
+        s[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(c, uf[1][ks], s[1], 0, 0, 0);
+        fill(ks);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    float m[2] = {0.f, 0.f}, mL[2] = {0.f, 0.f}, lsum[2] = {0.f, 0.f};
+    f32x4 s_nx[2];
+    auto mask_tail = [&](f32x4 (&s)[2], int64_t t) {
+      if (t == ntiles - 1 && (N % kTI) != 0) {
+        const int lim = (int)(N - t * kTI) - 16 * ih - 4 * gi;
+#pragma unroll
+        for (int uh = 0; uh < 2; ++uh)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) s[uh][r] = r >= lim ? -INFINITY : s[uh][r];
+      }
+    };
+    auto p_out = [&](int par) {  // 8 exponentials (4 items x 2 users), the sums, the packed P row pieces -> LDS
+#pragma unroll
+      for (int uh = 0; uh < 2; ++uh) {
+        float pv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          pv[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_nx[uh][r], kLog2e, -mL[uh]));
+          lsum[uh] += pv[r];
+        }
+        *reinterpret_cast<uint2*>(p_row(par, 16 * uh + c16) + 2 * (16 * ih + 8 * (gi & 1) + 4 * (gi >> 1))) =
+            make_uint2(pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3]));
+      }
+    };
+    if (t_beg < t_end) {
+      for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg), 0, i, i == 0);
+      if (t_beg + 1 < t_end)
+        for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg + 1), 1, i, false);
+      wait_vmcnt<0>();
+    }
+    barrier();  // [P0] tiles t_beg (and t_beg + 1) landed (consumers' pieces too)
+    float mh[2] = {0.f, 0.f};
+    if (t_beg < t_end) {
+      gemm1(lds, s_nx, [](int) {});
+      mask_tail(s_nx, t_beg);
+#pragma unroll
+      for (int uh = 0; uh < 2; ++uh) {
+        float mx = fmaxf(fmaxf(s_nx[uh][0], s_nx[uh][1]), fmaxf(s_nx[uh][2], s_nx[uh][3]));
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        mh[uh] = mx;
+        if (g == 0) xmax[q * 32 + 16 * uh + c16] = mx;
+      }
+    }
+    barrier();  // [PX] the first tile's half maxima of both producers of the user group
+    if (t_beg < t_end) {
+#pragma unroll
+      for (int uh = 0; uh < 2; ++uh) {
+        m[uh] = fmaxf(fmaxf(mh[uh], xmax[(q ^ 2) * 32 + 16 * uh + c16]), bound[uh] - kOffsetSpan);
+        mL[uh] = m[uh] * kLog2e;
+      }
+      p_out(0);  // P(t_beg) -> parity 0
+    }
+    barrier();  // [P1]
+    for (int64_t t = t_beg; t < t_end; ++t) {
+      const int li = (int)(t - t_beg);
+      const int nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
+      wait_vmcnt<0>();
+      barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
+      if (t + 1 < t_end) {
+        const uint32_t soff_dma = tile_soff(t + 2);  // branch-free: past the split the pieces fill the free slot
+        gemm1(lds + nxt * TB, s_nx, [&](int ks) {
+          const int kk = ks - DEC5_PDMA_AT;
+          if (kk >= 0 && (kk & 1) == 0 && kk / 2 < PA) issue_piece(soff_dma, s_dma, kk / 2, kk == 0);
+        });
+        mask_tail(s_nx, t + 1);
+        p_out(par ^ 1);
+      }
+    }
+    wait_vmcnt<0>();
+#pragma unroll
+    for (int uh = 0; uh < 2; ++uh) {
+      lsum[uh] += __shfl_xor(lsum[uh], 16, 64);  // over the 4 lanes g of the user
+      lsum[uh] += __shfl_xor(lsum[uh], 32, 64);
+    }
+    barrier();  // [PE0]
+    if (g == 0) {
+      xmax[q * 32 + c16] = lsum[0];
+      xmax[q * 32 + 16 + c16] = lsum[1];
+    }
+    barrier();  // [E0]
+    if (ih == 0 && g == 0) {  // l = l(half 0) + l(half 1), in that order
+#pragma unroll
+      for (int uh = 0; uh < 2; ++uh) {
+        xm[ug * 64 + 16 * uh + c16] = lsum[uh] + xmax[(q ^ 2) * 32 + 16 * uh + c16];
+        xm[ug * 64 + 32 + 16 * uh + c16] = m[uh];
+      }
+    }
+    barrier();  // [E1]
+    return;
+  }
   if (role == 0) {
     // ------------------------------------------------------------------ producer ---
     // producer q owns users u0 + 16 uh + c16 (uh = q >> 1) over both item halves of every tile: U of
@@ -320,7 +477,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
 #endif
       if (!(DEC5_ABL & 2)) barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
       if (t + 1 < t_end) {
-        const bool dma = !(DEC5_ABL & 1) && t + 2 < t_end;
+        const bool dma = !(DEC5_ABL & 1) && (DEC5_BFREE || t + 2 < t_end);
 #if DEC5_RSTAGE
         const bool ld3 = t + 3 < t_end;
         gemm1(lds + nxt * TB, s_nx, [&](int ks) {
@@ -341,7 +498,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
 #endif
         mask_tail(s_nx, t + 1);
         if (!(DEC5_ABL & 4)) p_out(par ^ 1);
-        else lsum += s_nx[0][0] + s_nx[1][0];
+        else lsum += (s_nx[0][0] + s_nx[1][0] > 1e30f) ? 0.f : 1.f;  // keeps GEMM1 live, l >= 1: no user flagged
       }
     }
     wait_vmcnt<0>();
@@ -411,6 +568,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     }
   }
   barrier();  // [P0]
+  if (DEC5_P32) barrier();  // [PX]
   barrier();  // [P1]
   for (int64_t t = t_beg; t < t_end; ++t) {
     const int li = (int)(t - t_beg);
@@ -420,7 +578,8 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     // P(t) in GEMM2's B layout: user col, positions 8 h .. 8 h + 7 of k-steps 0 and 1
     const uint4 pf0 = *reinterpret_cast<const uint4*>(p_row(par, col) + 16 * h);
     const uint4 pf1 = *reinterpret_cast<const uint4*>(p_row(par, col) + 32 + 16 * h);
-    const bool dma = !(DEC5_ABL & 1) && t + 2 < t_end;
+    // DEC5_BFREE (A/B): issue the pieces of tile t + 2 unconditionally (past the split they fill the free slot)
+    const bool dma = !(DEC5_ABL & 1) && (DEC5_BFREE || t + 2 < t_end);
     const uint32_t soff_dma = tile_soff(dma ? t + 2 : t);
     gemm2(lds + cur * TB, pf0, pf1, [&](int i) {
       const int ii = i - DEC5_CDMA_AT;
@@ -435,6 +594,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     });
   }
   if constexpr (PB > 0) wait_vmcnt<0>();
+  if (DEC5_P32) barrier();  // [PE0]
   barrier();  // [E0]
   barrier();  // [E1] producers' (l, m) published
   if (!wave_active || t_beg >= t_end || user >= nb) return;
@@ -458,7 +618,385 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   }
 }
 
+// ===================================================================================== fp8, d = 768 ---
+// k_dec5_f8: version 5's producer / consumer structure for the block-scaled fp8 sweep
+// (v_mfma_scale_f32_32x32x64_f8f6f4, e4m3 operands; the image, the exponent rules and the fixed offset are
+// k_dec_fp8's in hvae_decoder.hip). A tile is 64 items (48 KiB of e4m3 at d = 768); 8 waves, two per SIMD;
+// for q = 0..3, (ug, hq) = (q & 1, q >> 1):
+//   * producer q (role 0): U of user group ug (32 users) over all of D as e4m3 (96 VGPRs; fp8 halves the
+//     bf16 producer's registers per user, so it keeps 32 users and reads only its item half of each tile);
+//     per tile: GEMM1 S^T of items 32 hq .. 32 hq + 31 (k-block hq of GEMM2) for its 32 users (12 MFMAs),
+//     the half's max, block exponent, 16 exponentials per lane and the packed e4m3 P half + exponent -> LDS;
+//   * consumer q + 4 (role 1): O of ug over D half hq (192 VGPRs), GEMM2 of tile t over both item halves
+//     (12 MFMAs, K = the tile's 64 items) with both P halves read back, each half's exponent as its k-block's
+//     B scale (the MFMA takes k-block b's scale from lane column + 32 b).
+// One barrier per tile as in the bf16 version; the first tile's max crosses once between the two producers
+// of a user group for their common offset m, and l = l(half 0) + l(half 1) at the end.
+namespace f8 {
+constexpr int TI = 64;
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+constexpr int TB8 = TI * D;                 // tile bytes (48 KiB)
+constexpr int PBY = 1024 + 256;            // per producer and parity: P half (64 lanes x 16 B) + exponents
+constexpr int LDS_BYTES = NS * TB8 + 2 * 4 * PBY + 4 * 64 * 4 + 2 * 64 * 4;
+static_assert(LDS_BYTES <= 160 * 1024, "k_dec5_f8 LDS");
+// = hvae_decoder.hip's f8_sw / f8_item_of at D = 768 (D % 256 == 0 form)
+__device__ __forceinline__ constexpr int sw(int it) {
+  return ((it & 1) << 1) | (((it >> 1) & 1) << 2) | (((it >> 3) & 1) << 3) | ((it >> 2) & 1);
+}
+__device__ __forceinline__ constexpr int item_of(int h, int j) {
+  return 32 * (j >> 4) + (j & 3) + 8 * ((j & 15) >> 2) + 4 * h;
+}
+__device__ __forceinline__ int pack4(float a, float b, float c, float d) {
+  const int lo = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, lo, true);
+}
+}  // namespace f8
+
+#ifndef DEC5F8_DMA_B
+#define DEC5F8_DMA_B 6  // of each (ug, hq)'s 12 LDS-DMA pieces per tile, how many the consumer issues
+#endif
+#ifndef DEC5F8_G1_AHEAD
+#define DEC5F8_G1_AHEAD 2
+#endif
+#ifndef DEC5F8_PRIO
+#define DEC5F8_PRIO 0  // A/B: static s_setprio 1 for 1 the consumers, 2 the producers
+#endif
+
+template <bool WITH_O>
+__global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, int64_t ldu,
+                                                 const unsigned char* __restrict__ T8, const int* __restrict__ e_exp,
+                                                 const float* __restrict__ e_maxnorm, int64_t nb, int64_t N,
+                                                 int splits, int64_t tiles_per_split, Out out) {
+  using namespace f8;
+  constexpr int DW = D / 2;      // GEMM2: dims owned by one consumer
+  constexpr int DB = DW / 32;    // GEMM2 d-blocks (12)
+  constexpr int KS = D / 64;     // GEMM1 k-steps (12)
+  constexpr int PW = 12;         // 1-KiB LDS-DMA pieces per (ug, hq) per tile
+  constexpr int PB = DEC5F8_DMA_B;
+  constexpr int PA = PW - PB;
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned char* pbuf = lds + NS * TB8;                                    // [2 par][4 producers][PBY]
+  float* xmax = reinterpret_cast<float*>(lds + NS * TB8 + 2 * 4 * PBY);    // [4 producers][64]
+  float* xm = xmax + 4 * 64;                                              // [2 ug][l 32 | m 32]
+
+  const int tid = threadIdx.x, lane = tid & 63, h = lane >> 5, col = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int role = w >> 2, q = w & 3;
+  const int ug = q & 1, hq = q >> 1;
+  const int split = blockIdx.x % splits;
+  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 64 + ug * 32;
+  // tile indices in 32 bits (N < 2^31, checked by the host) and wave-uniform in SGPRs
+  const int ntiles = __builtin_amdgcn_readfirstlane((int)((N + TI - 1) / TI));
+  const int t_beg = __builtin_amdgcn_readfirstlane((int)(split * tiles_per_split));
+  const int t_end = __builtin_amdgcn_readfirstlane((int)min((int64_t)ntiles, (int64_t)t_beg + tiles_per_split));
+  const int ke = *e_exp;  // scalars before any LDS-DMA is in flight
+  const int sa = 127 - ke;
+
+  // LDS-DMA: a plain copy of the tile, piece p = q * 12 + i at byte p * 1 KiB of tile and slot
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<unsigned char*>(T8), (short)0, ntiles * TB8, 0x00020000);
+  const int voff = lane * 16;
+  const uint32_t ring0 = lds_addr(lds) + (uint32_t)(q * PW * 1024);
+  auto issue_piece = [&](uint32_t soff, int slot_i, int i, bool fresh) {
+    const uint32_t lb = ring0 + (uint32_t)(slot_i * TB8 + i * 1024);
+    const uint32_t so = soff + (uint32_t)((q * PW + i) * 1024);
+    if (fresh)
+      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :: "s"(lb), "v"(voff), "s"(rsrc), "s"(so) : "memory");
+    else
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                   :: "s"(lb), "v"(voff), "s"(rsrc), "s"(so) : "memory");
+  };
+  auto tile_soff = [&](int t) { return (uint32_t)__builtin_amdgcn_readfirstlane(t * TB8); };
+  auto barrier = [&] {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+  auto p_slot = [&](int par, int pq) { return pbuf + (par * 4 + pq) * PBY; };
+  if ((DEC5F8_PRIO == 1 && role == 1) || (DEC5F8_PRIO == 2 && role == 0)) __builtin_amdgcn_s_setprio(1);
+
+  if (role == 0) {
+    // ------------------------------------------------------------------ producer ---
+    const float emax = *e_maxnorm;
+    // u over all of D: lane (col, h) holds u[64 ks + 32 h + j], j < 32, as e4m3 of u 2^ku (ku from the row)
+    const float* urow = U + min(u0 + col, nb - 1) * ldu + 32 * h;
+    float amax = 0.f, usq = 0.f;
+#pragma unroll 8
+    for (int q4 = 0; q4 < D / 8; ++q4) {
+      const float4 a = *reinterpret_cast<const float4*>(urow + 64 * (q4 >> 3) + 4 * (q4 & 7));
+      amax = fmaxf(amax, fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w))));
+      usq += (a.x * a.x + a.y * a.y) + (a.z * a.z + a.w * a.w);
+    }
+    amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+    usq += __shfl_xor(usq, 32, 64);
+    int eu = 0;
+    (void)frexpf(amax, &eu);
+    const int ku = amax > 0.f ? min(127, 8 - eu) : 0;
+    const int sbu = 127 - ku;
+    const float qu = ldexpf(1.f, ku);
+    // re-read the row for the packing pass: without this the loads of the first pass are kept live (CSE),
+    // 384 floats a lane, and spill
+    // (each k-step's address depends on the previous k-step's packed words, so the compiler cannot hoist all 96
+    // loads of this pass ahead of the packing: 384 floats a lane would spill)
+    i32x8 uf[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const float* up = urow + 64 * ks;
+      if (ks > 0) asm volatile("" : "+v"(up) : "v"(uf[ks - 1]));
+#pragma unroll
+      for (int q4 = 0; q4 < 8; ++q4) {
+        const float4 a = *reinterpret_cast<const float4*>(up + 4 * q4);
+        uf[ks][q4] = pack4(a.x * qu, a.y * qu, a.z * qu, a.w * qu);
+      }
+    }
+    const float bound = sqrtf(usq) * emax * 1.02f;
+    // GEMM1 A operand (k-step ks): item row 32 hq + col, chunks 4 ks + 2 h + {0, 1}
+    const int swc = sw(col);  // sw depends on the low 4 bits of the row only
+    const int rowA = (32 * hq + col) * D;
+    auto rdA = [&](const unsigned char* buf, int ks) {
+      const int ch = 4 * ks + 2 * h;
+      const unsigned char* row = buf + rowA;
+      const uint4 x = *reinterpret_cast<const uint4*>(row + 16 * (ch ^ swc));
+      const uint4 y = *reinterpret_cast<const uint4*>(row + 16 * ((ch + 1) ^ swc));
+      i32x8 r;
+      r[0] = (int)x.x; r[1] = (int)x.y; r[2] = (int)x.z; r[3] = (int)x.w;
+      r[4] = (int)y.x; r[5] = (int)y.y; r[6] = (int)y.z; r[7] = (int)y.w;
+      return r;
+    };
+    auto gemm1 = [&](const unsigned char* buf, f32x16& sv, auto&& fill) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sv[r] = 0.f;
+      constexpr int AH = DEC5F8_G1_AHEAD;
+      i32x8 ra[AH];
+#pragma unroll
+      for (int j = 0; j < AH; ++j) ra[j] = rdA(buf, j);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const i32x8 c = ra[ks % AH];
+        if (ks + AH < KS) ra[ks % AH] = rdA(buf, ks + AH);
+        sv = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, uf[ks], sv, 0, 0, 0, sa, 0, sbu);
+        fill(ks);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    // own half of tile t: items past N -> -inf; the half's max over its 32 items (every lane of a column)
+    auto half_max = [&](int t, f32x16& sv) {
+      if (t == ntiles - 1 && (N % TI) != 0) {
+        const int lim = (int)(N - (int64_t)t * TI) - 4 * h - 32 * hq;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sv[r] = ((r & 3) + 8 * (r >> 2) >= lim) ? -INFINITY : sv[r];
+      }
+      const float a0 = fmaxf(fmaxf(sv[0], sv[1]), sv[2]), a1 = fmaxf(fmaxf(sv[3], sv[4]), sv[5]);
+      const float a2 = fmaxf(fmaxf(sv[6], sv[7]), sv[8]), a3 = fmaxf(fmaxf(sv[9], sv[10]), sv[11]);
+      const float a4 = fmaxf(fmaxf(sv[12], sv[13]), fmaxf(sv[14], sv[15]));
+      const float mx = fmaxf(fmaxf(fmaxf(a0, a1), a2), fmaxf(a3, a4));
+      const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      return fmaxf(__uint_as_float(s2[0]), __uint_as_float(s2[1]));
+    };
+    float m = 0.f, mL = 0.f, lsum = 0.f;
+    auto tile_exp = [&](float mh) { return max(-119, min(127, (int)ceilf(__builtin_fmaf(mh, kLog2e, -mL)) - 8)); };
+    // the 16 exponentials of the half, their sum, the packed e4m3 P half and its exponent -> LDS parity par
+    auto p_out = [&](const f32x16& sv, float mh, int par) {
+      const int e = tile_exp(mh);
+      const float cE = mL + (float)e;
+      float qsum = 0.f;
+      int pk[4];
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        float qv[4];
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          qv[b] = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[4 * j4 + b], kLog2e, -cE));
+          qsum += qv[b];
+        }
+        pk[j4] = pack4(qv[0], qv[1], qv[2], qv[3]);
+      }
+      lsum += ldexpf(qsum, e);
+      reinterpret_cast<int4*>(p_slot(par, q))[lane] = make_int4(pk[0], pk[1], pk[2], pk[3]);
+      reinterpret_cast<int*>(p_slot(par, q) + 1024)[lane] = e;
+    };
+    f32x16 s_nx;
+    if (t_beg < t_end) {
+      for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg), 0, i, i == 0);
+      if (t_beg + 1 < t_end)
+        for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg + 1), 1, i, false);
+      wait_vmcnt<0>();
+    }
+    barrier();  // [P0] tiles t_beg (and t_beg + 1) landed (consumers' pieces too)
+    float mh = 0.f;
+    if (t_beg < t_end) {
+      gemm1(lds, s_nx, [](int) {});
+      mh = half_max(t_beg, s_nx);
+      if (lane < 32) xmax[q * 64 + lane] = mh;
+    }
+    barrier();  // [PX] the first tile's half maxima of both producers of the user group
+    if (t_beg < t_end) {
+      m = fmaxf(fmaxf(mh, xmax[(q ^ 2) * 64 + col]), bound - kOffsetSpan);
+      mL = m * kLog2e;
+      p_out(s_nx, mh, 0);  // P(t_beg) -> parity 0
+    }
+    barrier();  // [P1]
+    for (int t = t_beg; t < t_end; ++t) {
+      const int li = t - t_beg;
+      const int nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
+      wait_vmcnt<0>();
+      barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
+      if (t + 1 < t_end) {
+        // branch-free DMA: past the split the pieces land in the free slot s_dma (tiles past N read as 0)
+        const uint32_t soff_dma = tile_soff(t + 2);
+        gemm1(lds + nxt * TB8, s_nx, [&](int ks) {
+          if (ks < PA) issue_piece(soff_dma, s_dma, ks, ks == 0);
+        });
+        mh = half_max(t + 1, s_nx);
+        p_out(s_nx, mh, par ^ 1);
+      }
+    }
+    wait_vmcnt<0>();
+    const float lw = lsum + __shfl_xor(lsum, 32, 64);  // both lane halves of the column
+    barrier();  // [E0]
+    if (lane < 32) xmax[q * 64 + lane] = lw;
+    barrier();  // [E1]
+    if (hq == 0 && lane < 32) {  // l = l(half 0) + l(half 1), in that order; m
+      xm[ug * 64 + lane] = lw + xmax[(q ^ 2) * 64 + lane];
+      xm[ug * 64 + 32 + lane] = m;
+    }
+    barrier();  // [E2]
+    return;
+  }
+
+  // -------------------------------------------------------------------- consumer ---
+  const bool wave_active = u0 < nb;
+  const int dbase = hq * DW;
+  // GEMM2 A operand (d-block db of this wave's D half): four transposed reads c of items item_of(h, 8 c + qq)
+  // = it0 + 16 c, which share the chunk swizzle sw(it0); chunk ch = 2 x + g1 (x = dbase / 32 + db) sits at
+  // 16 (ch ^ sw) = loff[x & 7] - row part + 256 (x >> 3): eight lane offsets, the rest immediates
+  const int g1 = (lane >> 4) & 1, qq = (lane & 15) >> 1, pp = lane & 1;
+  const int it0 = item_of(h, qq);
+  const int tsw = sw(it0);
+  int loff[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) loff[k] = it0 * D + 8 * pp + 16 * ((2 * k + g1) ^ tsw);
+  auto rdB = [&](const unsigned char* buf, int db) {
+    i32x8 r;
+    const int x = dbase / 32 + db;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const i32x2 v = __builtin_amdgcn_ds_read_tr8_b64_v2i32(
+          (__attribute__((address_space(3))) i32x2*)(void*)(buf + loff[x & 7] + 256 * (x >> 3) + 16 * D * c));
+      r[2 * c] = v[0];
+      r[2 * c + 1] = v[1];
+    }
+    return r;
+  };
+  f32x16 o[WITH_O ? DB : 1];
+#pragma unroll
+  for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = 0.f;
+  auto gemm2 = [&](const unsigned char* buf, const i32x8& pf, int sbp, auto&& fill) {
+    if constexpr (WITH_O) {
+      constexpr int AH2 = 2;
+      i32x8 a[AH2];
+#pragma unroll
+      for (int j = 0; j < AH2; ++j) a[j] = rdB(buf, j);
+#pragma unroll
+      for (int db = 0; db < DB; ++db) {
+        const i32x8 c = a[db % AH2];
+        if (db + AH2 < DB) a[db % AH2] = rdB(buf, db + AH2);
+        o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
+        fill(db);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int db = 0; db < DB; ++db) fill(db);
+    }
+  };
+  if constexpr (PB > 0) {
+    if (t_beg < t_end) {
+      for (int i = PA; i < PW; ++i) issue_piece(tile_soff(t_beg), 0, i, i == PA);
+      if (t_beg + 1 < t_end)
+        for (int i = PA; i < PW; ++i) issue_piece(tile_soff(t_beg + 1), 1, i, false);
+      wait_vmcnt<0>();
+    }
+  }
+  barrier();  // [P0]
+  barrier();  // [PX]
+  barrier();  // [P1]
+  const int pq0 = ug, pq1 = ug + 2;  // the producers of this user group: item halves 0 and 1
+  for (int t = t_beg; t < t_end; ++t) {
+    const int li = t - t_beg;
+    const int cur = li % NS, s_dma = (li + 2) % NS, par = li & 1;
+    if constexpr (PB > 0) wait_vmcnt<0>();
+    barrier();  // [L]
+    // P(t): k-block 0 = item half 0 (elements 0..15), k-block 1 = half 1; lane half h supplies k-block h's scale
+    const int4 y0 = reinterpret_cast<const int4*>(p_slot(par, pq0))[lane];
+    const int4 y1 = reinterpret_cast<const int4*>(p_slot(par, pq1))[lane];
+    const int eh = reinterpret_cast<const int*>(p_slot(par, h ? pq1 : pq0) + 1024)[lane];
+    i32x8 pf;
+    pf[0] = y0.x; pf[1] = y0.y; pf[2] = y0.z; pf[3] = y0.w;
+    pf[4] = y1.x; pf[5] = y1.y; pf[6] = y1.z; pf[7] = y1.w;
+    const int sbp = 127 + eh;
+    const uint32_t soff_dma = tile_soff(t + 2);  // branch-free, as the producers'
+    gemm2(lds + cur * TB8, pf, sbp, [&](int db) {
+      if constexpr (PB > 0)
+        if (db < PB) issue_piece(soff_dma, s_dma, PA + db, db == 0);
+    });
+  }
+  if constexpr (PB > 0) wait_vmcnt<0>();
+  barrier();  // [E0]
+  barrier();  // [E1]
+  barrier();  // [E2] producers' (l, m) published
+  const int64_t user = u0 + col;
+  if (!wave_active || t_beg >= t_end || user >= nb) return;
+  const float ltot = xm[ug * 64 + col], mu = xm[ug * 64 + 32 + col];
+  const int64_t row = out.direct ? user : (int64_t)split * nb + user;
+  if (h == 0 && hq == 0) {
+    out.flag[row] = !(ltot >= kMinL);
+    if (out.direct) out.lse[user] = mu + logf(ltot);
+    else { out.m[row] = mu; out.l[row] = ltot; }
+  }
+  if (WITH_O) {
+    const float sc = out.direct ? 1.0f / ltot : 1.0f;
+#pragma unroll
+    for (int d = 0; d < (WITH_O ? DB : 1); ++d)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int dd = dbase + 32 * d + 8 * g4 + 4 * h;
+        *reinterpret_cast<float4*>(out.O + row * D + dd) =
+            make_float4(o[d][4 * g4] * sc, o[d][4 * g4 + 1] * sc, o[d][4 * g4 + 2] * sc, o[d][4 * g4 + 3] * sc);
+      }
+  }
+}
+
 }  // namespace dec5
+
+// Launch of the fp8 version-5 sweep (d = 768, 64 users per block, 64-item tiles, block b's split = b % splits)
+int dec5_f8_launch(bool with_o, const float* U, int64_t ldu, const unsigned char* T8, const int* ke,
+                   const float* enorm, int64_t nb, int64_t N, int splits, int64_t tiles_per_split, int64_t blocks,
+                   int* flag, float* m, float* l, float* O, float* lse, int direct, hipStream_t st) {
+  using namespace dec5;
+  static bool attr_set = false;
+  if (!attr_set) {
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec5_f8<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 f8::LDS_BYTES));
+    HVAE_HIP(hipFuncSetAttribute((const void*)k_dec5_f8<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 f8::LDS_BYTES));
+    attr_set = true;
+  }
+  Out o{flag, m, l, O, lse, direct};
+  if (with_o)
+    k_dec5_f8<true><<<(unsigned)blocks, 512, f8::LDS_BYTES, st>>>(U, ldu, T8, ke, enorm, nb, N, splits,
+                                                                   tiles_per_split, o);
+  else
+    k_dec5_f8<false><<<(unsigned)blocks, 512, f8::LDS_BYTES, st>>>(U, ldu, T8, ke, enorm, nb, N, splits,
+                                                                    tiles_per_split, o);
+  HVAE_LAUNCH_CHECK("k_dec5_f8");
+  return HVAE_OK;
+}
 
 // Launch of the version-5 sweep (d = 768, 64 users per block, blocks = user blocks x splits, block b's
 // split = b % splits): called by hvae_decoder.hip's dispatch with its plan and outputs.

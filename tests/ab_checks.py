@@ -1,8 +1,8 @@
 """Checks of the A/B variant kernels (not collected by default: no test_ prefix).
 
 The product libhvae.so runs one sweep per (dtype, d) and ignores the environment. The retired variants -- bf16
-versions 2, 3 and 4 at d = 768 beside version 5, the fp8 sweep with version 4's structure (k_dec4_f8) beside
-the D-split ring -- build only with -DHVAE_AB=1 (`make -C recommendation-system_amd lib-ab` ->
+versions 2, 3 and 4 at d = 768 beside version 5, the fp8 sweep with version 4's structure (k_dec4_f8) and the
+D-split ring beside the fp8 version 5 (k_dec5_f8) -- build only with -DHVAE_AB=1 (`make -C recommendation-system_amd lib-ab` ->
 build_var/libhvae_ab.so), where HVAE_DEC_* select them at plan time. tests/test_gpu_ab_variant.py runs this file
 in a subprocess with HVAE_LIB pointing at that build, so the variants keep their parity checks without being
 shipped.
@@ -73,13 +73,18 @@ def test_decoder_d768_versions_agree(ops, dev, monkeypatch):
         assert _maxrel(oa, o2) < 5e-3 and _maxrel(ra, r2) < 1e-5 and _maxrel(da, d2) < 5e-3, name
 
 
+@pytest.mark.parametrize("variant", ["F8V4", "ring"])
 @pytest.mark.parametrize("nb,N", [(64, 2000), (300, 5001), (7, 100), (130, 4000)])
-def test_decoder_fp8_v4_structure(ops, dev, nb, N, monkeypatch):
-    """k_dec4_f8 (HVAE_DEC_F8V4=1) against float64 on the quantised operands, inside the e4m3 envelope of
-    tests/test_gpu_fp8.py, and its fused train form equal to its fwd + bwd."""
+def test_decoder_fp8_v4_structure(ops, dev, nb, N, variant, monkeypatch):
+    """The retired fp8 d = 768 sweeps -- k_dec4_f8 (HVAE_DEC_F8V4=1) and the D-split ring (HVAE_DEC_F8V5=0) --
+    against float64 on the quantised operands, inside the e4m3 envelope of tests/test_gpu_fp8.py, and the
+    fused train form equal to fwd + bwd."""
     from test_gpu_fp8 import _image, _o_envelope, _quantised
     D = 768
-    monkeypatch.setenv("HVAE_DEC_F8V4", "1")
+    if variant == "F8V4":
+        monkeypatch.setenv("HVAE_DEC_F8V4", "1")
+    else:
+        monkeypatch.setenv("HVAE_DEC_F8V5", "0")
     E = torch.as_tensor(synth_embeddings(N, D, seed=N))
     g = torch.Generator().manual_seed(nb)
     U = torch.randn(nb, D, generator=g) * 3.0

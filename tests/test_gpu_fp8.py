@@ -97,7 +97,7 @@ def test_fp8_image_layout(ops, hip_device, N, D):
                                     (300, 5000, 256), (520, 20011, 384), (64, 2000, 768), (300, 5001, 768),
                                     (7, 100, 768)])
 def test_decoder_fp8(ops, hip_device, nb, N, D):
-    """The fp8 sweep (k_dec_fp8; at d = 768 the D-split ring) against float64 on the quantised operands.
+    """The fp8 sweep (k_dec_fp8; at d = 768 k_dec5_f8, producer / consumer waves) against float64 on the quantised operands.
     (k_dec4_f8, the version-4 structure it tied with, runs on the A/B variant: tests/ab_checks.py.)"""
     E = torch.as_tensor(synth_embeddings(N, D, seed=N))
     g = torch.Generator().manual_seed(nb)
