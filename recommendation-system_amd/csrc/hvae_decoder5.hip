@@ -1,7 +1,7 @@
-// hvae_decoder5.hip -- version 5 of the bf16 decoder sweep at d = 768: version 4's work, with the two
-// GEMMs on different waves (producer / consumer specialisation, two waves per SIMD).
+// hvae_decoder5.hip -- version 5 of the bf16 decoder sweep at d = 768 (k_dec5_bf16) and its fp8 form
+// (k_dec5_f8): GEMM1 and GEMM2 on different waves (producer / consumer specialisation, two waves per SIMD).
 //
-// Version 4 (hvae_decoder.hip, k_dec4_bf16) runs one wave per SIMD that does everything for its
+// Version 4 (hvae_decoder.hip, k_dec4_bf16, A/B build) runs one wave per SIMD that does everything for its
 // (user group ug, D half dh): the LDS-DMA of the next tiles, GEMM1 S^T = E_tile U^T for its 16 items
 // over all of D, the exponentials, and GEMM2 O^T += E_tile^T P^T for its D half. At one wave per
 // SIMD nothing covers the issue cost of the 12 LDS-DMA pieces per tile, nor any LDS-read latency an
@@ -9,20 +9,24 @@
 //
 // Here a block is 8 waves, two per SIMD (waves q and q + 4 share one: the workgroup's waves go to the
 // SIMDs in a cyclic order of 4). For q = 0..3, (ug, dh) = (q & 1, q >> 1):
-//   * producer wave q (role 0): U of user group ug over all of D (192 VGPRs); per tile: the LDS-DMA
-//     pieces of tile t + 2, GEMM1 of tile t + 1 for items 16 dh .. 16 dh + 15 (48 16x16x32 MFMAs),
-//     its 8 exponentials, its P half -> LDS;
+//   * producer wave q (role 0): U of user group ug's 32 users over all of D (192 VGPRs; DEC5_P32); per
+//     tile: its share of the LDS-DMA pieces of tile t + 2, GEMM1 of tile t + 1 for items 16 dh .. 16 dh + 15
+//     (48 16x16x32 MFMAs, one A read serving both 16-user halves), its 8 exponentials, its P piece -> LDS;
+//     DEC5_P32=0 (A/B) gives the producer 16 users over both item halves (96 VGPRs, twice the GEMM1 reads);
 //   * consumer wave q + 4 (role 1): O of user group ug over D half dh (192 VGPRs: the file is compiled
 //     with -mllvm -amdgpu-mfma-vgpr-form, so that no AGPR block is allocated beside the producer's
 //     VGPRs and each wave fits the 256 registers of two waves per SIMD); per tile: GEMM2 of tile t
-//     over both item halves (24 32x32x16 MFMAs) with P(t) read back from LDS.
+//     over both item halves (24 32x32x16 MFMAs) with P(t) read back from LDS, and its share of the pieces.
 // The SIMD's two instruction streams interleave in hardware, so one wave's DMA issue, LDS waits and
 // exponentials run under the other's MFMAs. The MFMA work per SIMD and tile is version 4's (1536
-// cycles), as are the LDS image, the DMA piece map, the P layout, the fixed-offset / flag rules and
-// the summation orders, so the outputs equal version 4's bitwise. One barrier per tile:
+// cycles), as are the LDS image, the DMA piece map, the P layout and the fixed-offset / flag rules. One
+// barrier per tile:
 //   [barrier: tile t + 1 landed, P(t) published, GEMM2(t - 1) done]
 //   producers: DMA of t + 2 into the slot GEMM2(t - 1) freed | GEMM1(t + 1) | softmax | P(t + 1) out
 //   consumers: GEMM2(t) from slot t % 3 and P(t)
+// What bounds it (profiles/r03_dec5_ablation_*.jsonl): the E stream. 64 users per 48-KiB tile
+// is 98 GB of L2 -> LDS traffic per Syn-10M sweep; the stream alone, waited per tile as the ring needs,
+// takes 9.4 ms of the 10.1-10.4, while the MFMAs alone take 6.9.
 #include <algorithm>
 #include <array>
 
@@ -83,14 +87,17 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // Timing-ablation builds only (scripts/build_variant5.sh; outputs invalid by construction), a bit mask:
 // 1 no LDS-DMA pieces in the loop (and no vmcnt waits), 2 no per-tile barrier, 4 no exponentials / P out,
 // 8 GEMM1 A operands not re-read from LDS, 16 GEMM2 E^T operands not re-read, 32 no GEMM1 MFMAs,
-// 64 no GEMM2 MFMAs
+// 64 no GEMM2 MFMAs, 128 LDS-DMA pieces issued but never waited for, 256 only the even pieces issued
 #ifndef DEC5_ABL
 #define DEC5_ABL 0
 #endif
-// A/B placement of the LDS-DMA pieces: producer piece i at GEMM1 k-step DEC5_PDMA_AT + 2 i, consumer piece i at
-// GEMM2 MFMA DEC5_CDMA_AT + 2 i
+// Placement of the LDS-DMA pieces: producer piece i at GEMM1 k-step DEC5_PDMA_AT + DEC5_DMA_STRIDE i, consumer piece
+// i at GEMM2 MFMA DEC5_CDMA_AT + DEC5_DMA_STRIDE i (as early as possible: the fill latency is the sweep's limit)
 #ifndef DEC5_PDMA_AT
-#define DEC5_PDMA_AT 1
+#define DEC5_PDMA_AT 0
+#endif
+#ifndef DEC5_DMA_STRIDE
+#define DEC5_DMA_STRIDE 1  // MFMA gaps between a wave's consecutive pieces (profiles/r03_dec5_dma_placement_ab.jsonl)
 #endif
 #ifndef DEC5_CDMA_AT
 #define DEC5_CDMA_AT 0
@@ -103,11 +110,18 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #ifndef DEC5_DMA_BURST
 #define DEC5_DMA_BURST 0  // A/B: each wave issues its pieces back to back at its first DMA slot
 #endif
+#ifndef DEC5_XMIX
+#define DEC5_XMIX 0  // A/B (below; +1.4 %)
+#endif
+#ifndef DEC5_ROT
+#define DEC5_ROT 0  // A/B (below; +72 %: the blocks of a split must stream their L2 lines in lockstep)
+#endif
 #ifndef DEC5_BFREE
 #define DEC5_BFREE 0  // A/B: branch-free LDS-DMA issue in the loop
 #endif
 #ifndef DEC5_P32
-#define DEC5_P32 0  // A/B: producers of 32 users over one item half (GEMM1 reads each tile twice, not four times)
+#define DEC5_P32 1  // producers of 32 users over one item half (GEMM1 reads each tile twice, not four times);
+                    // 0 (A/B): producers of 16 users over both halves
 #endif
 #ifndef DEC5_PRIO
 #define DEC5_PRIO 0  // A/B: static s_setprio 1 before the loop for 1 the consumer waves (4..7), 2 the producers
@@ -140,8 +154,18 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int role = w >> 2, q = w & 3;
   const int ug = q & 1, dh = q >> 1;
-  const int split = blockIdx.x % splits;
-  const int64_t u0 = (int64_t)(blockIdx.x / splits) * 64 + ug * 32;
+  // block -> (user block, split): by default split = b % splits, so with 4 splits each XCD (b % 8) streams one
+  // split; DEC5_XMIX (A/B) deals each XCD's blocks over all splits (b / 8 picks the split) when the grid allows
+  int split, ublk;
+  if (DEC5_XMIX && gridDim.x % (8 * splits) == 0) {
+    const int r = blockIdx.x / 8;
+    split = r % splits;
+    ublk = (r / splits) * 8 + (blockIdx.x & 7);
+  } else {
+    split = blockIdx.x % splits;
+    ublk = blockIdx.x / splits;
+  }
+  const int64_t u0 = (int64_t)ublk * 64 + ug * 32;
   const int64_t ntiles = (N + kTI - 1) / kTI;
   const int64_t t_beg = (int64_t)split * tiles_per_split;
   const int64_t t_end = min(ntiles, t_beg + tiles_per_split);
@@ -166,6 +190,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
 #define DEC5_POL ""
 #endif
   auto issue_piece = [&](uint32_t soff, int slot_i, int i, bool fresh) {
+    if ((DEC5_ABL & 256) && (i & 1)) return;
     const uint32_t lb = ring0 + (uint32_t)(slot_i * TB);
     const int p = q * PW + i;
     const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
@@ -186,6 +211,11 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     asm volatile("" ::: "memory");
   };
   auto p_row = [&](int par, int uu) { return pbuf + ((par * 2 + ug) * 32 + uu) * PST; };
+  // DEC5_ROT (A/B): the i-th piece a wave issues in a tile is piece (i + user block) mod its count, so that the
+  // blocks of one split, which stream the same tiles from their XCD's L2 in near lockstep, ask for different
+  // lines at a time
+  const int rot = __builtin_amdgcn_readfirstlane(ublk);
+  auto prot = [&](int i, int n) { return DEC5_ROT ? (i + rot) % n : i; };
   if ((DEC5_PRIO == 1 && role == 1) || (DEC5_PRIO == 2 && role == 0)) __builtin_amdgcn_s_setprio(1);
 
   if (DEC5_P32 && role == 0) {
@@ -311,7 +341,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
         const uint32_t soff_dma = tile_soff(t + 2);  // branch-free: past the split the pieces fill the free slot
         gemm1(lds + nxt * TB, s_nx, [&](int ks) {
           const int kk = ks - DEC5_PDMA_AT;
-          if (kk >= 0 && (kk & 1) == 0 && kk / 2 < PA) issue_piece(soff_dma, s_dma, kk / 2, kk == 0);
+          if (kk >= 0 && kk % DEC5_DMA_STRIDE == 0 && kk / DEC5_DMA_STRIDE < PA) issue_piece(soff_dma, s_dma, prot(kk / DEC5_DMA_STRIDE, PA), kk == 0);
         });
         mask_tail(s_nx, t + 1);
         p_out(par ^ 1);
@@ -473,7 +503,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
       const int li = (int)(t - t_beg);
       const int nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
 #if !DEC5_RSTAGE
-      if (!(DEC5_ABL & 1)) wait_vmcnt<0>();
+      if (!(DEC5_ABL & (1 | 128))) wait_vmcnt<0>();
 #endif
       if (!(DEC5_ABL & 2)) barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
       if (t + 1 < t_end) {
@@ -492,7 +522,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
             for (int i = 0; i < PA; ++i) issue_piece(soff_dma, s_dma, i, i == 0);
 #else
           const int kk = ks - DEC5_PDMA_AT;
-          if (dma && kk >= 0 && (kk & 1) == 0 && kk / 2 < PA) issue_piece(soff_dma, s_dma, kk / 2, kk == 0);
+          if (dma && kk >= 0 && kk % DEC5_DMA_STRIDE == 0 && kk / DEC5_DMA_STRIDE < PA) issue_piece(soff_dma, s_dma, prot(kk / DEC5_DMA_STRIDE, PA), kk == 0);
 #endif
         });
 #endif
@@ -573,7 +603,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   for (int64_t t = t_beg; t < t_end; ++t) {
     const int li = (int)(t - t_beg);
     const int cur = li % NS, s_dma = (li + 2) % NS, par = li & 1;
-    if constexpr (PB > 0) if (!(DEC5_ABL & 1)) wait_vmcnt<0>();
+    if constexpr (PB > 0) if (!(DEC5_ABL & (1 | 128))) wait_vmcnt<0>();
     if (!(DEC5_ABL & 2)) barrier();  // [L]
     // P(t) in GEMM2's B layout: user col, positions 8 h .. 8 h + 7 of k-steps 0 and 1
     const uint4 pf0 = *reinterpret_cast<const uint4*>(p_row(par, col) + 16 * h);
@@ -589,7 +619,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
           for (int k = 0; k < PB; ++k) issue_piece(soff_dma, s_dma, PA + k, k == 0);
 #else
       if constexpr (PB > 0)
-        if (dma && ii >= 0 && (ii & 1) == 0 && ii / 2 < PB) issue_piece(soff_dma, s_dma, PA + ii / 2, ii == 0);
+        if (dma && ii >= 0 && ii % DEC5_DMA_STRIDE == 0 && ii / DEC5_DMA_STRIDE < PB) issue_piece(soff_dma, s_dma, PA + prot(ii / DEC5_DMA_STRIDE, PB), ii == 0);
 #endif
     });
   }
