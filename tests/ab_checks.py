@@ -102,3 +102,25 @@ def test_decoder_fp8_v4_structure(ops, dev, nb, N, variant, monkeypatch):
     lse_t, O_t, rr, dU = ops.decoder_train(xd, U.to(dev), img, enorm, E.to(dev), 1.0 / nb, want_o=True)
     rr_b, dU_b = ops.decoder_bwd(xd, U.to(dev), E.to(dev), lse, O, 1.0 / nb)
     assert torch.equal(lse_t, lse) and torch.equal(O_t, O) and torch.equal(rr, rr_b) and torch.equal(dU, dU_b)
+
+
+@pytest.mark.parametrize("nb,N", [(300, 5001), (4096, 20_000), (129, 777)])
+def test_decoder_d384_v5w_agrees_v2(ops, dev, nb, N, monkeypatch):
+    """The d = 384 128-user producer / consumer sweep (k_dec5w_bf16, the product's) against version 2's DS = 1 sweep
+    (HVAE_DEC_V5W=0): the same bf16 operands, P rounded to bf16 in both; only fp32 summation order differs."""
+    D = 384
+    g = torch.Generator(device=dev).manual_seed(nb)
+    E = torch.randn(N, D, device=dev, generator=g)
+    E /= E.norm(dim=1, keepdim=True)
+    U = torch.randn(nb, D, device=dev, generator=g)
+    U *= 4.0 / U.norm(dim=1, keepdim=True)
+    xd = ops.csr_from_scipy(synth_csr(nb, N, lam=15.0, seed=3), dev)
+    img = ops.decoder_image(E)
+    enorm = ops.row_norm_max(img)
+    out = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("HVAE_DEC_V5W", v)
+        out[v] = ops.decoder_train(xd, U, img, enorm, E, 1.0 / nb, want_o=True)
+    (la, oa, ra, da), (lb, ob, rb, db) = out["1"], out["0"]
+    assert (la - lb).abs().max() < 1e-4
+    assert _maxrel(oa, ob) < 5e-3 and _maxrel(ra, rb) < 1e-5 and _maxrel(da, db) < 5e-3

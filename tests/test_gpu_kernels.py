@@ -228,8 +228,10 @@ def test_reparam_kl(ops, hip_device):
 # --------------------------------------------------------------- decoder ---
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
 @pytest.mark.parametrize("nb,N,D", [(3, 50, 384), (64, 890, 384), (200, 12101, 384), (130, 1000, 128),
-                                    (17, 333, 64), (300, 5000, 256)])
+                                    (17, 333, 64), (300, 5000, 256), (129, 777, 384), (300, 5001, 384)])
 def test_decoder(ops, hip_device, dtype, nb, N, D):
+    """Every sweep against float64 (bf16: on the bf16-rounded operands). At d = 384 batches above 64 run the
+    128-user producer / consumer sweep (k_dec5w_bf16: partial last user block, item tails, 1 .. 8 splits)."""
     _check_decoder(ops, hip_device, dtype, nb, N, D)
 
 
@@ -261,13 +263,15 @@ def _check_decoder(ops, hip_device, dtype, nb, N, D):
     assert torch.allclose(lse2, lse, rtol=0, atol=1e-5)
 
 
-def test_decoder_large_norm_fixup(ops, hip_device):
-    """|u| in the hundreds: the fixed-offset bf16 path must flag and fix underflowing users."""
-    N, D = 4000, 128
+@pytest.mark.parametrize("D,reps", [(128, 1), (384, 12)])
+def test_decoder_large_norm_fixup(ops, hip_device, D, reps):
+    """|u| in the hundreds: the fixed-offset bf16 path must flag and fix underflowing users (d = 384 with 96
+    users: the 128-user sweep's flags)."""
+    N = 4000
     E = torch.as_tensor(synth_embeddings(N, D, seed=9))
     g = torch.Generator().manual_seed(1)
-    U = torch.randn(8, D, generator=g)
-    U = U / U.norm(dim=1, keepdim=True) * torch.tensor([1, 10, 50, 100, 200, 400, 800, 1500.0])[:, None]
+    U = torch.randn(8 * reps, D, generator=g)
+    U = U / U.norm(dim=1, keepdim=True) * torch.tensor([1, 10, 50, 100, 200, 400, 800, 1500.0]).repeat(reps)[:, None]
     Ek = ops.decoder_image(E.to(hip_device))
     lse, O = ops.decoder_fwd(U.to(hip_device), Ek, ops.row_norm_max(Ek))
     S = U.bfloat16().double() @ Ek.bf16.float().cpu().double().t()
@@ -275,12 +279,13 @@ def test_decoder_large_norm_fixup(ops, hip_device):
     rel = ((lse.double().cpu() - torch.logsumexp(S, 1)).abs() / torch.logsumexp(S, 1).abs().clamp(min=1))
     assert rel.max() < 2e-3
     # the fused train form recomputes flagged users inside its finalize: same lse, O-derived dU
-    X = synth_csr(8, N, lam=5.0, seed=2)
+    X = synth_csr(8 * reps, N, lam=5.0, seed=2)
     xd = ops.csr_from_scipy(X, hip_device)
     Ed = E.to(hip_device)
-    lse_t, O_t, _, dU_t = ops.decoder_train(xd, U.to(hip_device), Ek, ops.row_norm_max(Ek), Ed, 0.125, want_o=True)
+    sc = 1.0 / (8 * reps)
+    lse_t, O_t, _, dU_t = ops.decoder_train(xd, U.to(hip_device), Ek, ops.row_norm_max(Ek), Ed, sc, want_o=True)
     assert torch.equal(lse_t, lse) and torch.equal(O_t, O)
-    _, _, _, dU_n = ops.decoder_train(xd, U.to(hip_device), Ek, ops.row_norm_max(Ek), Ed, 0.125)
+    _, _, _, dU_n = ops.decoder_train(xd, U.to(hip_device), Ek, ops.row_norm_max(Ek), Ed, sc)
     assert torch.equal(dU_n, dU_t)
 
 
@@ -303,7 +308,8 @@ def test_decoder_bwd_sparse(ops, hip_device):
 
 
 @pytest.mark.parametrize("dtype", ["f32", "bf16"])
-@pytest.mark.parametrize("nb,N,D", [(40, 700, 384), (64, 12101, 384), (5, 3000, 128), (256, 2000, 64)])
+@pytest.mark.parametrize("nb,N,D", [(40, 700, 384), (64, 12101, 384), (5, 3000, 128), (256, 2000, 64),
+                                    (130, 4001, 384)])
 def test_decoder_train_fused(ops, hip_device, dtype, nb, N, D):
     _check_decoder_train_fused(ops, hip_device, dtype, nb, N, D)
 
