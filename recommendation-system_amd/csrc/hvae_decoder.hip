@@ -2954,9 +2954,10 @@ int dec5_launch(bool with_o, const float* U, int64_t ldu, const void* E, const f
 int dec5w_launch(bool with_o, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                  int splits, int64_t tiles_per_split, int64_t blocks, int* flag, float* m, float* l, float* O,
                  float* lse, int direct, hipStream_t st);
-// the d = 384 bf16 sweep of large batches (one DS = 1 block of version 2 = 128 users) runs version 5's producer /
-// consumer split with 128 users per block (k_dec5w_bf16); HVAE_DEC_V5W=0 keeps version 2 (A/B)
-static bool v5w_supported(int64_t D) { return D == 384 && env_int("HVAE_DEC_V5W", 1) != 0; }
+// HVAE_DEC_V5W=1 (A/B build) runs the d = 384 bf16 sweep of large batches as version 5's producer / consumer split
+// with 128 users per block (k_dec5w_bf16). It passes the decoder parity tests but measured slower than version 2's
+// DS = 1 sweep at Syn-1M (579-645 vs 520-531 us, profiles/r03_dec5w_vs_v2_syn1m.jsonl), so version 2 stays
+static bool v5w_supported(int64_t D) { return D == 384 && env_int("HVAE_DEC_V5W", 0) != 0; }
 int dec5_f8_launch(bool with_o, const float* U, int64_t ldu, const unsigned char* T8, const int* ke,
                    const float* enorm, int64_t nb, int64_t N, int splits, int64_t tiles_per_split, int64_t blocks,
                    int* flag, float* m, float* l, float* O, float* lse, int direct, hipStream_t st);
@@ -3172,9 +3173,11 @@ static int dispatch(int dtype, const float* U, int64_t ldu, const void* E, const
                               p.tiles_per_split, p.blocks, o.flag, o.m, o.l, o.O, o.lse, o.direct, st);
       default: break;
     }
+#if HVAE_AB
   } else if (dtype == HVAE_BF16 && p.v2 && p.ds == 1 && !p.v4 && D == 384 && v5w_supported(D)) {
     return dec5w_launch(WO, U, ldu, E, enorm, nb, N, p.splits, p.tiles_per_split, p.blocks, o.flag, o.m, o.l, o.O,
                         o.lse, o.direct, st);
+#endif
   } else if (dtype == HVAE_BF16 && p.v5 && D == 768) {
     return dec5_launch(WO, U, ldu, E, enorm, nb, N, p.splits, p.tiles_per_split, p.blocks, o.flag, o.m, o.l, o.O,
                        o.lse, o.direct, st);

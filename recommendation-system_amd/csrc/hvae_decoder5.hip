@@ -648,6 +648,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   }
 }
 
+#if HVAE_AB  // measured slower than version 2 at d = 384: A/B build only
 // ============================================================================ bf16, d = 384, 128 users ---
 // k_dec5w_bf16: version 5's producer / consumer split at d = 384 with 128 users per block (Syn-1M, configs[2]).
 // At d = 384 a user's U is 48 VGPRs and its O 96, so a block can hold four 32-user groups: producer q (role 0)
@@ -949,6 +950,8 @@ __global__ void __launch_bounds__(512) k_dec5w_bf16(const float* __restrict__ U,
       }
   }
 }
+
+#endif  // HVAE_AB
 
 // ===================================================================================== fp8, d = 768 ---
 // k_dec5_f8: version 5's producer / consumer structure for the block-scaled fp8 sweep
@@ -1306,6 +1309,7 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
 
 }  // namespace dec5
 
+#if HVAE_AB
 // Launch of the d = 384 version-5 sweep with 128 users per block (block b's split = b % splits)
 int dec5w_launch(bool with_o, const float* U, int64_t ldu, const void* E, const float* enorm, int64_t nb, int64_t N,
                  int splits, int64_t tiles_per_split, int64_t blocks, int* flag, float* m, float* l, float* O,
@@ -1329,6 +1333,8 @@ int dec5w_launch(bool with_o, const float* U, int64_t ldu, const void* E, const 
   HVAE_LAUNCH_CHECK("k_dec5w_bf16");
   return HVAE_OK;
 }
+
+#endif  // HVAE_AB
 
 // Launch of the fp8 version-5 sweep (d = 768, 64 users per block, 64-item tiles, block b's split = b % splits)
 int dec5_f8_launch(bool with_o, const float* U, int64_t ldu, const unsigned char* T8, const int* ke,

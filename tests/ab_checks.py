@@ -106,8 +106,9 @@ def test_decoder_fp8_v4_structure(ops, dev, nb, N, variant, monkeypatch):
 
 @pytest.mark.parametrize("nb,N", [(300, 5001), (4096, 20_000), (129, 777)])
 def test_decoder_d384_v5w_agrees_v2(ops, dev, nb, N, monkeypatch):
-    """The d = 384 128-user producer / consumer sweep (k_dec5w_bf16, the product's) against version 2's DS = 1 sweep
-    (HVAE_DEC_V5W=0): the same bf16 operands, P rounded to bf16 in both; only fp32 summation order differs."""
+    """The d = 384 128-user producer / consumer sweep (k_dec5w_bf16, HVAE_DEC_V5W=1, A/B only: slower) against
+    version 2's DS = 1 sweep (the product's): the same bf16 operands, P rounded to bf16 in both; only fp32
+    summation order differs."""
     D = 384
     g = torch.Generator(device=dev).manual_seed(nb)
     E = torch.randn(N, D, device=dev, generator=g)

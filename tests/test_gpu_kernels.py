@@ -230,8 +230,8 @@ def test_reparam_kl(ops, hip_device):
 @pytest.mark.parametrize("nb,N,D", [(3, 50, 384), (64, 890, 384), (200, 12101, 384), (130, 1000, 128),
                                     (17, 333, 64), (300, 5000, 256), (129, 777, 384), (300, 5001, 384)])
 def test_decoder(ops, hip_device, dtype, nb, N, D):
-    """Every sweep against float64 (bf16: on the bf16-rounded operands). At d = 384 batches above 64 run the
-    128-user producer / consumer sweep (k_dec5w_bf16: partial last user block, item tails, 1 .. 8 splits)."""
+    """Every sweep against float64 (bf16: on the bf16-rounded operands): partial last user blocks, item tails,
+    1 .. 8 splits."""
     _check_decoder(ops, hip_device, dtype, nb, N, D)
 
 
@@ -266,7 +266,7 @@ def _check_decoder(ops, hip_device, dtype, nb, N, D):
 @pytest.mark.parametrize("D,reps", [(128, 1), (384, 12)])
 def test_decoder_large_norm_fixup(ops, hip_device, D, reps):
     """|u| in the hundreds: the fixed-offset bf16 path must flag and fix underflowing users (d = 384 with 96
-    users: the 128-user sweep's flags)."""
+    users: the DS = 1 sweep's flags)."""
     N = 4000
     E = torch.as_tensor(synth_embeddings(N, D, seed=9))
     g = torch.Generator().manual_seed(1)
