@@ -11,6 +11,8 @@
 // Reference: src/ml/model.py:103-127 (_build_encoder), 138-155 (encode).
 #include <algorithm>
 
+#include <type_traits>
+
 #include "hvae_common.h"
 
 namespace hvae {
@@ -100,28 +102,36 @@ __global__ void __launch_bounds__(256) k_encoder_sparse_fwd(
     const int my_j = (lane < n) ? col_idx[base + lane] : 0;
     const float my_x = (lane < n) ? vals[base + lane] : 0.f;
     int t = 0;
-    for (; t + 4 <= n; t += 4) {
-      int j[4];
-      float x[4];
+    // R item rows in flight per step (8, then 4, then one at a time); the sum runs in entry order either way
+    auto rows = [&](auto rc) {
+      constexpr int R = decltype(rc)::value;
+      int j[R];
+      float x[R];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < R; ++u) {
         j[u] = __builtin_amdgcn_readlane(my_j, t + u);
         x[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), t + u));
       }
+      float4 w[NV][R];
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         const int64_t e = 4 * (int64_t)(lane + 64 * k);
-        if (e >= H) continue;
-        float4 w[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) w[u] = *reinterpret_cast<const float4*>(w1t + (int64_t)j[u] * H + e);
+        for (int u = 0; u < R; ++u)
+          w[k][u] = e < H ? *reinterpret_cast<const float4*>(w1t + (int64_t)j[u] * H + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          acc[k].x += x[u] * w[u].x; acc[k].y += x[u] * w[u].y;
-          acc[k].z += x[u] * w[u].z; acc[k].w += x[u] * w[u].w;
+      for (int k = 0; k < NV; ++k) {
+        if (4 * (int64_t)(lane + 64 * k) >= H) continue;
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          acc[k].x += x[u] * w[k][u].x; acc[k].y += x[u] * w[k][u].y;
+          acc[k].z += x[u] * w[k][u].z; acc[k].w += x[u] * w[k][u].w;
         }
       }
-    }
+    };
+    for (; t + 8 <= n; t += 8) rows(std::integral_constant<int, 8>{});
+    for (; t + 4 <= n; t += 4) rows(std::integral_constant<int, 4>{});
     for (; t < n; ++t) {
       const int j = __builtin_amdgcn_readlane(my_j, t);
       const float x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(my_x), t));
@@ -921,34 +931,35 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
               if (col < H) *reinterpret_cast<float4*>(dst + col) = acc[k];
             }
           } else {
-            float* dst = part + (int64_t)(run_lo == 0 ? 2 * c : 2 * c + 1) * H;
+            const __amdgpu_buffer_rsrc_t prs = coherent_rsrc(part);
+            const uint32_t dst = (uint32_t)((run_lo == 0 ? 2 * c : 2 * c + 1) * H) * 4u;
 #pragma unroll
             for (int k = 0; k < NV; ++k) {
               const int64_t col = 4 * (int64_t)(lane + 64 * k);
-              if (col < H) {
-                st_shared_f(dst + col, acc[k].x); st_shared_f(dst + col + 1, acc[k].y);
-                st_shared_f(dst + col + 2, acc[k].z); st_shared_f(dst + col + 3, acc[k].w);
-              }
+              if (col < H) st_sc1_f4(prs, dst + (uint32_t)col * 4u, acc[k]);
             }
             __builtin_amdgcn_s_waitcnt(0);  // this wave's partial has reached the coherence point
             const int ca = beg / CH, cb = (end - 1) / CH;
             int tk = 0;
-            // acq_rel: every chunk's release publishes its partial before its ticket, and the last taker's acquire
-            // orders its partial loads after all of them (HIP memory model, agent scope)
-            if (lane == 0) tk = __hip_atomic_fetch_add(ticket + si, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+            // The hand-off is MI355X_MICROARCH's measured valid form (sc1 16-B stores, every storing wave's
+            // vmcnt(0) before its agent-scope ticket add, the last taker's sc1 16-B loads after its add returned);
+            // the last taker adds an agent acquire (an L1 invalidate, no L2 writeback) so the ordering holds under
+            // the HIP memory model too. An acq_rel add costs every chunk an L2 writeback: Syn-1M
+            // rowgrad_apply 50 -> 96 us (profiles/r03_full_bench_syn1m.json).
+            if (lane == 0) tk = __hip_atomic_fetch_add(ticket + si, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             tk = __shfl(tk, 0, 64);
             if (tk == cb - ca) {  // the segment's last chunk to finish: its partials, in chunk order
-              const float* first = part + (int64_t)(2 * ca + (beg % CH == 0 ? 0 : 1)) * H;
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+              const __amdgpu_buffer_rsrc_t prs = coherent_rsrc(part);
+              const uint32_t first = (uint32_t)((2 * ca + (beg % CH == 0 ? 0 : 1)) * H) * 4u;
 #pragma unroll
               for (int k = 0; k < NV; ++k) {
                 const int64_t col = 4 * (int64_t)(lane + 64 * k);
                 if (col >= H) continue;
-                float4 sum = make_float4(ld_shared_f(first + col), ld_shared_f(first + col + 1),
-                                         ld_shared_f(first + col + 2), ld_shared_f(first + col + 3));
+                float4 sum = ld_sc1_f4(prs, first + (uint32_t)col * 4u);
                 for (int cc = ca + 1; cc <= cb; ++cc) {
-                  const float* pc = part + (int64_t)(2 * cc) * H + col;
-                  sum.x += ld_shared_f(pc); sum.y += ld_shared_f(pc + 1);
-                  sum.z += ld_shared_f(pc + 2); sum.w += ld_shared_f(pc + 3);
+                  const float4 v = ld_sc1_f4(prs, (uint32_t)((2 * cc) * H + col) * 4u);
+                  sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
                 }
                 *reinterpret_cast<float4*>(out_rows + (int64_t)si * H + col) = sum;
               }

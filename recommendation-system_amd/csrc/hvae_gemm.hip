@@ -159,6 +159,62 @@ __device__ __forceinline__ void gemm_finish(const GemmP& g, const f32x4 (&acc)[B
     return;
   }
   // ---- split-K: publish the partial tile, the last arrival reduces
+  const unsigned tile = by * g.gx + bx;
+  if (M % BM == 0 && N % BN == 0) {
+    // whole tiles: the partials in fragment order, one 16-B coherent store per accumulator (a dword sc1 store
+    // costs ~6x a dwordx4 per byte), read back by the same thread of the last block in split order -- the same
+    // sums in the same order as the element-order slab below
+    constexpr int FR = IM * JN * 4;
+    const int64_t ntile = (int64_t)g.gx * g.gy;
+    const __amdgpu_buffer_rsrc_t srs = coherent_rsrc(slab);
+    const uint32_t mine = (uint32_t)((((int64_t)bz * ntile + tile) * (BM * BN) + (int64_t)t * FR) * 4);
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+        st_sc1_f4(srs, mine + 16u * (i * JN + j), make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]));
+    if (!last_block_arrives(&tickets[tile], g.gz)) return;
+    const int S = (int)g.gz;
+    f32x4 sum[IM][JN];
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum[i][j][r] = 0.f;
+    for (int z = 0; z < S; ++z) {
+      const uint32_t src = (uint32_t)((((int64_t)z * ntile + tile) * (BM * BN) + (int64_t)t * FR) * 4);
+      float4 v[IM][JN];  // every load of the split in flight together
+#pragma unroll
+      for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j) v[i][j] = ld_sc1_f4(srs, src + 16u * (i * JN + j));
+#pragma unroll
+      for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j) {
+          sum[i][j][0] += v[i][j].x; sum[i][j][1] += v[i][j].y; sum[i][j][2] += v[i][j].z; sum[i][j][3] += v[i][j].w;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < IM; ++i)
+#pragma unroll
+      for (int j = 0; j < JN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = m0 + wm + i * 16 + 4 * (lane >> 4) + r;
+          const int64_t col = n0 + wn + j * 16 + (lane & 15);
+          float c = alpha * sum[i][j][r];
+          if (beta != 0.f) c += beta * C[row * ldc + col];
+          C[row * ldc + col] = epi_apply(ep, step, row, col, N, ldc, c, C);
+        }
+    if (ep.opa_rowsum && bx == 0 && t < BM && m0 + t < M) {
+      float r = 0.f;
+      for (int z = 0; z < S; ++z) r += ld_shared_f(&slab[(int64_t)S * M * N + (int64_t)z * M + m0 + t]);
+      ep.opa_rowsum[m0 + t] = alpha * r;
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < IM; ++i)
 #pragma unroll
@@ -169,7 +225,6 @@ __device__ __forceinline__ void gemm_finish(const GemmP& g, const f32x4 (&acc)[B
         const int64_t col = n0 + wn + j * 16 + (lane & 15);
         if (row < M && col < N) st_shared_f(&slab[((int64_t)bz * M + row) * N + col], acc[i][j][r]);
       }
-  const unsigned tile = by * g.gx + bx;
   if (!last_block_arrives(&tickets[tile], g.gz)) return;
   // the tile's elements per thread: one coherent load each per split, all in flight together
   constexpr int Q = BM * BN / 256;
