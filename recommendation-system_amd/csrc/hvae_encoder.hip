@@ -1163,6 +1163,15 @@ extern "C" size_t hvae_w1_rowgrad_workspace(int64_t n_items) {
   return (size_t)(cdiv(n_items, kScanItemsPerBlock) + 1) * sizeof(int64_t);  // look-back words + block counter
 }
 
+namespace hvae {
+int rg_plan_sorted(const hvae_csr_batch* x, const hvae_rowgrad* rg, hipStream_t st);
+int64_t rgsort_scratch_floats(int64_t cap, int64_t N);
+}  // namespace hvae
+static bool env_flag_ab(const char* name, int dflt) {
+  const char* v = ab_getenv(name);
+  return (v && *v) ? atoi(v) != 0 : dflt != 0;
+}
+
 static int rg_check(const hvae_rowgrad* rg) {
   HVAE_REQUIRE(rg && rg->cnt && rg->slot_of && rg->item_of && rg->seg_off && rg->fill && rg->contrib_row &&
                    rg->contrib_val && rg->rows && rg->n_unique,
@@ -1196,6 +1205,12 @@ extern "C" int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad*
                                         rg->contrib_slot, rg->n_unique);
     HVAE_LAUNCH_CHECK("k_rg_plan_small");
     return HVAE_OK;
+  }
+  // the sorted plan (hvae_rgsort.hip): one stable radix sort instead of per-item atomics; HVAE_RG_SORTED=0 (A/B
+  // build) keeps the atomic plan below, which also runs when the scratch cannot hold the sort
+  if (env_flag_ab("HVAE_RG_SORTED", 1)) {
+    const int rc = rg_plan_sorted(x, rg, st);
+    if (rc != HVAE_ERR_UNSUPPORTED) return rc;
   }
   const unsigned rgrid = (unsigned)cdiv(x->nb, 4);
   const bool small_scan = N <= kSmallScanItems;
@@ -1231,7 +1246,9 @@ static int rg_chunk(int64_t cap) {
 }
 
 extern "C" int64_t hvae_rowgrad_part_floats(int64_t cap, int64_t H) {
-  return std::max<int64_t>(2 * (cap / rg_chunk(cap) + 1) * H, 2 * cap);
+  // the apply's chunk partials, the atomic plan's long-segment staging, or the sorted plan's scratch (keys of up
+  // to 2^30 items: the largest rocPRIM temporary)
+  return std::max<int64_t>({2 * (cap / rg_chunk(cap) + 1) * H, 2 * cap, rgsort_scratch_floats(cap, 1ll << 30)});
 }
 
 extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowgrad* rg, void* stream) {

@@ -125,3 +125,38 @@ def test_decoder_d384_v5w_agrees_v2(ops, dev, nb, N, monkeypatch):
     (la, oa, ra, da), (lb, ob, rb, db) = out["1"], out["0"]
     assert (la - lb).abs().max() < 1e-4
     assert _maxrel(oa, ob) < 5e-3 and _maxrel(ra, rb) < 1e-5 and _maxrel(da, db) < 5e-3
+
+
+@pytest.mark.parametrize("nb,N,lam,hot", [(4096, 100_000, 15.0, 300), (300, 2000, 8.0, 100), (40000, 3000, 1.0, 6000),
+                                         (2000, 1_000_003, 15.0, 0), (32768, 1_000_000, 15.0, 0)])
+def test_rowgrad_sorted_plan_equals_atomic_plan(ops, dev, nb, N, lam, hot, monkeypatch):
+    """The radix-sort plan (hvae_rgsort.hip, the product's) against the atomic plan (HVAE_RG_SORTED=0): every
+    output the apply and the lazy Adam read is bitwise equal (slots, segments, contributions and their slots,
+    slot_of at the batch's items), and so are the gradient rows."""
+    import numpy as np
+    import scipy.sparse as sp
+    X = synth_csr(nb, N, lam=lam, seed=nb)
+    if hot:
+        X = X.tolil()
+        X[:hot, 0] = 1.0
+        X = sp.csr_matrix(X)
+    H = 64
+    da = torch.randn(nb, H, generator=torch.Generator().manual_seed(2)).to(dev)
+    xd = ops.csr_from_scipy(X, dev)
+    outs = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("HVAE_RG_SORTED", v)
+        rg = ops.RowGradBuffers(N, H, int(X.nnz), dev)
+        ops.w1_rowgrad(xd, da, rg)
+        nu = int(rg.n_unique.item())
+        tot = int(rg.seg_off[nu].item())
+        items = rg.item_of[:nu].long()
+        outs[v] = (nu, tot, rg.item_of[:nu].clone(), rg.seg_off[: nu + 1].clone(), rg.contrib_row[:tot].clone(),
+                   rg.contrib_val[:tot].clone(), rg.contrib_slot[:tot].clone(), rg.slot_of[items].clone(),
+                   rg.rows[:nu].clone(), int(rg.cnt.abs().sum()), int(rg.fill.abs().sum()))
+    a, b = outs["1"], outs["0"]
+    assert a[0] == b[0] and a[1] == b[1] == X.nnz
+    for x, y in zip(a[2:9], b[2:9]):
+        assert torch.equal(x, y)
+    assert a[9] == 0 and a[10] == 0
+    np.testing.assert_array_equal(a[2].cpu().numpy(), np.unique(X.indices))
