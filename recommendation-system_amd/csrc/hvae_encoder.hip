@@ -1167,9 +1167,9 @@ namespace hvae {
 int rg_plan_sorted(const hvae_csr_batch* x, const hvae_rowgrad* rg, hipStream_t st);
 int64_t rgsort_scratch_floats(int64_t cap, int64_t N);
 }  // namespace hvae
-static bool env_flag_ab(const char* name, int dflt) {
+static int env_flag_ab(const char* name, int dflt) {
   const char* v = ab_getenv(name);
-  return (v && *v) ? atoi(v) != 0 : dflt != 0;
+  return (v && *v) ? (atoi(v) != 0 ? 1 : 0) : dflt;
 }
 
 static int rg_check(const hvae_rowgrad* rg) {
@@ -1206,9 +1206,14 @@ extern "C" int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad*
     HVAE_LAUNCH_CHECK("k_rg_plan_small");
     return HVAE_OK;
   }
-  // the sorted plan (hvae_rgsort.hip): one stable radix sort instead of per-item atomics; HVAE_RG_SORTED=0 (A/B
-  // build) keeps the atomic plan below, which also runs when the scratch cannot hold the sort
-  if (env_flag_ab("HVAE_RG_SORTED", 1)) {
+  // the sorted plan (hvae_rgsort.hip): one stable radix sort instead of per-item atomics, for the large batches of
+  // data parallelism's union (W x B rows): 3.6x faster at W = 8 (782 -> 216 us), 1.5x at one rank's batch (121
+  // -> 79 us, profiles/r03_rowgrad_sorted_vs_atomic.jsonl). Below kSortedPlanMinCap entries the atomic plan stays:
+  // the sort's 15 launches against the atomic plan's 4 make the captured step's host-side replay outlast the GPU
+  // at Syn-1M (1.20 -> 1.30 ms per step). HVAE_RG_SORTED (A/B build): 1 always sorted, 0 never.
+  constexpr int64_t kSortedPlanMinCap = 150000;
+  const int sorted_ab = env_flag_ab("HVAE_RG_SORTED", -1);
+  if (sorted_ab == 1 || (sorted_ab == -1 && rg->cap >= kSortedPlanMinCap)) {
     const int rc = rg_plan_sorted(x, rg, st);
     if (rc != HVAE_ERR_UNSUPPORTED) return rc;
   }

@@ -42,8 +42,17 @@ def main():
             ops.w1_rowgrad(xd, da, rg)
         e.record()
         torch.cuda.synchronize()
+        both = s.elapsed_time(e) * 1e3 / args.reps
+        s.record()
+        for _ in range(args.reps):
+            ops.w1_rowgrad_plan(xd, rg)
+        e.record()
+        torch.cuda.synchronize()
+        import os
         print(json.dumps({"world": W, "rows": nb, "nnz": int(Xb.nnz), "unique_items": int(rg.n_unique.item()),
-                          "plan_plus_apply_us": round(s.elapsed_time(e) * 1e3 / args.reps, 1)}), flush=True)
+                          "plan_plus_apply_us": round(both, 1),
+                          "plan_us": round(s.elapsed_time(e) * 1e3 / args.reps, 1),
+                          "plan": "atomic" if os.environ.get("HVAE_RG_SORTED") == "0" else "sorted"}), flush=True)
 
 
 if __name__ == "__main__":
