@@ -291,6 +291,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps)
+    t_enq = time.perf_counter() - t0  # host time to enqueue the K graph replays (== elapsed when host-bound)
     torch.cuda.synchronize()
     if group is not None:
         torch.distributed.barrier()
@@ -361,6 +362,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
+            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
