@@ -222,6 +222,7 @@ class _StepBuffers:
         # side-stream GEMMs: their split-K slabs must not alias the main stream's
         self.ws2 = torch.empty_like(self.ws) if ex.two_streams else None
         self.graph = None
+        self.graph_k, self.graph_k_steps = None, 0  # single GPU: K consecutive steps in one graph (host-bound steps)
         self.graph_pre = self.graph_up = None  # data parallel: the CSR-packet and update graphs of a step
         self.graph_data = None  # the DeviceData a captured graph reads (held, compared by identity)
 
@@ -794,16 +795,19 @@ class FusedTrainer:
         const_beta = getattr(beta_fn, "constant", None)
         anneal = self._anneal
         B = batch_size
-        for bi in range(n_full):
+        bi = 0
+        while bi < n_full:
             beta = self._step_beta(beta_fn, const_beta, anneal, bi)
             bf = self._buffers(B, data.max_batch_nnz(B), train)
             if self.use_graphs and (const_beta is not None or anneal is not None):
-                if not self._replay(bf, data, train, beta, p_drop, bi, (beta, anneal, p_drop) + self._hyper()):
-                    continue
+                done = self._replay(bf, data, train, beta, p_drop, bi, (beta, anneal, p_drop) + self._hyper(),
+                                    n_full - bi)
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), train, beta, p_drop, advance=B)
+                done = 1
             if train:
-                self.host_step += 1
+                self.host_step += done
+            bi += done
         if tail:
             beta = self._step_beta(beta_fn, const_beta, anneal, n_full)
             bf = self._buffers(tail, data.max_batch_nnz(tail), train)
@@ -847,8 +851,7 @@ class FusedTrainer:
             beta = const_beta if const_beta is not None else beta_fn(bi)
             bf = self._buffers(B, data.max_batch_nnz(B), False)
             if self.use_graphs and const_beta is not None:
-                if not self._replay(bf, data, False, beta, p_drop, k, (beta, None, p_drop) + self._hyper()):
-                    continue
+                self._replay(bf, data, False, beta, p_drop, k, (beta, None, p_drop) + self._hyper())
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), False, beta, p_drop, advance=B)
         if mine_tail:
@@ -862,19 +865,21 @@ class FusedTrainer:
                 "kl_loss": tot[2] / n_batches}, 0
 
     def _replay(self, bf: _StepBuffers, data: DeviceData, train: bool, beta: float, p_drop: float, bi: int,
-                key) -> bool:
-        """Run one full batch through its captured graph(s), capturing them first if needed. The first use of
-        a buffer set runs eagerly instead (loads kernels, sets attributes) and returns False (already stepped).
-        A graph holds the DeviceData it reads (compared by identity, so a freed dataset's address reused by a
-        new one never replays a stale graph)."""
+                key, left: int = 1) -> int:
+        """Run full batches through their captured graph(s), capturing them first if needed; returns the steps
+        run. The first use of a buffer set runs one step eagerly instead (loads kernels, sets attributes). A graph
+        holds the DeviceData it reads (compared by identity, so a freed dataset's address reused by a new one
+        never replays a stale graph). Single GPU: where `left` allows, one replay of the K-step graph runs K
+        consecutive steps (the batch offset advances on the device), so the host pays one replay per K steps."""
         if bf.graph is None or bf.graph_key != key or bf.graph_data is not data:
             if bi == 0 and bf.graph is None:
                 self._launch(bf, self._csr(data, bf.B, data.perm, self.boff), train, beta, p_drop, advance=bf.B,
                              weight=key[-1] if self.dp is not None and train else 1.0)
-                if train:
-                    self.host_step += 1
-                return False
+                return 1
             self._capture(bf, data, train, beta, p_drop, key)
+        if bf.graph_k is not None and left >= bf.graph_k_steps:
+            bf.graph_k.replay()
+            return bf.graph_k_steps
         if bf.graph_pre is not None:  # data parallel: the CSR packet, then its exchange
             bf.graph_pre.replay()
             self.dp.communicate_csr()
@@ -882,7 +887,7 @@ class FusedTrainer:
         if bf.graph_up is not None:  # data parallel: the gradients' exchange between the step's graphs
             self.dp.communicate_grads()
             bf.graph_up.replay()
-        return True
+        return 1
 
     # ------------------------------------------------------ data parallel ---
     def _dp_cap(self, data: DeviceData, B: int) -> int:
@@ -937,9 +942,7 @@ class FusedTrainer:
             beta = self._step_beta(beta_fn, const_beta, anneal, bi)
             bf = self._buffers(B, W * cap, True)
             if self.use_graphs and (const_beta is not None or anneal is not None):
-                if not self._replay(bf, data, True, beta, p_drop, bi,
-                                    (beta, anneal, p_drop) + self._hyper() + (cap, 1.0 / W)):
-                    continue
+                self._replay(bf, data, True, beta, p_drop, bi, (beta, anneal, p_drop) + self._hyper() + (cap, 1.0 / W))
             else:
                 self._launch(bf, self._csr(data, B, data.perm, self.boff), True, beta, p_drop, advance=B,
                              weight=1.0 / W)
@@ -989,6 +992,14 @@ class FusedTrainer:
             with torch.cuda.graph(g):
                 self._launch(bf, csr, train, beta, p_drop, advance=bf.B)
             bf.graph_pre = bf.graph_up = None
+            k = self._steps_per_graph(bf.B) if self.dp is None else 1
+            bf.graph_k, bf.graph_k_steps = None, 0
+            if k > 1:  # the same step K times: each one reads the batch offset the previous one advanced
+                gk = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gk):
+                    for _ in range(k):
+                        self._launch(bf, csr, train, beta, p_drop, advance=bf.B)
+                bf.graph_k, bf.graph_k_steps = gk, k
         else:
             g0 = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g0):
@@ -1003,6 +1014,14 @@ class FusedTrainer:
         bf.graph = g
         bf.graph_key = key
         bf.graph_data = data
+
+    def _steps_per_graph(self, B: int) -> int:
+        """Steps per replay for batch size B: a step of a few hundred microseconds is host-bound on one replay
+        per step (HVAE_STEPS_PER_GRAPH overrides)."""
+        env = os.environ.get("HVAE_STEPS_PER_GRAPH")
+        if env:
+            return max(1, int(env))
+        return 8 if B <= 1024 else 1
 
     def sync_state_to_model(self):
         """Parameters are views of the flat buffer already; nothing to copy."""
