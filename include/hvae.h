@@ -243,6 +243,63 @@ int hvae_reparam_kl_bwd(const float* dz, const float* mu, const float* logvar, i
 int hvae_anneal_beta(int64_t* anneal_step, double beta_min, double beta_max, int64_t anneal_steps, int64_t nb,
                      float* out2, void* stream);
 
+/* ------------------------------------------- latent + projection MLP, row-parallel -- */
+/* The chain between the encoder's last hidden layer and the decoder, for batches of at most
+ * HVAE_MLP_ROWS_MAX_NB rows, in one launch per direction (each block owns a few batch rows and
+ * streams the three weight matrices once; replaces four launches forward and three data-gradient
+ * GEMMs backward). Forward (src/ml/model.py:126-127,152-153 fc_mu / fc_logvar, :157-179
+ * reparameterize, :90-95,195 the projection Linear -> GELU -> Dropout -> Linear):
+ *   heads = h W_heads^T + b_heads           [nb, 2L]  (mu | logvar)
+ *   z, eps, kl_rows                          as hvae_reparam_kl_fwd (same Philox stream)
+ *   p1 = z W_a^T + b_a ; q = Drop(GELU(p1))  [nb, D]   (dropout as HVAE_EPI_BIAS_GELU_DROP, tag 0x200)
+ *   u = q W_b^T + b_b                        [nb, D]
+ * Backward (their autograd, data gradients only; the weight gradients follow with
+ * hvae_gemm_f32_multi):
+ *   dp1 = (dU W_b) * dropmult * GELU'(p1) ; dz = dp1 W_a ;
+ *   dheads = [dz + ks mu | dz eps 0.5 exp(0.5 lv) + ks 0.5 (exp(lv) - 1)] (hvae_reparam_kl_bwd's math,
+ *   ks = beta / B or *ks_dev) ; dh = dheads W_heads.
+ * Every matrix is row-major and dense (ld = its width); H, L, D multiples of 32, at most 1024. */
+#define HVAE_MLP_ROWS_MAX_NB 1024
+typedef struct hvae_mlp_rows {
+  int64_t nb, H, L, D;
+  const float* W_heads; const float* b_heads; /* [2L, H], [2L] */
+  const float* W_a; const float* b_a;         /* [D, L], [D]   */
+  const float* W_b; const float* b_b;         /* [D, D], [D]   */
+  int train;
+  float p_drop;
+  const float* drop_mult;                     /* [nb, D] explicit dropout multipliers or NULL  */
+  const float* eps_in;                        /* [nb, L] explicit noise or NULL (Philox)       */
+  uint64_t seed;
+  const int64_t* step_dev;
+  /* forward: in h; out heads, z, eps (nullable), kl_rows, p1, q, u */
+  const float* h;
+  float* heads; float* z; float* eps; float* kl_rows; float* p1; float* q; float* u;
+  /* backward: in dU (and heads, eps, p1 above); out dp1, dheads, dh */
+  const float* dU;
+  float ks; const float* ks_dev;
+  float* dp1; float* dheads; float* dh;
+  /* forward, optional: the batch's W1 row-gradient plan (hvae_w1_rowgrad_plan) run by one more block of the
+   * same launch, beside the rows -- for batches whose plan fits one block (rg->cap <= 4096, nb <= 4096);
+   * both NULL: no plan */
+  const hvae_csr_batch* plan_x;
+  const hvae_rowgrad* plan_rg;
+  /* backward, optional: the last hidden layer's LayerNorm -> GELU -> Dropout backward on dh, fused
+   * (hvae_ln_gelu_drop_bwd's outputs: da, d_ln_w, d_ln_b and, if non-NULL, d_bias; its dropout stream
+   * `enc_layer`, multipliers enc_drop_mult [nb, H] or NULL); ln_w == NULL: dh only. ws >=
+   * hvae_mlp_bwd_rows_workspace(nb, H) bytes for the column sums */
+  const float* ln_w; const float* ln_b; const float* xhat; const float* rstd;
+  const float* enc_drop_mult; uint32_t enc_layer;
+  float* da; float* d_ln_w; float* d_ln_b; float* d_bias;
+  void* ws; size_t ws_bytes;
+} hvae_mlp_rows;
+int hvae_mlp_fwd_rows(const hvae_mlp_rows* a, void* stream);
+int hvae_mlp_bwd_rows(const hvae_mlp_rows* a, void* stream);
+size_t hvae_mlp_bwd_rows_workspace(int64_t nb, int64_t H);
+/* Up to 4 independent weight gradients dW = A^T B (each desc trans_a = 1, trans_b = 0, no split-K,
+ * its own epilogue, e.g. opa_rowsum for the bias gradient) in one launch: the three Linear weight
+ * gradients of the latent / projection MLP's backward (model.py:126-127,90-95) after hvae_mlp_bwd_rows. */
+int hvae_gemm_f32_multi(const hvae_gemm_desc* d, int n, void* stream);
+
 /* -------------------------------------------------- decoder (K7, K8, K10) -- */
 /* Streaming decoder over all N items, scores never stored:
  *   lse[b] = log sum_i exp(u_b . E_i)         (multinomial normaliser)

@@ -623,6 +623,27 @@ __global__ void __launch_bounds__(256) k_gemm_f32_pair(GemmP g0, GemmP g1) {
   }
 }
 
+// Up to kMultiMax independent weight gradients dW = A^T B in one launch (the latent / projection MLP's three
+// after hvae_mlp_bwd_rows): block b runs the problem whose block range holds it, on the register-staged kernel
+// in 32 x 32 tiles, without split-K.
+constexpr int kMultiMax = 4;
+struct GemmMulti {
+  GemmP g[kMultiMax];
+  unsigned start[kMultiMax + 1];
+  int n;
+};
+
+__global__ void __launch_bounds__(256) k_gemm_f32_multi(GemmMulti m) {
+  __shared__ __attribute__((aligned(16))) float sA[gemm_smem_floats<32>()];
+  __shared__ __attribute__((aligned(16))) float sB[gemm_smem_floats<32>()];
+  unsigned b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < m.n && b >= m.start[i + 1]) ++i;
+  b -= m.start[i];
+  const GemmP& g = m.g[i];
+  gemm_block<true, false, 32, 32>(g, b % g.gx, (b / g.gx) % g.gy, b / (g.gx * g.gy), sA, sB);
+}
+
 // ---------------------------------------------------------------- colsum ---
 __global__ void k_colsum_part(const float* __restrict__ X, int64_t M, int64_t N, int64_t ldx,
                               int64_t rows_per_part, float beta, float* __restrict__ out,
@@ -892,6 +913,36 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
   else if (bt1 == 64) k_gemm_f32_pair<32, 64><<<nblk, 256, 0, st>>>(g0, g1);
   else k_gemm_f32_pair<32, 32><<<nblk, 256, 0, st>>>(g0, g1);
   HVAE_LAUNCH_CHECK("k_gemm_f32_pair");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_gemm_f32_multi(const hvae_gemm_desc* d, int n, void* stream) {
+  HVAE_REQUIRE(d && n >= 1 && n <= kMultiMax, "hvae_gemm_f32_multi: 1..4 descriptors");
+  GemmMulti m{};
+  m.n = 0;
+  unsigned nblk = 0;
+  for (int i = 0; i < n; ++i) {
+    HVAE_REQUIRE(d[i].trans_a == 1 && d[i].trans_b == 0, "hvae_gemm_f32_multi: weight gradients only (A^T B)");
+    if (d[i].M == 0 || d[i].N == 0) continue;
+    GemmP g{};
+    int bt = 32;
+    // no workspace: one k range per tile
+    if (int rc = gemm_setup(1, 0, d[i].M, d[i].N, d[i].K, d[i].alpha, d[i].A, d[i].lda, d[i].B, d[i].ldb, d[i].beta,
+                            d[i].C, d[i].ldc, d[i].epi, nullptr, 0, g, bt))
+      return rc;
+    g.gx = (unsigned)cdiv(d[i].N, 32);
+    g.gy = (unsigned)cdiv(d[i].M, 32);
+    g.gz = 1;
+    m.start[m.n] = nblk;
+    m.g[m.n++] = g;
+    nblk += g.gx * g.gy;
+  }
+  if (m.n == 0) return HVAE_OK;
+  m.start[m.n] = nblk;
+  hipStream_t st = as_stream(stream);
+  ProbeScope probe("gemm", st);
+  k_gemm_f32_multi<<<nblk, 256, 0, st>>>(m);
+  HVAE_LAUNCH_CHECK("k_gemm_f32_multi");
   return HVAE_OK;
 }
 

@@ -72,6 +72,23 @@ class GemmDesc(C.Structure):
     ]
 
 
+class MlpRows(C.Structure):  # hvae_mlp_rows
+    _fields_ = [
+        ("nb", i64), ("H", i64), ("L", i64), ("D", i64),
+        ("W_heads", vp), ("b_heads", vp), ("W_a", vp), ("b_a", vp), ("W_b", vp), ("b_b", vp),
+        ("train", cint), ("p_drop", f32), ("drop_mult", vp), ("eps_in", vp), ("seed", u64), ("step_dev", vp),
+        ("h", vp), ("heads", vp), ("z", vp), ("eps", vp), ("kl_rows", vp), ("p1", vp), ("q", vp), ("u", vp),
+        ("dU", vp), ("ks", f32), ("ks_dev", vp), ("dp1", vp), ("dheads", vp), ("dh", vp),
+        ("plan_x", C.POINTER(CsrBatch)), ("plan_rg", C.POINTER(RowGrad)),
+        ("ln_w", vp), ("ln_b", vp), ("xhat", vp), ("rstd", vp), ("enc_drop_mult", vp), ("enc_layer", u32),
+        ("da", vp), ("d_ln_w", vp), ("d_ln_b", vp), ("d_bias", vp), ("ws", vp), ("ws_bytes", sz),
+    ]
+
+
+MLP_ROWS_MAX_NB = 1024  # include/hvae.h HVAE_MLP_ROWS_MAX_NB
+PLAN_SMALL_CAP = 4096   # csrc/hvae_rgplan.h kPlanSmallCap (the one-block row-gradient plan)
+
+
 class Adam(C.Structure):
     _fields_ = [
         ("lr", f64), ("beta1", f64), ("beta2", f64), ("eps", f64), ("weight_decay", f64),
@@ -108,6 +125,10 @@ SIGNATURES = {
     "hvae_reparam_kl_fwd": (cint, [vp, vp, i64, i64, i64, cint, vp, u64, vp, vp, vp, vp, vp]),
     "hvae_reparam_kl_bwd": (cint, [vp, vp, vp, i64, vp, i64, i64, f32, vp, cint, vp, vp, i64, vp]),
     "hvae_anneal_beta": (cint, [vp, f64, f64, i64, i64, vp, vp]),
+    "hvae_mlp_fwd_rows": (cint, [P(MlpRows), vp]),
+    "hvae_mlp_bwd_rows": (cint, [P(MlpRows), vp]),
+    "hvae_mlp_bwd_rows_workspace": (sz, [i64, i64]),
+    "hvae_gemm_f32_multi": (cint, [P(GemmDesc), cint, vp]),
     "hvae_decoder_image_bytes": (sz, [cint, i64, i64]),
     "hvae_decoder_image": (cint, [cint, vp, i64, i64, vp, vp]),
     "hvae_decoder_fwd": (cint, [cint, vp, i64, vp, vp, i64, i64, i64, vp, vp, vp, sz, vp]),

@@ -210,6 +210,8 @@ class _StepBuffers:
             need.append(L_.hvae_colsum_workspace(B, n))
         for hd in H:
             need.append(L_.hvae_ln_gelu_drop_bwd_workspace(B, hd))
+        if B <= _lib.MLP_ROWS_MAX_NB:  # the row-parallel MLP backward's LayerNorm column sums
+            need.append(L_.hvae_mlp_bwd_rows_workspace(B, H[-1]))
         # (m, n, k) of every split-K-capable GEMM of the step: forward, data- and weight-gradient products
         gemms = [(B, 2 * L, H[-1]), (2 * L, H[-1], B), (B, H[-1], 2 * L)]
         if lay.has_proj:
@@ -272,6 +274,10 @@ class FusedTrainer:
         # saves (All_Beauty B = 64: 0.1815 ms/step with the plan in line, 0.1965 beside; Syn-1M B = 4096:
         # 1.545 -> 1.293 ms/step beside)
         self.plan_side_min_batch = int(os.environ.get("HVAE_PLAN_SIDE_MIN_BATCH", "512"))
+        # batches up to MLP_ROWS_MAX_NB run the latent / projection MLP row-parallel (hvae_mlp_*_rows)
+        self.mlp_rows = bool(int(os.environ.get("HVAE_MLP_ROWS", "1")))
+        # and, when the batch's row-gradient plan fits one block, that plan as one more block of the same launch
+        self.plan_in_rows = bool(int(os.environ.get("HVAE_PLAN_IN_ROWS", "1")))
         self.boff = torch.zeros(1, dtype=torch.int64, device=device)
         self.norm = torch.zeros(1, device=device)
         self.coef = torch.ones(1, device=device)
@@ -496,6 +502,9 @@ class FusedTrainer:
 
         ev_plan = None
         dp = self.dp is not None
+        plan_in_rows = (train and not dp and self.side is None and self.plan_in_rows and self._mlp_rows_ok(B)
+                        and not (self.plan_stream is not None and B >= self.plan_side_min_batch)
+                        and bf.rg.struct.cap <= _lib.PLAN_SMALL_CAP and B <= _lib.PLAN_SMALL_CAP)
         anneal = self._anneal if train else None
         beta_dev = None
         if anneal is not None:  # this step's (beta, beta / B) from the device schedule counter, which it advances
@@ -535,6 +544,14 @@ class FusedTrainer:
                   "w1_rowgrad_plan")
             ev_plan = torch.cuda.Event()
             ev_plan.record(ps)
+        elif train and plan_in_rows:
+            # the plan runs as one more block of the row-parallel MLP forward's launch (hvae_mlp_fwd_rows); the
+            # batch's W1t rows replay their deferred steps, found from the CSR, before the encoder reads them
+            if self.lazy_adam:
+                cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
+                check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
+                                                    ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
+                      "adam_lazy_catchup_csr")
         elif train:  # the row-gradient plan depends on the batch only: overlap it with the forward
             self._fork(main, side)
             check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st2),
@@ -562,12 +579,19 @@ class FusedTrainer:
                                            step, k, tr, ptr(bf.h[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]), st),
                   "ln_gelu_drop_fwd")
         Hl = H[-1]
-        epi_b = Epilogue(_lib.EPI_BIAS, ptr(self.b_heads), None, None, 0.0, None, 0, None, 0, 0, None)
-        gemm(0, 1, B, 2 * Lt, Hl, ptr(bf.h[-1]), Hl, ptr(self.W_heads), Hl, ptr(bf.heads), 2 * Lt, epi_b)
+        rows = self._mlp_rows_args(bf, B, tr, p_drop, ext, seed) if self._mlp_rows_ok(B) else None
         mu, lv = bf.heads, bf.heads[:, Lt:]
-        check(L_.hvae_reparam_kl_fwd(ptr(mu), ptr(lv), 2 * Lt, B, Lt, tr, ptr(ext.get("eps")), seed, step,
-                                     ptr(bf.z), ptr(bf.eps), ptr(bf.kl_rows), st), "reparam_kl_fwd")
-        if lay.has_proj:
+        if rows is not None:
+            if plan_in_rows:
+                rows.plan_x, rows.plan_rg = C.pointer(csr), C.pointer(bf.rg.struct)
+            # heads -> reparameterisation -> projection, the rows of the batch spread over blocks: one launch
+            check(L_.hvae_mlp_fwd_rows(C.byref(rows), st), "mlp_fwd_rows")
+        else:
+            epi_b = Epilogue(_lib.EPI_BIAS, ptr(self.b_heads), None, None, 0.0, None, 0, None, 0, 0, None)
+            gemm(0, 1, B, 2 * Lt, Hl, ptr(bf.h[-1]), Hl, ptr(self.W_heads), Hl, ptr(bf.heads), 2 * Lt, epi_b)
+            check(L_.hvae_reparam_kl_fwd(ptr(mu), ptr(lv), 2 * Lt, B, Lt, tr, ptr(ext.get("eps")), seed, step,
+                                         ptr(bf.z), ptr(bf.eps), ptr(bf.kl_rows), st), "reparam_kl_fwd")
+        if lay.has_proj and rows is None:
             Wa, ba = self.P["projection_layer.0.weight"], self.P["projection_layer.0.bias"]
             Wb, bb = self.P["projection_layer.3.weight"], self.P["projection_layer.3.bias"]
             epi1 = Epilogue(_lib.EPI_BIAS_GELU_DROP, ptr(ba), ptr(bf.p1), None, p_drop, ptr(ext.get("proj_mask")),
@@ -604,7 +628,36 @@ class FusedTrainer:
             dw, dx = desc(1, wgrad, we), desc(0, xgrad, xepi)
             check(L_.hvae_gemm_f32_pair(C.byref(dw), C.byref(dx), st), "gemm_pair")
 
-        if lay.has_proj:
+        if rows is not None:
+            # the data gradients dp1 -> dheads -> dh of every row in one launch, then the three weight gradients
+            # (with their bias gradients) in one more
+            rows.dU, rows.dp1, rows.dheads, rows.dh = ptr(bf.dU), ptr(bf.dp1), ptr(bf.dheads), ptr(bf.dh[-1])
+            rows.ks = beta / B
+            rows.ks_dev = ptr(beta_dev[1:]) if beta_dev is not None else None
+            # with the last hidden layer's LayerNorm -> GELU -> Dropout backward (dh -> da) fused
+            kl_ = len(H) - 1
+            il = 4 * kl_
+            rows.ln_w, rows.ln_b = ptr(self.P[f"encoder.{il + 1}.weight"]), ptr(self.P[f"encoder.{il + 1}.bias"])
+            rows.xhat, rows.rstd, rows.enc_drop_mult = ptr(bf.xhat[kl_]), ptr(bf.rstd[kl_]), ptr(encm[kl_])
+            rows.enc_layer = kl_
+            rows.da, rows.d_ln_w = ptr(bf.da[kl_]), ptr(G[f"encoder.{il + 1}.weight"])
+            rows.d_ln_b, rows.d_bias = ptr(G[f"encoder.{il + 1}.bias"]), ptr(G[f"encoder.{il}.bias"])
+            rows.ws, rows.ws_bytes = ws, wsn
+            check(L_.hvae_mlp_bwd_rows(C.byref(rows), st), "mlp_bwd_rows")
+            keep = []
+
+            def wdesc(M, N, A, lda, Bm, ldb, Cm, ldc, rowsum):
+                e = Epilogue(_lib.EPI_NONE, None, None, None, 0.0, None, 0, None, 0, 0, ptr(rowsum))
+                keep.append(e)
+                return GemmDesc(1, 0, M, N, B, 1.0, A, lda, Bm, ldb, 0.0, Cm, ldc, C.pointer(e), None, 0)
+            descs = (GemmDesc * 3)(
+                wdesc(d, d, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d,
+                      G["projection_layer.3.bias"]),
+                wdesc(d, Lt, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt,
+                      G["projection_layer.0.bias"]),
+                wdesc(2 * Lt, Hl, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl, self.gb_heads))
+            check(L_.hvae_gemm_f32_multi(descs, 3, st), "gemm_multi")
+        elif lay.has_proj:
             epi3 = Epilogue(_lib.EPI_GELU_DROP_BWD, None, None, ptr(bf.p1), p_drop, ptr(ext.get("proj_mask")), seed,
                             step, _lib.TAG_PROJ_DROP, tr, None)
             layer_bwd((d, d, B, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d),
@@ -620,15 +673,17 @@ class FusedTrainer:
             check(L_.hvae_reparam_kl_bwd(ptr(bf.dz), ptr(mu), ptr(lv), 2 * Lt, ptr(bf.eps), B, Lt, beta / B,
                                          ptr(beta_dev[1:]) if beta_dev is not None else None, tr,
                                          ptr(dmu), ptr(dlv), 2 * Lt, st), "reparam_kl_bwd")
-        layer_bwd((2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl), self.gb_heads,
-                  (B, Hl, 2 * Lt, ptr(bf.dheads), 2 * Lt, ptr(self.W_heads), Hl, ptr(bf.dh[-1]), Hl))
+        if rows is None:
+            layer_bwd((2 * Lt, Hl, B, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl),
+                      self.gb_heads, (B, Hl, 2 * Lt, ptr(bf.dheads), 2 * Lt, ptr(self.W_heads), Hl, ptr(bf.dh[-1]), Hl))
         for k in range(len(H) - 1, -1, -1):
             i = 4 * k
-            check(L_.hvae_ln_gelu_drop_bwd(ptr(bf.dh[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]),
-                                           ptr(self.P[f"encoder.{i + 1}.weight"]), ptr(self.P[f"encoder.{i + 1}.bias"]),
-                                           B, H[k], p_drop, ptr(encm[k]), seed, step, k, tr, ptr(bf.da[k]),
-                                           ptr(G[f"encoder.{i + 1}.weight"]), ptr(G[f"encoder.{i + 1}.bias"]),
-                                           ptr(G[f"encoder.{i}.bias"]), ws, wsn, st), "ln_gelu_drop_bwd")
+            if not (rows is not None and k == len(H) - 1):  # (the row-parallel MLP backward did the last one)
+                check(L_.hvae_ln_gelu_drop_bwd(
+                    ptr(bf.dh[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]), ptr(self.P[f"encoder.{i + 1}.weight"]),
+                    ptr(self.P[f"encoder.{i + 1}.bias"]), B, H[k], p_drop, ptr(encm[k]), seed, step, k, tr,
+                    ptr(bf.da[k]), ptr(G[f"encoder.{i + 1}.weight"]), ptr(G[f"encoder.{i + 1}.bias"]),
+                    ptr(G[f"encoder.{i}.bias"]), ws, wsn, st), "ln_gelu_drop_bwd")
             if k > 0:
                 W = self.P[f"encoder.{i}.weight"]
                 layer_bwd((H[k], H[k - 1], B, ptr(bf.da[k]), H[k], ptr(bf.h[k - 1]), H[k - 1],
@@ -639,6 +694,31 @@ class FusedTrainer:
         if not dp:
             check(L_.hvae_w1_rowgrad_apply(ptr(bf.da[0]), H[0], bf.rg.ref, st), "w1_rowgrad_apply")
         self._fork(side, main)  # join: every gradient is complete on the main stream
+
+    def _mlp_rows_ok(self, B: int) -> bool:
+        """The row-parallel latent / projection MLP (hvae_mlp_fwd_rows / _bwd_rows) serves this batch:
+        a projection layer, B <= MLP_ROWS_MAX_NB, widths that are multiples of 32 up to 1024 whose
+        activations fit the kernels' LDS. HVAE_MLP_ROWS=0 keeps the GEMM chain."""
+        lay = self.layout
+        if not self.mlp_rows or not lay.has_proj or B > _lib.MLP_ROWS_MAX_NB:
+            return False
+        H, L, d = lay.hidden[-1], lay.L, lay.d
+        if any(v % 32 or v > 1024 for v in (H, L, d)):
+            return False
+        R = 1 if B <= 32 else 2 if B <= 512 else 4  # csrc/hvae_mlp.hip mlp_rows_per_block
+        lds = 160 * 1024  # hvae_mlp.hip kMlpLdsMax, kMlpThreads = 1024
+        return R * (H + 3 * L + 2 * d) * 4 <= lds and R * (2 * d + 2 * L + 2 * H) * 4 + 4 * 1024 * R * 4 <= lds
+
+    def _mlp_rows_args(self, bf: _StepBuffers, B: int, tr: int, p_drop: float, ext: dict, seed: int):
+        lay = self.layout
+        return _lib.MlpRows(
+            nb=B, H=lay.hidden[-1], L=lay.L, D=lay.d,
+            W_heads=ptr(self.W_heads), b_heads=ptr(self.b_heads),
+            W_a=ptr(self.P["projection_layer.0.weight"]), b_a=ptr(self.P["projection_layer.0.bias"]),
+            W_b=ptr(self.P["projection_layer.3.weight"]), b_b=ptr(self.P["projection_layer.3.bias"]),
+            train=tr, p_drop=p_drop, drop_mult=ptr(ext.get("proj_mask")), eps_in=ptr(ext.get("eps")), seed=seed,
+            step_dev=ptr(self.step_dev), h=ptr(bf.h[-1]), heads=ptr(bf.heads), z=ptr(bf.z), eps=ptr(bf.eps),
+            kl_rows=ptr(bf.kl_rows), p1=ptr(bf.p1), q=ptr(bf.q), u=ptr(bf.u))
 
     def _launch_update(self, rg, bf: _StepBuffers, advance: int = 0):
         """clip_grad_norm_(5.0) + Adam over the flat state: two launches.
