@@ -291,6 +291,10 @@ typedef struct hvae_mlp_rows {
   const float* enc_drop_mult; uint32_t enc_layer;
   float* da; float* d_ln_w; float* d_ln_b; float* d_bias;
   void* ws; size_t ws_bytes;
+  /* forward, optional (one hidden layer, H <= 512): the first encoder layer (hvae_encoder_fwd) in the same launch --
+   * reads enc_x, w1t, b1, ln_w, ln_b, enc_drop_mult; writes h (as h_out), xhat and rstd; NULL: h is an input */
+  const hvae_csr_batch* enc_x;
+  const float* w1t; const float* b1;
 } hvae_mlp_rows;
 int hvae_mlp_fwd_rows(const hvae_mlp_rows* a, void* stream);
 int hvae_mlp_bwd_rows(const hvae_mlp_rows* a, void* stream);

@@ -22,6 +22,7 @@
 
 #include "hvae_common.h"
 #include "hvae_rgplan.h"
+#include "hvae_encoder_row.h"
 
 namespace hvae {
 
@@ -56,6 +57,11 @@ struct MlpP {
   uint32_t enc_tag;
   float* da; float* d_ln_w; float* d_ln_b; float* d_bias;
   float* ln_part; unsigned* ln_ticket;
+  // forward: the first encoder layer of the rows, when enc_w1t != NULL (writes h_out, xhat, rstd)
+  const int64_t* e_row_ptr; const int32_t* e_col_idx; const float* e_vals; const int32_t* e_rows;
+  const int64_t* e_rows_offset;
+  const float* enc_w1t; const float* enc_b1;
+  float* h_out; float* xhat_out; float* rstd_out;
 };
 
 __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
@@ -213,10 +219,28 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * R;
   const int64_t step = load_step(p.step_dev);
-  for (int i = t; i < R * H / 4; i += kMlpThreads) {
-    const int r = i / (H / 4), k4 = i % (H / 4);
-    reinterpret_cast<float4*>(xs)[i] = (b0 + r < p.nb)
-        ? reinterpret_cast<const float4*>(p.h + (b0 + r) * H)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (p.enc_w1t) {  // the first encoder layer: wave w gathers, normalises and activates row w
+    if (w < R) {
+      const int64_t b = b0 + w;
+      if (b < p.nb) {
+        auto enc = [&](auto nv) {
+          encoder_sparse_row<decltype(nv)::value, false>(p.e_row_ptr, p.e_col_idx, p.e_vals, p.e_rows, p.e_rows_offset, b,
+                                                  p.enc_w1t, p.enc_b1, p.ln_w, p.ln_b, H, p.p_drop, p.scale,
+                                                  p.enc_drop_mult, p.seed, step, p.train, p.h_out, p.xhat_out,
+                                                  p.rstd_out, xs + w * H);
+        };
+        if (H <= 256) enc(std::integral_constant<int, 1>{});
+        else enc(std::integral_constant<int, 2>{});  // H <= 512 (host check)
+      } else {
+        for (int e = lane; e < H; e += 64) xs[w * H + e] = 0.f;
+      }
+    }
+  } else {
+    for (int i = t; i < R * H / 4; i += kMlpThreads) {
+      const int r = i / (H / 4), k4 = i % (H / 4);
+      reinterpret_cast<float4*>(xs)[i] = (b0 + r < p.nb)
+          ? reinterpret_cast<const float4*>(p.h + (b0 + r) * H)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
   __syncthreads();
   rows_nt<R>(p.Wh, L2, H, xs, hs, p.rot);
@@ -421,7 +445,7 @@ static size_t mlp_bwd_smem(int R, const hvae_mlp_rows* a) {
   return (size_t)R * (2 * a->D + 2 * a->L + 2 * a->H) * 4 + (size_t)4 * kMlpThreads * R * 4;
 }
 
-constexpr size_t kMlpLdsMax = 160 * 1024;  // gfx950 LDS per CU
+constexpr size_t kMlpLdsMax = 159 * 1024;  // gfx950 LDS per CU (160 KiB) less the kernels' static LDS
 
 // launch with `smem` bytes of dynamic LDS, the kernel's limit raised to kMlpLdsMax once
 #define HVAE_MLP_LAUNCH(KERNEL)                                                                        \
@@ -442,6 +466,17 @@ static int mlp_setup(const hvae_mlp_rows* a, bool fwd, MlpP& p) {
   if (fwd) {
     HVAE_REQUIRE(a->b_heads && a->b_a && a->b_b, "hvae_mlp_fwd_rows: null biases");
     HVAE_REQUIRE(a->h && a->heads && a->z && a->kl_rows && a->p1 && a->q && a->u, "hvae_mlp_fwd_rows: null buffer");
+    if (a->enc_x) {
+      const hvae_csr_batch* x = a->enc_x;
+      HVAE_REQUIRE(x->row_ptr && x->col_idx && x->vals && x->nb == a->nb && a->w1t && a->b1 && a->ln_w && a->ln_b,
+                   "hvae_mlp_fwd_rows: the encoder layer needs enc_x (nb rows), w1t, b1, ln_w, ln_b");
+      HVAE_REQUIRE(a->H <= 512, "hvae_mlp_fwd_rows: the fused encoder layer takes H <= 512 (hvae_encoder_fwd beyond)");
+      p.e_row_ptr = x->row_ptr; p.e_col_idx = x->col_idx; p.e_vals = x->vals; p.e_rows = x->rows;
+      p.e_rows_offset = x->rows_offset;
+      p.enc_w1t = a->w1t; p.enc_b1 = a->b1; p.ln_w = a->ln_w; p.ln_b = a->ln_b; p.enc_drop_mult = a->enc_drop_mult;
+      p.h_out = const_cast<float*>(a->h); p.xhat_out = const_cast<float*>(a->xhat);
+      p.rstd_out = const_cast<float*>(a->rstd);
+    }
   } else {
     HVAE_REQUIRE(a->dU && a->p1 && a->heads && a->dp1 && a->dheads && a->dh, "hvae_mlp_bwd_rows: null buffer");
     HVAE_REQUIRE(!a->train || a->eps, "hvae_mlp_bwd_rows: train backward needs eps");

@@ -344,8 +344,9 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
       const int64_t e = g0 + threadIdx.x;
       if (e < e1) {
         const int j = x.col_idx[e];
-        const int from = __hip_atomic_load(last_step + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (from < to && atomicCAS(last_step + j, from, to) == from) {
+        // one atomic claims the row: the block that raises last_step[j] to `to` replays steps from..to - 1
+        const int from = atomicMax(last_step + j, to);
+        if (from < to) {
           const int k = atomicAdd(&s_n, 1);
           s_j[k] = j;
           s_from[k] = from;

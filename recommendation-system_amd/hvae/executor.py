@@ -565,10 +565,17 @@ class FusedTrainer:
                 ev_plan = torch.cuda.Event()
                 ev_plan.record(side)
         # ------------------------------------------------------ forward ---
-        check(L_.hvae_encoder_fwd(csr_ref, ptr(self.w1t), ptr(self.P["encoder.0.bias"]),
-                                  ptr(self.P["encoder.1.weight"]), ptr(self.P["encoder.1.bias"]), H[0], p_drop,
-                                  ptr(encm[0]), seed, step, tr, ptr(bf.h[0]), ptr(bf.xhat[0]), ptr(bf.rstd[0]),
-                                  st), "encoder_fwd")
+        rows = self._mlp_rows_args(bf, B, tr, p_drop, ext, seed) if self._mlp_rows_ok(B) else None
+        if rows is not None and len(H) == 1 and H[0] <= 512:
+            # one hidden layer: the encoder layer runs in the row-parallel MLP forward's launch below
+            rows.enc_x, rows.w1t, rows.b1 = C.pointer(csr), ptr(self.w1t), ptr(self.P["encoder.0.bias"])
+            rows.ln_w, rows.ln_b = ptr(self.P["encoder.1.weight"]), ptr(self.P["encoder.1.bias"])
+            rows.enc_drop_mult, rows.xhat, rows.rstd = ptr(encm[0]), ptr(bf.xhat[0]), ptr(bf.rstd[0])
+        else:
+            check(L_.hvae_encoder_fwd(csr_ref, ptr(self.w1t), ptr(self.P["encoder.0.bias"]),
+                                      ptr(self.P["encoder.1.weight"]), ptr(self.P["encoder.1.bias"]), H[0], p_drop,
+                                      ptr(encm[0]), seed, step, tr, ptr(bf.h[0]), ptr(bf.xhat[0]),
+                                      ptr(bf.rstd[0]), st), "encoder_fwd")
         for k in range(1, len(H)):
             i = 4 * k
             W = self.P[f"encoder.{i}.weight"]
@@ -579,7 +586,6 @@ class FusedTrainer:
                                            step, k, tr, ptr(bf.h[k]), ptr(bf.xhat[k]), ptr(bf.rstd[k]), st),
                   "ln_gelu_drop_fwd")
         Hl = H[-1]
-        rows = self._mlp_rows_args(bf, B, tr, p_drop, ext, seed) if self._mlp_rows_ok(B) else None
         mu, lv = bf.heads, bf.heads[:, Lt:]
         if rows is not None:
             if plan_in_rows:
@@ -706,7 +712,7 @@ class FusedTrainer:
         if any(v % 32 or v > 1024 for v in (H, L, d)):
             return False
         R = 1 if B <= 32 else 2 if B <= 512 else 4  # csrc/hvae_mlp.hip mlp_rows_per_block
-        lds = 160 * 1024  # hvae_mlp.hip kMlpLdsMax, kMlpThreads = 1024
+        lds = 159 * 1024  # hvae_mlp.hip kMlpLdsMax, kMlpThreads = 1024
         return R * (H + 3 * L + 2 * d) * 4 <= lds and R * (2 * d + 2 * L + 2 * H) * 4 + 4 * 1024 * R * 4 <= lds
 
     def _mlp_rows_args(self, bf: _StepBuffers, B: int, tr: int, p_drop: float, ext: dict, seed: int):
