@@ -165,7 +165,7 @@ def cpu_baseline(w: dict, X, E, seconds: float, threads: int | None = None) -> d
 
 # kernel families the library's probe can bracket (ProbeScope names in csrc/)
 FAMILIES = ("decoder_sweep", "decoder_finalize", "gemm", "adam_rows", "adam_catchup", "encoder_fwd", "ln_bwd",
-            "rowgrad_plan", "rowgrad_apply", "clip")
+            "rowgrad_plan", "rowgrad_apply", "clip", "mlp_fwd", "mlp_bwd")
 
 
 def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int, kernels: dict) -> dict:
@@ -202,7 +202,10 @@ def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int,
         put("decoder_sweep", "hbm", dec_bytes, PEAK_HBM_GBS, "GB/s",
             tflops=round(dec_flops / kernels["decoder_sweep"][0] / 1e12, 3) if kernels["decoder_sweep"][0] else None)
     n_gemm = max(kernels["gemm"][1], 1)
-    gemm_flops = 6.0 * B * (2 * Lt * H + (D * Lt + D * D if Lt != D else 0))
+    # batches <= 1024 run the latent / projection forward and data gradients in the row-parallel MLP launches
+    # (hvae_mlp_*_rows); their GEMM launches are the weight gradients only (one third of the flops)
+    rows = fused._mlp_rows_ok(B)
+    gemm_flops = (2.0 if rows else 6.0) * B * (2 * Lt * H + (D * Lt + D * D if Lt != D else 0))
     for k in range(1, len(w["hidden"])):
         gemm_flops += 6.0 * B * w["hidden"][k] * w["hidden"][k - 1]
     put("gemm", "mfma", gemm_flops / n_gemm, PEAK_F32_TFLOPS, "TFLOP/s")
@@ -214,6 +217,14 @@ def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int,
         adam_bytes = 24.0 * N * H + 4.0 * N + 28.0 * n_small
     put("adam_rows", "hbm", adam_bytes, PEAK_HBM_GBS, "GB/s")
     put("encoder_fwd", "hbm", 4.0 * nnz * H + 8.0 * B * H, PEAK_HBM_GBS, "GB/s")
+    if rows:
+        # every block streams the three weight matrices once (from L2): blocks x weight bytes, + the encoder's
+        # gathered W1t rows in the forward launch when it runs there (one hidden layer)
+        R = 1 if B <= 32 else 2 if B <= 512 else 4
+        wbytes = 4.0 * (2 * Lt * H + D * Lt + D * D) * -(-B // R)
+        enc = 4.0 * nnz * H if len(w["hidden"]) == 1 and H <= 512 else 0.0
+        put("mlp_fwd", "l2", wbytes + enc, None, "GB/s")
+        put("mlp_bwd", "l2", wbytes, None, "GB/s")
     return out
 
 
@@ -326,7 +337,8 @@ def main():
     roof = roofline_models(w, args.precision, B, fused, X, users, rank, kernels)
     # the dominant kernel family: the largest per-step total (average launch x launches per step) among the
     # families with an algorithmic model
-    dom = max(roof, key=lambda k: kernels[k][0] * max(kernels[k][1], 1))
+    # (the row-parallel MLP launches stream weights from L2 and have no HBM / MFMA peak: reported, not dominant)
+    dom = max((k for k in roof if roof[k]["peak"]), key=lambda k: kernels[k][0] * max(kernels[k][1], 1))
     r = roof[dom]
     traffic, stale = None, None
     pmc = ROOT / "profiles" / (f"pmc_{args.workload}.json" if args.precision == "bf16"

@@ -4,7 +4,7 @@ set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${OUT:-r03_final}
 mkdir -p $O
-KRX='k_dec|k_gemm|k_adam_lazy|k_encoder_sparse_fwd'
+KRX='k_dec|k_gemm|k_adam_lazy|k_encoder_sparse_fwd|k_mlp'
 cd /tmp && export TMPDIR=/tmp
 pmc() {  # name, bench args
   local n=$1; shift
@@ -21,3 +21,4 @@ timeout -k 10 420 python -u bench.py --precision fp8 --steps 60 --warmup 5 --pro
 timeout -k 10 300 python -u bench.py --workload syn1m --steps 200 --warmup 20 --probe-steps 10 --no-cpu-baseline > $O/bench_syn1m.json 2> $O/bench_syn1m.log
 timeout -k 10 300 python -u bench.py --workload syn1m --precision fp8 --steps 200 --warmup 20 --probe-steps 10 --no-cpu-baseline > $O/bench_syn1m_fp8.json 2> $O/bench_syn1m_fp8.log
 timeout -k 10 300 python -u bench.py --workload all_beauty --steps 300 --warmup 30 --probe-steps 20 --no-cpu-baseline > $O/bench_all_beauty.json 2> $O/bench_all_beauty.log
+timeout -k 10 300 python -u bench.py --workload appliances --steps 300 --warmup 30 --probe-steps 20 --no-cpu-baseline > $O/bench_appliances.json 2> $O/bench_appliances.log
