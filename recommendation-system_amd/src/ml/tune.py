@@ -109,58 +109,113 @@ def evaluate_config_on_val(model, train_matrix: csr_matrix, val_df: pd.DataFrame
     return {f"{name}@{k}": float(np.mean(m[k][name])) for k in k_values for name in ("recall", "ndcg", "hit_ratio")}
 
 
+class _GridData:
+    """What every configuration of one grid search reads: the split matrices, loaders and the embeddings."""
+
+    def __init__(self, data_dir: str, embeddings_path: str, batch_size: int, device: str | None):
+        self.dev = _get_device(device)
+        full_matrix, train_df, self.val_df, mappings = load_training_data(data_dir)
+        self.user_to_idx, self.item_to_idx = mappings["user_to_idx"], mappings["item_to_idx"]
+        self.n_items = full_matrix.shape[1]
+        self.train_matrix = _build_interaction_matrix(train_df, self.user_to_idx, self.item_to_idx, full_matrix.shape)
+        val_matrix = _build_interaction_matrix(self.val_df, self.user_to_idx, self.item_to_idx, full_matrix.shape)
+        emb_path = Path(embeddings_path)
+        self.embeddings, _, _ = load_embeddings(embeddings_path,
+                                                str(emb_path.with_name(f"{emb_path.stem}_mappings.pkl")))
+        self.train_loader = DataLoader(
+            UserInteractionDataset(self.train_matrix, get_user_indices_from_df(train_df, self.user_to_idx)),
+            batch_size=batch_size, shuffle=True, num_workers=0)
+        self.val_loader = DataLoader(
+            UserInteractionDataset(val_matrix, get_user_indices_from_df(self.val_df, self.user_to_idx)),
+            batch_size=batch_size, shuffle=False, num_workers=0)
+
+
+def _one_config(g: _GridData, cfg: dict, use_annealing: bool, epochs: int, patience: int,
+                seed: int | None) -> dict[str, Any]:
+    """Train and score one grid point (reference: tune.py:240-279); failures are recorded, not raised."""
+    try:
+        if seed is not None:  # concurrent grids: every configuration from its own seed, wherever it runs
+            torch.manual_seed(seed)
+            np.random.seed(seed % 2 ** 32)
+        model = create_hybrid_vae(n_items=g.n_items, item_embeddings=g.embeddings,
+                                  latent_dim=cfg.get("latent_dim", 64), hidden_dims=cfg.get("hidden_dims", [256]),
+                                  dropout=cfg.get("dropout", 0.5), beta=cfg.get("beta", 0.2),
+                                  use_annealing=use_annealing, anneal_steps=len(g.train_loader) * epochs // 2)
+        val_loss, best_epoch = train_single_config(model, g.train_loader, g.val_loader, g.dev,
+                                                   learning_rate=cfg.get("learning_rate", 1e-3),
+                                                   epochs=epochs, patience=patience)
+        metrics = evaluate_config_on_val(model, g.train_matrix, g.val_df, g.user_to_idx, g.item_to_idx, g.dev,
+                                         n_negatives=99, k_values=[10])
+        return {"config": cfg, "val_loss": val_loss, "best_epoch": best_epoch, **metrics}
+    except Exception as e:  # the reference records the failure and moves on (tune.py:277-279)
+        logger.error(f"  Failed: {e}")
+        return {"config": cfg, "error": str(e)}
+    finally:
+        torch.cuda.empty_cache()
+
+
+_WORKER: dict[str, Any] = {}
+
+
+def _worker_init(data_dir: str, embeddings_path: str, batch_size: int, device: str | None) -> None:
+    _WORKER["grid"] = _GridData(data_dir, embeddings_path, batch_size, device)
+
+
+def _worker_run(task: tuple) -> tuple[int, dict[str, Any]]:
+    i, cfg, use_annealing, epochs, patience, seed = task
+    return i, _one_config(_WORKER["grid"], cfg, use_annealing, epochs, patience, seed)
+
+
 def run_grid_search(data_dir: str, embeddings_path: str, output_dir: str,
                     search_space: dict[str, list] | None = None, epochs_per_config: int = 10, patience: int = 3,
-                    batch_size: int = 512, use_annealing: bool = True, device: str | None = None) -> dict[str, Any]:
-    """Grid search over search_space; writes output_dir/grid_search_results.json (reference: tune.py:183-322)."""
+                    batch_size: int = 512, use_annealing: bool = True, device: str | None = None,
+                    concurrent: int = 1, seed: int | None = None) -> dict[str, Any]:
+    """Grid search over search_space; writes output_dir/grid_search_results.json (reference: tune.py:183-322).
+
+    concurrent > 1 packs that many configurations onto the GPU at once: one process each (spawned, at most 8), each
+    loading the data once and taking grid points as they free up. A configuration's train step at B = 512 leaves
+    the GPU mostly idle between its short launches, so concurrent ones overlap. Every configuration then starts
+    from its own seed (seed + its index; seed defaults to 0 here) so that its result does not depend on which
+    process ran it or when: the same grid with the same seed gives the same results at any concurrency. Results
+    and the selection (first best NDCG@10 in grid order) are as in the serial search.
+    """
     search_space = search_space or DEFAULT_SEARCH_SPACE
-    dev = _get_device(device)
-    logger.info(f"Using device: {dev}")
+    if concurrent < 1 or concurrent > 8:
+        raise ValueError("concurrent must be in 1..8 (processes sharing one GPU)")
     output_path = Path(output_dir)
     output_path.mkdir(parents=True, exist_ok=True)
-
-    full_matrix, train_df, val_df, mappings = load_training_data(data_dir)
-    user_to_idx, item_to_idx = mappings["user_to_idx"], mappings["item_to_idx"]
-    n_items = full_matrix.shape[1]
-    train_matrix = _build_interaction_matrix(train_df, user_to_idx, item_to_idx, full_matrix.shape)
-    val_matrix = _build_interaction_matrix(val_df, user_to_idx, item_to_idx, full_matrix.shape)
-
-    emb_path = Path(embeddings_path)
-    embeddings, _, _ = load_embeddings(embeddings_path, str(emb_path.with_name(f"{emb_path.stem}_mappings.pkl")))
-
-    train_loader = DataLoader(UserInteractionDataset(train_matrix, get_user_indices_from_df(train_df, user_to_idx)),
-                              batch_size=batch_size, shuffle=True, num_workers=0)
-    val_loader = DataLoader(UserInteractionDataset(val_matrix, get_user_indices_from_df(val_df, user_to_idx)),
-                            batch_size=batch_size, shuffle=False, num_workers=0)
-
     param_names = list(search_space.keys())
-    all_configs = list(itertools.product(*search_space.values()))
+    all_configs = [dict(zip(param_names, values)) for values in itertools.product(*search_space.values())]
     logger.info(f"Grid search over {len(all_configs)} configurations")
-    results, best_config, best_metric = [], None, -float("inf")
-    for i, values in enumerate(all_configs):
-        cfg = dict(zip(param_names, values))
-        logger.info(f"\n[{i + 1}/{len(all_configs)}] Testing: {cfg}")
-        try:
-            model = create_hybrid_vae(n_items=n_items, item_embeddings=embeddings,
-                                      latent_dim=cfg.get("latent_dim", 64), hidden_dims=cfg.get("hidden_dims", [256]),
-                                      dropout=cfg.get("dropout", 0.5), beta=cfg.get("beta", 0.2),
-                                      use_annealing=use_annealing,
-                                      anneal_steps=len(train_loader) * epochs_per_config // 2)
-            val_loss, best_epoch = train_single_config(model, train_loader, val_loader, dev,
-                                                       learning_rate=cfg.get("learning_rate", 1e-3),
-                                                       epochs=epochs_per_config, patience=patience)
-            metrics = evaluate_config_on_val(model, train_matrix, val_df, user_to_idx, item_to_idx, dev,
-                                             n_negatives=99, k_values=[10])
-            results.append({"config": cfg, "val_loss": val_loss, "best_epoch": best_epoch, **metrics})
-            if metrics["ndcg@10"] > best_metric:
-                best_metric, best_config = metrics["ndcg@10"], cfg
-            logger.info(f"  Val Loss: {val_loss:.4f}, NDCG@10: {metrics['ndcg@10']:.4f}, "
-                        f"Recall@10: {metrics['recall@10']:.4f}")
-        except Exception as e:  # the reference records the failure and moves on (tune.py:277-279)
-            logger.error(f"  Failed: {e}")
-            results.append({"config": cfg, "error": str(e)})
-        finally:
-            torch.cuda.empty_cache()
+    if concurrent > 1 and seed is None:
+        seed = 0
+    seeds = [None if seed is None else seed + i for i in range(len(all_configs))]
+    if concurrent == 1:
+        g = _GridData(data_dir, embeddings_path, batch_size, device)
+        logger.info(f"Using device: {g.dev}")
+        results = []
+        for i, cfg in enumerate(all_configs):
+            logger.info(f"\n[{i + 1}/{len(all_configs)}] Testing: {cfg}")
+            results.append(_one_config(g, cfg, use_annealing, epochs_per_config, patience, seeds[i]))
+            r = results[-1]
+            if "error" not in r:
+                logger.info(f"  Val Loss: {r['val_loss']:.4f}, NDCG@10: {r['ndcg@10']:.4f}, "
+                            f"Recall@10: {r['recall@10']:.4f}")
+    else:
+        _get_device(device)  # fail before spawning when no HIP device is visible
+        import multiprocessing as mp
+        tasks = [(i, cfg, use_annealing, epochs_per_config, patience, seeds[i]) for i, cfg in enumerate(all_configs)]
+        results = [None] * len(all_configs)
+        with mp.get_context("spawn").Pool(concurrent, initializer=_worker_init,
+                                          initargs=(data_dir, embeddings_path, batch_size, device)) as pool:
+            for i, r in pool.imap_unordered(_worker_run, tasks):
+                results[i] = r
+                logger.info(f"[{i + 1}/{len(all_configs)}] {r['config']}: "
+                            + (f"NDCG@10 {r['ndcg@10']:.4f}" if "error" not in r else f"failed: {r['error']}"))
+    best_config, best_metric = None, -float("inf")
+    for r in results:
+        if "error" not in r and r["ndcg@10"] > best_metric:
+            best_metric, best_config = r["ndcg@10"], r["config"]
 
     valid_results = sorted([r for r in results if "error" not in r], key=lambda x: x["ndcg@10"], reverse=True)
     output_file = output_path / "grid_search_results.json"
@@ -192,12 +247,16 @@ def main() -> None:
     parser.add_argument("--dropouts", type=float, nargs="+", default=[0.3, 0.5])
     parser.add_argument("--betas", type=float, nargs="+", default=[0.1, 0.2, 0.3])
     parser.add_argument("--learning-rates", type=float, nargs="+", default=[1e-3, 5e-4])
+    parser.add_argument("--concurrent", type=int, default=1,
+                        help="configurations trained at once on the GPU, one process each (1-8; MI355X addition)")
+    parser.add_argument("--seed", type=int, default=None,
+                        help="seed configuration i with seed + i (default with --concurrent > 1: 0)")
     args = parser.parse_args()
     run_grid_search(data_dir=args.data, embeddings_path=args.embeddings, output_dir=args.output,
                     search_space={"latent_dim": args.latent_dims, "hidden_dims": [[256], [512], [256, 128]],
                                   "dropout": args.dropouts, "beta": args.betas, "learning_rate": args.learning_rates},
                     epochs_per_config=args.epochs, patience=args.patience, batch_size=args.batch_size,
-                    device=args.device)
+                    device=args.device, concurrent=args.concurrent, seed=args.seed)
 
 
 if __name__ == "__main__":

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--batch-size", type=int, default=512)
     ap.add_argument("--configs", type=int, default=2)
+    ap.add_argument("--concurrent", type=int, nargs="*", default=[],
+                    help="instead: time an 8-configuration grid at each of these concurrencies")
     args = ap.parse_args()
     from gen import write_planted_artifacts
     from src.ml.tune import run_grid_search
@@ -34,6 +36,26 @@ def main():
     t0 = time.perf_counter()
     data, emb = write_planted_artifacts(tmp)
     print(json.dumps({"artifacts_s": round(time.perf_counter() - t0, 1)}), flush=True)
+    if args.concurrent:
+        # an 8-point grid from the default search space at each concurrency, seeded per configuration so that every
+        # run computes the same results
+        space = {"latent_dim": [64, 128], "hidden_dims": [[512], [256]], "dropout": [0.3, 0.5], "beta": [0.2],
+                 "learning_rate": [1e-3]}
+        ref = None
+        for conc in args.concurrent:
+            t = time.perf_counter()
+            out = run_grid_search(str(data), str(emb), str(tmp / f"models_c{conc}"), search_space=space,
+                                  epochs_per_config=args.epochs, patience=args.epochs, batch_size=args.batch_size,
+                                  use_annealing=True, device="cuda", concurrent=conc, seed=0)
+            wall = time.perf_counter() - t
+            res = [(r.get("val_loss"), r.get("ndcg@10"), r.get("error")) for r in out["all_results"]]
+            same = None if ref is None else res == ref
+            ref = ref or res
+            print(json.dumps({"concurrent": conc, "configs": len(res), "epochs": args.epochs,
+                              "batch_size": args.batch_size, "wall_s": round(wall, 2),
+                              "wall_s_per_config": round(wall / len(res), 3), "results_equal_first_run": same,
+                              "errors": [e for _, _, e in res if e]}), flush=True)
+        return
     grid = [{"latent_dim": [128], "hidden_dims": [[512]], "dropout": [0.3], "beta": [b], "learning_rate": [1e-3]}
             for b in (0.2, 0.1, 0.3)][: args.configs]
     for anneal in (True, False):

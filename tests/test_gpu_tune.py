@@ -87,3 +87,23 @@ def test_evaluate_config_on_val_protocol(hip_device, tmp_path):
     for k in (5, 10):
         for m in ("recall", "ndcg", "hit_ratio"):
             assert abs(got[f"{m}@{k}"] - float(np.mean(acc[k][m]))) <= tol, (m, k)
+
+
+def test_grid_search_concurrent_equals_serial(hip_device, tmp_path):
+    """--concurrent packs configurations onto the GPU in spawned processes; with per-configuration seeds the results
+    (losses, metrics, selection, order) equal the serial search's exactly."""
+    from src.ml.tune import run_grid_search
+    data, emb = write_planted_artifacts(tmp_path, SMALL)
+    space = {"latent_dim": [16], "hidden_dims": [[64]], "dropout": [0.3], "beta": [0.1, 0.2, 0.3],
+             "learning_rate": [1e-3]}
+    outs = []
+    for conc in (1, 2):
+        out = run_grid_search(str(data), str(emb), str(tmp_path / f"models{conc}"), search_space=space,
+                              epochs_per_config=2, patience=2, batch_size=64, device="cuda", concurrent=conc, seed=5)
+        outs.append(out)
+    a, b = outs
+    assert [r["config"] for r in a["all_results"]] == [r["config"] for r in b["all_results"]]
+    assert all("error" not in r for r in a["all_results"] + b["all_results"]), (a, b)
+    for ra, rb in zip(a["all_results"], b["all_results"]):
+        assert ra == rb
+    assert a["best_config"] == b["best_config"] and a["best_metric"] == b["best_metric"]
