@@ -79,3 +79,27 @@ def test_non_hip_device_fails_loudly(modname, device):
     mod = importlib.import_module(modname)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         mod._get_device(device)
+
+
+@pytest.mark.parametrize("conc", [0, 9])
+def test_tune_concurrency_bounds(tmp_path, conc):
+    """--concurrent packs 1..8 configuration processes onto one GPU; anything else fails before data loads."""
+    from src.ml.tune import run_grid_search
+    with pytest.raises(ValueError, match="concurrent"):
+        run_grid_search(str(tmp_path / "no_data"), str(tmp_path / "no_emb.npy"), str(tmp_path / "out"),
+                        concurrent=conc)
+
+
+def test_tune_cli_concurrency_flags():
+    """The MI355X additions to the reference's tune flags: --concurrent (default 1, the serial search) and --seed."""
+    import sys
+    from unittest import mock
+    import src.ml.tune as t
+    with mock.patch.object(t, "run_grid_search") as run, \
+            mock.patch.object(sys, "argv", ["tune", "--concurrent", "4", "--seed", "3"]):
+        t.main()
+    kw = run.call_args.kwargs
+    assert kw["concurrent"] == 4 and kw["seed"] == 3
+    with mock.patch.object(t, "run_grid_search") as run, mock.patch.object(sys, "argv", ["tune"]):
+        t.main()
+    assert run.call_args.kwargs["concurrent"] == 1 and run.call_args.kwargs["seed"] is None
