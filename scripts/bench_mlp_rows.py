@@ -37,8 +37,21 @@ def main():
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--batches", default="64,512,1024")
     ap.add_argument("--d", type=int, default=384)
+    ap.add_argument("--shapes", default=None,
+                    help="H:L:D list (e.g. 512:128:384,32:32:384) timed at the first batch instead of --d")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if args.shapes:
+        B = int(args.batches.split(",")[0])
+        for sh in args.shapes.split(","):
+            H, L, D = (int(v) for v in sh.split(":"))
+            t, d, out = _setup(B, H, L, D, dev, 1)
+            a = _args(B, H, L, D, d, out, True, 0.3, explicit=False, seed=3)
+            fwd = probe("mlp_fwd", lambda: check(lib().hvae_mlp_fwd_rows(C.byref(a), None), "fwd"), args.reps)
+            bwd = probe("mlp_bwd", lambda: check(lib().hvae_mlp_bwd_rows(C.byref(a), None), "bwd"), args.reps)
+            print(json.dumps({"B": B, "H": H, "L": L, "D": D, "fwd_us": fwd, "bwd_us": bwd,
+                              "weight_bytes": 4 * (2 * L * H + D * L + D * D)}), flush=True)
+        return
     H, L, D = 512, 128, args.d
     for B in (int(b) for b in args.batches.split(",")):
         t, d, out = _setup(B, H, L, D, dev, 1)
