@@ -299,6 +299,9 @@ typedef struct hvae_mlp_rows {
 int hvae_mlp_fwd_rows(const hvae_mlp_rows* a, void* stream);
 int hvae_mlp_bwd_rows(const hvae_mlp_rows* a, void* stream);
 size_t hvae_mlp_bwd_rows_workspace(int64_t nb, int64_t H);
+/* 1 if hvae_mlp_fwd_rows and hvae_mlp_bwd_rows accept a batch of nb rows at these widths (fused_enc: with the
+ * first encoder layer in the forward launch), else 0 -- the caller then runs the GEMM chain */
+int hvae_mlp_rows_supported(int64_t nb, int64_t H, int64_t L, int64_t D, int fused_enc);
 /* Up to 4 independent weight gradients dW = A^T B (each desc trans_a = 1, trans_b = 0, no split-K,
  * its own epilogue, e.g. opa_rowsum for the bias gradient) in one launch: the three Linear weight
  * gradients of the latent / projection MLP's backward (model.py:126-127,90-95) after hvae_mlp_bwd_rows. */
@@ -425,7 +428,7 @@ int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v, const hva
  * step, so they are deferred and replayed -- the same float operations in the
  * same order, bitwise equal to updating eagerly -- when the row is next needed.
  *   last_step [N] int32: steps already applied to each row (start at 0)
- *   tab [tab_len][2] float: per-step (lr / bc1_t, sqrt(bc2_t)), entry t written
+ *   tab [tab_len][2] float: per-step (lr / bc1_t, 1 / sqrt(bc2_t)), entry t written
  *                           by step t's hvae_adam_lazy; tab_len > total steps
  * hvae_adam_lazy: step t = *cfg->step_dev + 1 for the dense segment and for the
  *   gradient rows of rg (their missed steps replayed first).

@@ -536,6 +536,19 @@ extern "C" int hvae_mlp_fwd_rows(const hvae_mlp_rows* a, void* stream) {
   return HVAE_OK;
 }
 
+// the shapes hvae_mlp_fwd_rows / _bwd_rows accept (mlp_setup's width rules, both directions' LDS at this batch's
+// rows per block), so that the host picks the GEMM chain instead of a launch that would fail its HVAE_REQUIRE
+extern "C" int hvae_mlp_rows_supported(int64_t nb, int64_t H, int64_t L, int64_t D, int fused_enc) {
+  if (nb <= 0 || nb > HVAE_MLP_ROWS_MAX_NB) return 0;
+  for (int64_t v : {H, L, D})
+    if (v < 32 || v > 1024 || v % 32) return 0;
+  if (fused_enc && H > 512) return 0;
+  hvae_mlp_rows a{};
+  a.nb = nb; a.H = H; a.L = L; a.D = D;
+  const int R = mlp_rows_per_block(nb);
+  return mlp_fwd_smem(R, &a) <= kMlpLdsMax && mlp_bwd_smem(R, &a) <= kMlpLdsMax;
+}
+
 extern "C" size_t hvae_mlp_bwd_rows_workspace(int64_t nb, int64_t H) {
   return nb > 0 ? (size_t)cdiv(nb, mlp_rows_per_block(nb)) * 3 * H * sizeof(float) : 0;
 }

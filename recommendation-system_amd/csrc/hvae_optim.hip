@@ -22,11 +22,12 @@ constexpr int kNormBlocks = 512;
 // so that the Adam launches that follow read the pre-increment step from
 // step_snap and no separate counter launch is needed.
 // torch's per-step Adam scalars for step t, in double as torch computes them (Python floats):
-// (step_size = lr / (1 - b1^t), sqrt(1 - b2^t)), rounded to fp32 where the kernels use them.
+// (step_size = lr / (1 - b1^t), 1 / sqrt(1 - b2^t)), rounded to fp32 where the kernels use them (the element
+// update multiplies by the reciprocal of bias_correction2_sqrt instead of dividing by it: adam_elem).
 __device__ __forceinline__ float2 adam_step_consts(double lr, double b1, double b2, int64_t t) {
   const double bc1 = 1.0 - pow(b1, (double)t);
   const double bc2 = 1.0 - pow(b2, (double)t);
-  return make_float2((float)(lr / bc1), (float)sqrt(bc2));
+  return make_float2((float)(lr / bc1), (float)(1.0 / sqrt(bc2)));
 }
 
 struct ClipArgs {
@@ -96,11 +97,15 @@ __global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
 
 struct AdamK {
   float lr_over_bc1;  // step_size
-  float bc2_sqrt;
+  float inv_bc2_sqrt;  // 1 / bias_correction2_sqrt
   float omb1, b2, omb2, eps, wd;
 };
 
-// torch.optim.Adam single-tensor arithmetic, element-wise.
+// torch.optim.Adam single-tensor arithmetic, element-wise, with the hardware square root and reciprocal
+// (v_sqrt_f32, v_rcp_f32: 1 ulp) where torch divides and takes a correctly rounded root: the parameter update
+// differs from torch's by a few ulp of the step (compared at STEP_TOL, tests/test_gpu_train.py), and the lazy
+// replays run VALU-light enough to stay near the HBM bound (the IEEE division / square-root sequences made
+// the exact replays VALU-bound).
 // No FMA contraction: every kernel that applies a step (dense, flat, lazy rows, replays) must round
 // identically whatever code shape the compiler sees around it, or the lazy update would drift off
 // the dense one by an ulp (hipcc contracts a*b+c freely by default).
@@ -109,8 +114,19 @@ __device__ __forceinline__ void adam_elem(float& p, float& m, float& v, float g,
   if (k.wd != 0.f) g = g + k.wd * p;
   m = m + k.omb1 * (g - m);                 // exp_avg.lerp_(grad, 1 - beta1)
   v = v * k.b2 + k.omb2 * g * g;            // exp_avg_sq.mul_(beta2).addcmul_(g, g, 1 - beta2)
-  const float denom = sqrtf(v) / k.bc2_sqrt + k.eps;
-  p = p - k.lr_over_bc1 * (m / denom);      // param.addcdiv_(exp_avg, denom, -step_size)
+  const float denom = __builtin_amdgcn_sqrtf(v) * k.inv_bc2_sqrt + k.eps;  // (sqrt(v) / bc2_sqrt).add_(eps)
+  p = p - k.lr_over_bc1 * (m * __builtin_amdgcn_rcpf(denom));             // param.addcdiv_(m, denom, -step_size)
+}
+
+// adam_elem with g = 0 and no weight decay (the lazy replays), bitwise equal to it: m + omb1 (0 - m) is
+// m - omb1 m for every m (signed zeros and NaN included: 0 - m is -m but for m = +0, where both forms give +0),
+// and v b2 + omb2 0 0 is v b2 because v is never -0 (it starts at +0 and only ever adds g g >= +0)
+__device__ __forceinline__ void adam_elem0(float& p, float& m, float& v, const AdamK& k) {
+#pragma clang fp contract(off)
+  m = m - k.omb1 * m;
+  v = v * k.b2;
+  const float denom = __builtin_amdgcn_sqrtf(v) * k.inv_bc2_sqrt + k.eps;
+  p = p - k.lr_over_bc1 * (m * __builtin_amdgcn_rcpf(denom));
 }
 
 struct AdamArgs {
@@ -124,7 +140,7 @@ __device__ __forceinline__ AdamK adam_consts(const AdamArgs& a) {
   const float2 c = adam_step_consts(a.lr, a.b1, a.b2, t);
   AdamK k;
   k.lr_over_bc1 = c.x;
-  k.bc2_sqrt = c.y;
+  k.inv_bc2_sqrt = c.y;
   k.omb1 = (float)(1.0 - a.b1);
   k.b2 = (float)a.b2;
   k.omb2 = (float)(1.0 - a.b2);
@@ -235,11 +251,11 @@ __global__ void __launch_bounds__(256) k_adam_flat(AdamArgs a, float* __restrict
 // before the forward of a batch that contains it (catch-up of the batch rows),
 // in the update (rows merged from other ranks), and at an epoch end / state
 // read (flush of all rows). last_step[j] = steps already applied to row j;
-// tab[t] = (lr / bc1_t, sqrt(bc2_t)) of step t, written by the step's update.
+// tab[t] = (lr / bc1_t, 1 / sqrt(bc2_t)) of step t, written by the step's update.
 __device__ __forceinline__ AdamK adam_consts_tab(const AdamArgs& a, float2 c) {
   AdamK k;
   k.lr_over_bc1 = c.x;
-  k.bc2_sqrt = c.y;
+  k.inv_bc2_sqrt = c.y;
   k.omb1 = (float)(1.0 - a.b1);
   k.b2 = (float)a.b2;
   k.omb2 = (float)(1.0 - a.b2);
@@ -279,10 +295,17 @@ __device__ __forceinline__ void col_update(const AdamArgs& a, const float2* __re
     for (int u = 0; u < 8; ++u) {
       if (s0 + u > to) break;
       const AdamK k = adam_consts_tab(a, c[u]);
-      adam_elem(pp.x, mm.x, vv.x, 0.f, k);
-      adam_elem(pp.y, mm.y, vv.y, 0.f, k);
-      adam_elem(pp.z, mm.z, vv.z, 0.f, k);
-      adam_elem(pp.w, mm.w, vv.w, 0.f, k);
+      if (k.wd == 0.f) {
+        adam_elem0(pp.x, mm.x, vv.x, k);
+        adam_elem0(pp.y, mm.y, vv.y, k);
+        adam_elem0(pp.z, mm.z, vv.z, k);
+        adam_elem0(pp.w, mm.w, vv.w, k);
+      } else {
+        adam_elem(pp.x, mm.x, vv.x, 0.f, k);
+        adam_elem(pp.y, mm.y, vv.y, 0.f, k);
+        adam_elem(pp.z, mm.z, vv.z, 0.f, k);
+        adam_elem(pp.w, mm.w, vv.w, 0.f, k);
+      }
     }
   }
   if (step) {
@@ -388,7 +411,7 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
   const bool have = c0t.x != 0.f || c0t.y != 0.f;
   const AdamK k = have ? adam_consts_tab(a, c0t) : adam_consts(a);
   const float coef = a.coef_dev ? *a.coef_dev : 1.f;
-  if (!have && blockIdx.x == 0 && threadIdx.x == 0) tab[t] = make_float2(k.lr_over_bc1, k.bc2_sqrt);
+  if (!have && blockIdx.x == 0 && threadIdx.x == 0) tab[t] = make_float2(k.lr_over_bc1, k.inv_bc2_sqrt);
   const int nu = *n_unique;
   const int64_t H4 = H / 4;
   const int rr = threadIdx.x / rm.h4s, cc = threadIdx.x % rm.h4s;

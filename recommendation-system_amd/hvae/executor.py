@@ -276,6 +276,7 @@ class FusedTrainer:
         self.plan_side_min_batch = int(os.environ.get("HVAE_PLAN_SIDE_MIN_BATCH", "512"))
         # batches up to MLP_ROWS_MAX_NB run the latent / projection MLP row-parallel (hvae_mlp_*_rows)
         self.mlp_rows = bool(int(os.environ.get("HVAE_MLP_ROWS", "1")))
+        self._mlp_rows_cache: dict[int, bool] = {}
         # and, when the batch's row-gradient plan fits one block, that plan as one more block of the same launch
         self.plan_in_rows = bool(int(os.environ.get("HVAE_PLAN_IN_ROWS", "1")))
         self.boff = torch.zeros(1, dtype=torch.int64, device=device)
@@ -316,10 +317,12 @@ class FusedTrainer:
         self.precision = precision
         self.enorm = ops.row_norm_max(self.E_dec)
         self._e_version = model.item_embeddings._version
+        self._e_src_ptr = model.item_embeddings.data_ptr()
         self._bufs: dict[tuple, _StepBuffers] = {}
         self._views()
         self.dp = None
         self.dp_epoch = 0
+        self.dp_val_epoch = 0
         self._dp_caps: dict = {}
         if process_group is not None and torch.distributed.get_world_size(process_group) > 1:
             from .dist import DPExchange
@@ -388,7 +391,9 @@ class FusedTrainer:
         checkpoint of another embedding file): bring the fp32 copy, the decoder image and max||E|| up to date in
         place, so captured graphs keep their pointers. Cheap when nothing changed (a version compare)."""
         E = self.model.item_embeddings
-        if E._version == self._e_version and E.data_ptr() == self.E32.data_ptr():
+        # the source tensor last synced from (its address and version), not E32's address: E32 is a private copy
+        # whenever the module's buffer is non-contiguous or has been reassigned
+        if E._version == self._e_version and E.data_ptr() == self._e_src_ptr:
             return
         with torch.no_grad():
             if E.data_ptr() != self.E32.data_ptr():
@@ -397,6 +402,7 @@ class FusedTrainer:
                 self.E_dec.refresh(self.E32)
             ops.row_norm_max(self.E_dec, out=self.enorm)
         self._e_version = E._version
+        self._e_src_ptr = E.data_ptr()
 
     def grad_of(self, name: str) -> torch.Tensor:
         """Current gradient of a small parameter (after the last step)."""
@@ -708,12 +714,11 @@ class FusedTrainer:
         lay = self.layout
         if not self.mlp_rows or not lay.has_proj or B > _lib.MLP_ROWS_MAX_NB:
             return False
-        H, L, d = lay.hidden[-1], lay.L, lay.d
-        if any(v % 32 or v > 1024 for v in (H, L, d)):
-            return False
-        R = 1 if B <= 32 else 2 if B <= 512 else 4  # csrc/hvae_mlp.hip mlp_rows_per_block
-        lds = 159 * 1024  # hvae_mlp.hip kMlpLdsMax, kMlpThreads = 1024
-        return R * (H + 3 * L + 2 * d) * 4 <= lds and R * (2 * d + 2 * L + 2 * H) * 4 + 4 * 1024 * R * 4 <= lds
+        ok = self._mlp_rows_cache.get(B)
+        if ok is None:  # the library's own shape rules (rows per block, LDS of both directions)
+            ok = bool(lib().hvae_mlp_rows_supported(B, lay.hidden[-1], lay.L, lay.d, 0))
+            self._mlp_rows_cache[B] = ok
+        return ok
 
     def _mlp_rows_args(self, bf: _StepBuffers, B: int, tr: int, p_drop: float, ext: dict, seed: int):
         lay = self.layout
@@ -827,7 +832,13 @@ class FusedTrainer:
         """
         n = int(data.users.numel())
         if n == 0:
-            return {"total_loss": float("nan"), "recon_loss": float("nan"), "kl_loss": float("nan")}
+            nan = {"total_loss": float("nan"), "recon_loss": float("nan"), "kl_loss": float("nan")}
+            if not train and self.dp is not None and not data.dp_global:
+                # an empty shard still joins the other ranks' batch-weighted validation sum
+                tot = self.dp.all_reduce([0.0, 0.0, 0.0, 0.0]).tolist()
+                if tot[3] > 0:
+                    return {"total_loss": tot[0] / tot[3], "recon_loss": tot[1] / tot[3], "kl_loss": tot[2] / tot[3]}
+            return nan
         self.sync_embeddings()
         anneal = getattr(beta_fn, "anneal", None) if train else None
         if anneal is not None:
@@ -857,9 +868,13 @@ class FusedTrainer:
     def _run_epoch_local(self, data: DeviceData, batch_size: int, shuffle: bool, beta_fn, p_drop: float,
                          train: bool, drop_last: bool, generator, max_batches) -> tuple[dict, int]:
         n = int(data.users.numel())
+        shard_reduce = False
         if not train and self.dp is not None and data.users_host is not None:
-            return self._run_eval_sharded(data, batch_size, shuffle, beta_fn, p_drop, drop_last, generator,
-                                          max_batches)
+            if data.dp_global:  # every rank holds every user: deal the single-GPU batches over the ranks
+                return self._run_eval_sharded(data, batch_size, shuffle, beta_fn, p_drop, drop_last, generator,
+                                              max_batches)
+            # per-rank shards: each rank validates its whole shard, then the batch losses are summed over ranks
+            shard_reduce = True
         if shuffle:
             order = _sampler_order(n, generator, self.device)
             data.perm.copy_(data.users[order.to(self.device)])
@@ -902,6 +917,9 @@ class FusedTrainer:
                 self.host_step += 1
         self.flush()
         sums = accum.cpu().tolist()  # the one host sync of the epoch
+        if shard_reduce:  # batch-weighted: the mean over every rank's batches, as one GPU over all shards
+            tot = self.dp.all_reduce(np.array(sums + [float(n_batches)], dtype=np.float64)).tolist()
+            sums, n_batches = tot[:3], int(round(tot[3]))
         return ({"total_loss": sums[0] / n_batches, "recon_loss": sums[1] / n_batches,
                  "kl_loss": sums[2] / n_batches}, n_batches if train else 0)
 
@@ -915,7 +933,12 @@ class FusedTrainer:
         dp, W, r = self.dp, self.dp.world, self.dp.rank
         users = data.users_host
         n = len(users)
-        order = users[_sampler_order(n, generator, self.device).cpu().numpy()] if shuffle else users
+        if shuffle:  # one order on every rank: drawn from the shared data-parallel seed, not a per-rank generator
+            rng = np.random.default_rng([self.dp_seed, 0x5EA1, self.dp_val_epoch])
+            self.dp_val_epoch += 1
+            order = users[rng.permutation(n)]
+        else:
+            order = users
         n_full, tail = divmod(n, B)
         if drop_last:
             tail = 0

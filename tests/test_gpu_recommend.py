@@ -84,3 +84,41 @@ def test_module_recommend_is_exact(core):
             i = int(idx[r, j])
             assert i == int(ref.indices[j]) or abs(S[r, i].item() - ref.values[j].item()) <= tol
             assert abs(val[r, j].item() - S[r, i].item()) <= tol
+
+
+def _topk_gemm(m, z, k):
+    """The exact score-matrix path on the module's current E: fp32 hvae_gemm_f32 + hvae_topk."""
+    from hvae import ops
+    with torch.no_grad():
+        u = m.projection_layer(z).contiguous()
+        S = ops.gemm(u, m.item_embeddings.detach().t())
+        return ops.topk(S, k)
+
+
+def test_recommend_after_new_embeddings(core):
+    """The fused top-K caches E's bf16 image keyed on the buffer's version (src/ml/model.py topk_scores): a
+    recommend -> load_state_dict with another embedding file -> recommend must rank against the NEW E, as
+    gemm + hvae_topk do (reference model.py:236-256 reads self.item_embeddings on every call). Then once more
+    through an in-place copy_ of E."""
+    from src.ml.model import HybridVAE
+    m = core.model
+    g = torch.Generator().manual_seed(11)
+    z = torch.randn(9, 64, generator=g).to(core.device)
+    i0, _ = m.recommend(z, top_k=20)
+    r0, _ = _topk_gemm(m, z, 20)
+    assert (i0.cpu() == r0.cpu().long()).float().mean() > 0.99
+    E2 = synth_embeddings(2000, 384, seed=77)
+    torch.manual_seed(3)  # same weights, other embeddings: only E changes
+    other = HybridVAE(2000, E2, latent_dim=64, hidden_dims=[256], dropout=0.3, beta=0.2)
+    m.load_state_dict(other.state_dict())
+    i1, v1 = m.recommend(z, top_k=20)
+    r1, s1 = _topk_gemm(m, z, 20)
+    assert not torch.equal(i1.cpu(), i0.cpu())  # the ranking moved with E
+    assert (i1.cpu() == r1.cpu().long()).float().mean() > 0.99
+    torch.testing.assert_close(v1.cpu(), s1.cpu(), rtol=2e-5, atol=2e-5)
+    with torch.no_grad():
+        m.item_embeddings.copy_(torch.as_tensor(synth_embeddings(2000, 384, seed=78), device=core.device))
+    i2, v2 = m.recommend(z, top_k=20)
+    r2, s2 = _topk_gemm(m, z, 20)
+    assert (i2.cpu() == r2.cpu().long()).float().mean() > 0.99
+    torch.testing.assert_close(v2.cpu(), s2.cpu(), rtol=2e-5, atol=2e-5)

@@ -140,3 +140,85 @@ def test_topk_fused_exclusion_edges(hip_device):
     assert sorted(idx[2].cpu().tolist()) == list(range(N - k, N))  # exactly the k unseen items
     R0 = ops.topk_fused(Ud[:0], img, Ed, emax, k)
     assert R0[0].shape == (0, k)
+
+
+def test_topk_fused_bf16_midpoint_adversarial(hip_device):
+    """the shortlist bound eps_u (hvae_topk.hip) must cover bf16 rounding of BOTH u and E. u's first
+    half and the true top item's E row sit just below the bf16 rounding midpoint (both round down by ~2^-8), so
+    the top item's bf16 score is ~2^-7 low; 40 competitors live on u's bf16-exact half with bf16-exact E, scoring
+    just under the top in fp32 but ~0.49 above it in bf16, i.e. above the top by more than a 2^-8 bound (0.37)
+    and less than the 2^-7 one (0.73). The fused top-K must still return the top item first, as the fp32 score
+    matrix + hvae_topk do."""
+    from hvae import ops
+    N, D, k = 3000, 128, 10
+    c = 1.0 + 2.0 ** -8 - 2.0 ** -20  # rounds down to 1.0 in bf16
+    u = torch.ones(1, D, dtype=torch.float64)
+    u[0, : D // 2] = c
+    g = torch.Generator().manual_seed(5)
+    E = torch.rand(N, D, generator=g, dtype=torch.float64) * 0.05  # the rest: far below
+    E[0] = 0.0
+    E[0, : D // 2] = c  # the true top: 64 c^2 = 64.4995 in fp32, 64 in bf16
+    for j in range(1, 41):  # competitors: bf16-exact, on u's exact half, 64.43 .. 64.49 in both precisions
+        E[j] = 0.0
+        n_up = 55 + (j % 9)
+        E[j, D // 2:] = 1.0
+        E[j, D // 2: D // 2 + n_up] = 1.0078125
+    U = u.float()
+    Ef = E.float()
+    S = U.double() @ Ef.double().t()
+    assert int(S[0].argmax()) == 0 and S[0, 0] - S[0, 1:41].max() > 0
+    Ud, Ed = U.to(hip_device), Ef.to(hip_device)
+    img = ops.decoder_image(Ed)
+    emax = ops.row_norm_max(Ed)
+    bf = (U.bfloat16().double() @ Ef.bfloat16().double().t())[0]
+    assert bf[1:41].min() - bf[0] > 0.37 * 1.02  # the 2^-8 bound would have dropped the top item
+    idx, val, flag = ops.topk_fused(Ud, img, Ed, emax, k, with_flags=True)
+    assert int(flag.sum()) == 0
+    assert int(idx[0, 0]) == 0
+    _check(idx, val, U, Ef, k)
+    i2, _ = ops.topk(ops.gemm(Ud, Ed.t()), k)  # the exact score-matrix path
+    assert idx.cpu().tolist() == i2.cpu().tolist()
+
+
+@pytest.mark.timeout(300)
+def test_topk_fused_extent_past_2gb(hip_device):
+    """the bf16 image of 1.5 M items x d 768 is 2.3 GB, past the 2^31-byte extent one buffer
+    resource addresses (hvae_topk.hip splits the sweep into extents with split-relative resources). 64 users must
+    get the float64 ranking of the same fp32 inputs (or a clean HVAE_REQUIRE error, never a wrong answer)."""
+    from hvae import ops
+    R, N, D, k = 64, 1_500_000, 768, 20
+    assert N * D * 2 >= 2 ** 31
+    g = torch.Generator(device=hip_device).manual_seed(1234)
+    Ed = torch.randn(N, D, generator=g, device=hip_device)
+    Ed /= Ed.norm(dim=1, keepdim=True)
+    # users aligned with items spread over the whole range (the last extent included) plus noise
+    tgt = torch.linspace(0, N - 1, R, device=hip_device).long()
+    Ud = (4.0 * Ed[tgt] + 0.5 * torch.randn(R, D, generator=g, device=hip_device) / D ** 0.5).contiguous()
+    img = ops.decoder_image(Ed)
+    emax = ops.row_norm_max(Ed)
+    try:
+        idx, val, flag = ops.topk_fused(Ud, img, Ed, emax, k, with_flags=True)
+    except RuntimeError as e:  # the only acceptable failure: the library refuses the extent itself
+        assert "extent" in str(e).lower() or "2^31" in str(e), e
+        return
+    torch.cuda.synchronize()
+    # float64 reference on the device, in item chunks
+    Ud64 = Ud.double()
+    best_v = torch.full((R, k + 16), -float("inf"), dtype=torch.float64, device=hip_device)
+    best_i = torch.zeros((R, k + 16), dtype=torch.long, device=hip_device)
+    for s in range(0, N, 100_000):
+        Sc = Ud64 @ Ed[s:s + 100_000].double().t()
+        v, i = torch.topk(torch.cat([best_v, Sc], 1), k + 16, dim=1)
+        best_i = torch.gather(torch.cat([best_i, torch.arange(s, s + Sc.shape[1], device=hip_device).expand(R, -1)],
+                                        1), 1, i)
+        best_v = v
+    gi, gv = idx.long(), val.double()
+    tol = 2e-6 * best_v[:, 0].abs().max().item()
+    for r in range(R):
+        cand = sorted(zip(best_v[r].tolist(), best_i[r].tolist()), key=lambda t: (-t[0], -t[1]))[:k]
+        for j in range(k):
+            got = int(gi[r, j])
+            if got != cand[j][1]:
+                assert abs(cand[j][0] - (Ud64[r] @ Ed[got].double()).item()) <= tol, (r, j, got, cand[j])
+            assert abs(gv[r, j].item() - (Ud64[r] @ Ed[got].double()).item()) <= tol, (r, j)
+    assert (gi[:, 0] == tgt).float().mean() > 0.9  # the planted item leads (sanity of the construction)
