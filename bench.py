@@ -175,7 +175,7 @@ def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int,
       longer at peak than reading E once (2 B, 1 B or 4 B per element) takes at 8 TB/s, HBM-bound otherwise.
     gemm: the exact-fp32 MFMA GEMMs of the step: heads, projection forward, and their data and weight
       gradients, 6 B (2 L H + d L + d^2) flop per step, split evenly over the launches per step.
-    adam_rows (lazy exact Adam): p, m, v (24 B per element) of the batch's unique W1t rows and of the 1/8 of
+    adam_rows (lazy exact Adam): p, m, v (24 B per element) of the batch's unique W1t rows and of the 1/period of
       W1t rows the rotating g = 0 sweep brings up to date (plus 8 B per swept row), and p, m, v, g (28 B) of
       the small dense parameters; with HVAE_DENSE_ADAM=1 all N rows.
     encoder_fwd: the gathered W1t rows (nnz H 4 B) + h, xhat (B H 8 B) written.
@@ -211,7 +211,8 @@ def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int,
     put("gemm", "mfma", gemm_flops / n_gemm, PEAK_F32_TFLOPS, "TFLOP/s")
     n_small = fused.layout.n_small
     if fused.lazy_adam:
-        swept = -(-N // 8)
+        from hvae._lib import lib
+        swept = -(-N // int(lib().hvae_adam_lazy_sweep_period()))
         adam_bytes = 24.0 * H * (uniq + swept) + 8.0 * swept + 28.0 * n_small
     else:
         adam_bytes = 24.0 * N * H + 4.0 * N + 28.0 * n_small

@@ -438,6 +438,8 @@ int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v, const hva
  * hvae_adam_lazy_catchup_csr: the same for the rows the CSR batch x lists (duplicates
  *   replayed once), without the W1-gradient plan: the plan can then run beside
  *   the forward. Bitwise equal to hvae_adam_lazy_catchup on the plan's rows. */
+/* Rows of W1t the hvae_adam_lazy sweep brings up to date per step: ceil(N / period) (the longest replay). */
+int hvae_adam_lazy_sweep_period(void);
 int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
                    int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense, int64_t dense_off,
                    int64_t n_dense, void* stream);

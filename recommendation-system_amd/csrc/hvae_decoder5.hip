@@ -997,6 +997,19 @@ __device__ __forceinline__ int pack4(float a, float b, float c, float d) {
 #ifndef DEC5F8_PRIO
 #define DEC5F8_PRIO 0  // A/B: static s_setprio 1 for 1 the consumers, 2 the producers
 #endif
+// Timing-ablation builds only (DEC5_ABL's bits for the fp8 sweep; scripts/build_variant5.sh, outputs invalid by
+// construction): 1 no LDS-DMA pieces in the loop (and no vmcnt waits), 2 no per-tile barrier, 4 no exponentials /
+// P out, 8 GEMM1 A operands not re-read from LDS, 16 GEMM2 operands not re-read, 32 no GEMM1 MFMAs, 64 no GEMM2
+// MFMAs, 128 LDS-DMA pieces issued but never waited for (profiles/r04_dec5_f8_ablation.jsonl)
+#ifndef DEC5F8_ABL
+#define DEC5F8_ABL 0
+#endif
+// DEC5F8_RSTAGE (A/B): the producer's pieces through registers instead of LDS-DMA -- buffer_load_dwordx4 to VGPRs
+// under GEMM1's MFMAs, ds_write_b128 into the free slot after them (same ring, same timing, another mechanism);
+// 2: all 12 pieces of the (ug, hq) pair on the producer that way, none on the consumer
+#ifndef DEC5F8_RSTAGE
+#define DEC5F8_RSTAGE 0
+#endif
 
 template <bool WITH_O>
 __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, int64_t ldu,
@@ -1008,7 +1021,7 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
   constexpr int DB = DW / 32;    // GEMM2 d-blocks (12)
   constexpr int KS = D / 64;     // GEMM1 k-steps (12)
   constexpr int PW = 12;         // 1-KiB LDS-DMA pieces per (ug, hq) per tile
-  constexpr int PB = DEC5F8_DMA_B;
+  constexpr int PB = DEC5F8_RSTAGE == 2 ? 0 : DEC5F8_DMA_B;
   constexpr int PA = PW - PB;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   unsigned char* pbuf = lds + NS * TB8;                                    // [2 par][4 producers][PBY]
@@ -1111,8 +1124,9 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const i32x8 c = ra[ks % AH];
-        if (ks + AH < KS) ra[ks % AH] = rdA(buf, ks + AH);
-        sv = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, uf[ks], sv, 0, 0, 0, sa, 0, sbu);
+        if (!(DEC5F8_ABL & 8) && ks + AH < KS) ra[ks % AH] = rdA(buf, ks + AH);
+        if (!(DEC5F8_ABL & 32)) sv = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, uf[ks], sv, 0, 0, 0, sa, 0, sbu);
+        else sv[0] += (float)(c[0] ^ uf[ks][0]);
         fill(ks);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1154,6 +1168,17 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
       reinterpret_cast<int*>(p_slot(par, q) + 1024)[lane] = e;
     };
     f32x16 s_nx;
+#if DEC5F8_RSTAGE
+    uint4 stg[PA];
+    auto rs_load = [&](uint32_t soff, int i) {
+      stg[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, (int)(soff + (uint32_t)((q * PW + i) * 1024)), 0));
+    };
+    auto rs_write = [&](int slot_i) {
+#pragma unroll
+      for (int i = 0; i < PA; ++i)
+        *reinterpret_cast<uint4*>(lds + slot_i * TB8 + (q * PW + i) * 1024 + lane * 16) = stg[i];
+    };
+#endif
     if (t_beg < t_end) {
       for (int i = 0; i < PA; ++i) issue_piece(tile_soff(t_beg), 0, i, i == 0);
       if (t_beg + 1 < t_end)
@@ -1177,16 +1202,24 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
     for (int t = t_beg; t < t_end; ++t) {
       const int li = t - t_beg;
       const int nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
-      wait_vmcnt<0>();
-      barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
+      if (!(DEC5F8_ABL & (1 | 128))) wait_vmcnt<0>();
+      if (!(DEC5F8_ABL & 2)) barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
       if (t + 1 < t_end) {
         // branch-free DMA: past the split the pieces land in the free slot s_dma (tiles past N read as 0)
         const uint32_t soff_dma = tile_soff(t + 2);
+#if DEC5F8_RSTAGE
         gemm1(lds + nxt * TB8, s_nx, [&](int ks) {
-          if (ks < PA) issue_piece(soff_dma, s_dma, ks, ks == 0);
+          if (ks < PA) rs_load(soff_dma, ks);
         });
+        rs_write(s_dma);
+#else
+        gemm1(lds + nxt * TB8, s_nx, [&](int ks) {
+          if (!(DEC5F8_ABL & 1) && ks < PA) issue_piece(soff_dma, s_dma, ks, ks == 0);
+        });
+#endif
         mh = half_max(t + 1, s_nx);
-        p_out(s_nx, mh, par ^ 1);
+        if (!(DEC5F8_ABL & 4)) p_out(s_nx, mh, par ^ 1);
+        else lsum += (s_nx[0] > 1e30f) ? 0.f : 1.f;  // keeps GEMM1 live, l >= 1: no user flagged
       }
     }
     wait_vmcnt<0>();
@@ -1240,8 +1273,9 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
 #pragma unroll
       for (int db = 0; db < DB; ++db) {
         const i32x8 c = a[db % AH2];
-        if (db + AH2 < DB) a[db % AH2] = rdB(buf, db + AH2);
-        o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
+        if (!(DEC5F8_ABL & 16) && db + AH2 < DB) a[db % AH2] = rdB(buf, db + AH2);
+        if (!(DEC5F8_ABL & 64)) o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(c, pf, o[db], 0, 0, 0, sa, 0, sbp);
+        else o[db][0] += (float)(c[0] ^ pf[0]);
         fill(db);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -1265,8 +1299,8 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
   for (int t = t_beg; t < t_end; ++t) {
     const int li = t - t_beg;
     const int cur = li % NS, s_dma = (li + 2) % NS, par = li & 1;
-    if constexpr (PB > 0) wait_vmcnt<0>();
-    barrier();  // [L]
+    if constexpr (PB > 0) if (!(DEC5F8_ABL & (1 | 128))) wait_vmcnt<0>();
+    if (!(DEC5F8_ABL & 2)) barrier();  // [L]
     // P(t): k-block 0 = item half 0 (elements 0..15), k-block 1 = half 1; lane half h supplies k-block h's scale
     const int4 y0 = reinterpret_cast<const int4*>(p_slot(par, pq0))[lane];
     const int4 y1 = reinterpret_cast<const int4*>(p_slot(par, pq1))[lane];
@@ -1278,7 +1312,7 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
     const uint32_t soff_dma = tile_soff(t + 2);  // branch-free, as the producers'
     gemm2(lds + cur * TB8, pf, sbp, [&](int db) {
       if constexpr (PB > 0)
-        if (db < PB) issue_piece(soff_dma, s_dma, PA + db, db == 0);
+        if (!(DEC5F8_ABL & 1) && db < PB) issue_piece(soff_dma, s_dma, PA + db, db == 0);
     });
   }
   if constexpr (PB > 0) wait_vmcnt<0>();

@@ -393,8 +393,12 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
 // with t) through step t with g = 0 -- skipping rows with a gradient, which the first
 // group owns -- so that no row ever lags more than kLazySweep steps; the rest run the
 // dense segment. Row work is column-parallel (RowMap).
+// The period trades the sweep's bytes (24 H B per swept row) against longer replays in the catch-up: with the
+// hardware square root and reciprocal (adam_elem) the replays are cheap, and at the Syn-10M shard a period of
+// 8 / 16 / 32 ran 11.74 / 11.59 / 11.53 ms per step (adam_rows 457 / 318 / 251 us, catch-up 168 / 172 / 186 us;
+// profiles/r04_lazy_sweep_period_ab.jsonl). Replays stay at most 32 steps long.
 #ifndef HVAE_LAZY_SWEEP
-#define HVAE_LAZY_SWEEP 8
+#define HVAE_LAZY_SWEEP 32
 #endif
 constexpr int kLazySweep = HVAE_LAZY_SWEEP;
 __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restrict__ tab, float* __restrict__ p,
@@ -656,3 +660,5 @@ extern "C" int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len,
   HVAE_LAUNCH_CHECK("k_adam_lazy");
   return HVAE_OK;
 }
+
+extern "C" int hvae_adam_lazy_sweep_period(void) { return hvae::kLazySweep; }
