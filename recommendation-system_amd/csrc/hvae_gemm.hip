@@ -37,6 +37,16 @@ struct GTile {
   static constexpr int LD4 = (BM * GBK / 4 + 255) / 256;             // float4 staged per thread
 };
 constexpr int kRegStages = 12;  // k-tiles a block keeps in flight at once (K per block <= 384)
+// Register-staged k-tiles per instantiation (NST): 12 for k ranges of 5..12 tiles, which load every tile up
+// front; 4 for the rest -- k ranges of at most 4 tiles load up front, longer ones stream through a ring of 4
+// tiles in flight. The 12-tile staging alone holds 192 VGPRs, so a kernel compiled with it runs one wave per SIMD
+// (248 VGPRs + 24 AGPRs at 64 x 64): long-K products (K = d = 768 at the Syn-10M shard) ran with one tile of
+// lookahead at that occupancy (MFMA busy 27 %, profiles/r04_pmc_sq_gemm_syn10m_summary.txt).
+constexpr int kRingStages = 4;
+static int nst_class(int64_t kps) {
+  const int64_t n = (kps + GBK - 1) / GBK;
+  return (n > kRingStages && n <= kRegStages) ? kRegStages : kRingStages;
+}
 
 struct EpiArgs {
   int kind;
@@ -260,7 +270,7 @@ __device__ __forceinline__ void gemm_finish(const GemmP& g, const f32x4 (&acc)[B
 }
 
 // The block (bx, by, bz) of problem g: tile rows by*BM.., columns bx*BN.., k split bz.
-template <bool TA, bool TB, int BM, int BN>
+template <bool TA, bool TB, int BM, int BN, int NST>
 __device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned by, unsigned bz,
                                            float* __restrict__ sA_, float* __restrict__ sB_) {
   using TAo = GTile<BM>;
@@ -372,16 +382,16 @@ __device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned
   };
 
   const int64_t nst = (ke > kb) ? (ke - kb + GBK - 1) / GBK : 0;
-  if (nst > 0 && nst <= kRegStages) {
+  if (nst > 0 && nst <= NST) {
     // short k range (the batch-sized GEMMs of the path): every global load of the block is issued
     // up front -- one memory latency instead of one per k-tile -- then the tiles stream through
     // double-buffered LDS with one barrier each
-    float4 ra[kRegStages][LA], rb[kRegStages][LB];
+    float4 ra[NST][LA], rb[NST][LB];
 #pragma unroll
-    for (int st = 0; st < kRegStages; ++st)
+    for (int st = 0; st < NST; ++st)
       if (st < nst) gload(kb + (int64_t)st * GBK, ra[st], rb[st]);
 #pragma unroll
-    for (int st = 0; st < kRegStages; ++st) {
+    for (int st = 0; st < NST; ++st) {
       if (st < nst) {
         lstore(st & 1, ra[st], rb[st]);
         __syncthreads();
@@ -389,19 +399,22 @@ __device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned
       }
     }
   } else if (nst > 0) {
-    float4 ra[LA], rb[LB];
-    gload(kb, ra, rb);
-    lstore(0, ra, rb);
-    __syncthreads();
-    int buf = 0;
-    for (int64_t k0 = kb; k0 < ke; k0 += GBK) {
-      const bool more = k0 + GBK < ke;
-      if (more) gload(k0 + GBK, ra, rb);
-      compute(buf);
-      if (more) {
-        lstore(buf ^ 1, ra, rb);
-        __syncthreads();
-        buf ^= 1;
+    // long k range: a ring of NST register-staged k-tiles, each slot refilled NST tiles ahead as soon as it
+    // has been copied to LDS (LDS buffer st & 1 was last read by compute(st - 2), which every wave finished
+    // before the barrier of st - 1)
+    float4 ra[NST][LA], rb[NST][LB];
+#pragma unroll
+    for (int u = 0; u < NST; ++u) gload(kb + (int64_t)u * GBK, ra[u], rb[u]);
+    for (int64_t st0 = 0; st0 < nst; st0 += NST) {
+#pragma unroll
+      for (int u = 0; u < NST; ++u) {
+        const int64_t st = st0 + u;
+        if (st < nst) {
+          lstore((int)(st & 1), ra[u], rb[u]);
+          __syncthreads();
+          if (st + NST < nst) gload(kb + (st + NST) * GBK, ra[u], rb[u]);
+          compute((int)(st & 1));
+        }
       }
     }
   }
@@ -580,7 +593,7 @@ __global__ void __launch_bounds__(256) k_gemm_fast(GemmP g) {
 
 // the (dW = dY^T X, dX = dY W) pair of a layer's backward: the weight gradient (long K, split-K) on the
 // fast path in F0 x F0 tiles, the data gradient (short K) on the register-staged kernel in BT1 x BT1 tiles
-template <int F0, int BT1>
+template <int F0, int BT1, int NST1>
 __global__ void __launch_bounds__(256) k_gemm_mixed_pair(GemmP g0, GemmP g1) {
   constexpr int S0 = fast_smem_f4<F0, F0>() * 4, S1 = gemm_smem_floats<BT1>() * 2;
   __shared__ __attribute__((aligned(16))) float smem[S0 > S1 ? S0 : S1];
@@ -591,23 +604,23 @@ __global__ void __launch_bounds__(256) k_gemm_mixed_pair(GemmP g0, GemmP g1) {
                                          reinterpret_cast<float4*>(smem));
   } else {
     b -= n0;
-    gemm_block<false, false, BT1, BT1>(g1, b % g1.gx, (b / g1.gx) % g1.gy, b / (g1.gx * g1.gy), smem,
+    gemm_block<false, false, BT1, BT1, NST1>(g1, b % g1.gx, (b / g1.gx) % g1.gy, b / (g1.gx * g1.gy), smem,
                                        smem + gemm_smem_floats<BT1>());
   }
 }
 
-template <bool TA, bool TB, int BM, int BN>
+template <bool TA, bool TB, int BM, int BN, int NST>
 __global__ void __launch_bounds__(256) k_gemm_f32(GemmP g) {
   __shared__ __attribute__((aligned(16))) float sA[gemm_smem_floats<BM>()];
   __shared__ __attribute__((aligned(16))) float sB[gemm_smem_floats<BN>()];
-  gemm_block<TA, TB, BM, BN>(g, blockIdx.x, blockIdx.y, blockIdx.z, sA, sB);
+  gemm_block<TA, TB, BM, BN, NST>(g, blockIdx.x, blockIdx.y, blockIdx.z, sA, sB);
 }
 
 // Two independent GEMMs in one launch (a weight gradient dW = dY^T X and the data gradient
 // dX = dY W of one layer): the first g0.gx*g0.gy*g0.gz blocks run g0, the rest g1. Both depend
 // only on inputs already complete, so the launch costs max(t0, t1) instead of t0 + t1 plus a
 // kernel boundary.
-template <int BM0, int BM1>
+template <int BM0, int BM1, int NST0, int NST1>
 __global__ void __launch_bounds__(256) k_gemm_f32_pair(GemmP g0, GemmP g1) {
   constexpr int SA = gemm_smem_floats<BM0>() > gemm_smem_floats<BM1>() ? gemm_smem_floats<BM0>()
                                                                        : gemm_smem_floats<BM1>();
@@ -616,10 +629,10 @@ __global__ void __launch_bounds__(256) k_gemm_f32_pair(GemmP g0, GemmP g1) {
   const unsigned n0 = g0.gx * g0.gy * g0.gz;
   unsigned b = blockIdx.x;
   if (b < n0) {
-    gemm_block<true, false, BM0, BM0>(g0, b % g0.gx, (b / g0.gx) % g0.gy, b / (g0.gx * g0.gy), sA, sB);
+    gemm_block<true, false, BM0, BM0, NST0>(g0, b % g0.gx, (b / g0.gx) % g0.gy, b / (g0.gx * g0.gy), sA, sB);
   } else {
     b -= n0;
-    gemm_block<false, false, BM1, BM1>(g1, b % g1.gx, (b / g1.gx) % g1.gy, b / (g1.gx * g1.gy), sA, sB);
+    gemm_block<false, false, BM1, BM1, NST1>(g1, b % g1.gx, (b / g1.gx) % g1.gy, b / (g1.gx * g1.gy), sA, sB);
   }
 }
 
@@ -641,7 +654,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32_multi(GemmMulti m) {
   while (i + 1 < m.n && b >= m.start[i + 1]) ++i;
   b -= m.start[i];
   const GemmP& g = m.g[i];
-  gemm_block<true, false, 32, 32>(g, b % g.gx, (b / g.gx) % g.gy, b / (g.gx * g.gy), sA, sB);
+  gemm_block<true, false, 32, 32, kRingStages>(g, b % g.gx, (b / g.gx) % g.gy, b / (g.gx * g.gy), sA, sB);
 }
 
 // ---------------------------------------------------------------- colsum ---
@@ -854,9 +867,12 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
     HVAE_LAUNCH_CHECK("k_gemm_fast");
     return HVAE_OK;
   }
-#define HVAE_GEMM_CALL(TA_, TB_)                                                 \
-  (bt == 64 ? (k_gemm_f32<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(g))            \
-            : (k_gemm_f32<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(g)))
+  const int nstc = nst_class(g.kps);
+#define HVAE_GEMM_CALL(TA_, TB_)                                                                  \
+  (bt == 64 ? (nstc == kRegStages ? (k_gemm_f32<TA_, TB_, 64, 64, kRegStages><<<grid, 256, 0, st>>>(g))  \
+                                  : (k_gemm_f32<TA_, TB_, 64, 64, kRingStages><<<grid, 256, 0, st>>>(g))) \
+            : (nstc == kRegStages ? (k_gemm_f32<TA_, TB_, 32, 32, kRegStages><<<grid, 256, 0, st>>>(g))  \
+                                  : (k_gemm_f32<TA_, TB_, 32, 32, kRingStages><<<grid, 256, 0, st>>>(g))))
   if (!trans_a && !trans_b) HVAE_GEMM_CALL(false, false);
   else if (!trans_a && trans_b) HVAE_GEMM_CALL(false, true);
   else if (trans_a && !trans_b) HVAE_GEMM_CALL(true, false);
@@ -899,19 +915,31 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
     }
     const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
     ProbeScope probe("gemm", st);
-    if (f0.bm == 64 && bt1 == 64) k_gemm_mixed_pair<64, 64><<<nblk, 256, 0, st>>>(g0, g1);
-    else if (f0.bm == 64) k_gemm_mixed_pair<64, 32><<<nblk, 256, 0, st>>>(g0, g1);
-    else if (bt1 == 64) k_gemm_mixed_pair<32, 64><<<nblk, 256, 0, st>>>(g0, g1);
-    else k_gemm_mixed_pair<32, 32><<<nblk, 256, 0, st>>>(g0, g1);
+    const bool r1 = nst_class(g1.kps) == kRegStages;
+#define HVAE_MIXED(F0_, BT1_)                                                                            \
+  (r1 ? (k_gemm_mixed_pair<F0_, BT1_, kRegStages><<<nblk, 256, 0, st>>>(g0, g1))                         \
+      : (k_gemm_mixed_pair<F0_, BT1_, kRingStages><<<nblk, 256, 0, st>>>(g0, g1)))
+    if (f0.bm == 64 && bt1 == 64) HVAE_MIXED(64, 64);
+    else if (f0.bm == 64) HVAE_MIXED(64, 32);
+    else if (bt1 == 64) HVAE_MIXED(32, 64);
+    else HVAE_MIXED(32, 32);
+#undef HVAE_MIXED
     HVAE_LAUNCH_CHECK("k_gemm_mixed_pair");
     return HVAE_OK;
   }
   const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
   ProbeScope probe("gemm", st);
-  if (bt0 == 64 && bt1 == 64) k_gemm_f32_pair<64, 64><<<nblk, 256, 0, st>>>(g0, g1);
-  else if (bt0 == 64) k_gemm_f32_pair<64, 32><<<nblk, 256, 0, st>>>(g0, g1);
-  else if (bt1 == 64) k_gemm_f32_pair<32, 64><<<nblk, 256, 0, st>>>(g0, g1);
-  else k_gemm_f32_pair<32, 32><<<nblk, 256, 0, st>>>(g0, g1);
+  const bool q0 = nst_class(g0.kps) == kRegStages, q1 = nst_class(g1.kps) == kRegStages;
+#define HVAE_PAIR(B0_, B1_)                                                                              \
+  (q0 ? (q1 ? (k_gemm_f32_pair<B0_, B1_, kRegStages, kRegStages><<<nblk, 256, 0, st>>>(g0, g1))          \
+            : (k_gemm_f32_pair<B0_, B1_, kRegStages, kRingStages><<<nblk, 256, 0, st>>>(g0, g1)))        \
+      : (q1 ? (k_gemm_f32_pair<B0_, B1_, kRingStages, kRegStages><<<nblk, 256, 0, st>>>(g0, g1))         \
+            : (k_gemm_f32_pair<B0_, B1_, kRingStages, kRingStages><<<nblk, 256, 0, st>>>(g0, g1))))
+  if (bt0 == 64 && bt1 == 64) HVAE_PAIR(64, 64);
+  else if (bt0 == 64) HVAE_PAIR(64, 32);
+  else if (bt1 == 64) HVAE_PAIR(32, 64);
+  else HVAE_PAIR(32, 32);
+#undef HVAE_PAIR
   HVAE_LAUNCH_CHECK("k_gemm_f32_pair");
   return HVAE_OK;
 }

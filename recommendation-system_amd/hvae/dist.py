@@ -155,8 +155,12 @@ class DPExchange:
                 send_g=torch.zeros(ns, dtype=torch.float32, device=dev),
                 recv_g=torch.zeros(W, ns, dtype=torch.float32, device=dev),
                 recv_da=torch.zeros(W * B, H, dtype=torch.float32, device=dev),
+                # the two-exchange step gathers the CSR part of the packet only (the small gradients travel in
+                # their own exchange after the backward): [W][row offsets | items | values]
+                recv_csr=torch.zeros(W, L - ns, dtype=torch.float32, device=dev),
                 rp_u=torch.zeros(W * (B + 1), dtype=torch.int64, device=dev),
                 base=(torch.arange(W, dtype=torch.int64, device=dev) * L + ns + B + 1)[:, None],
+                base_csr=(torch.arange(W, dtype=torch.int64, device=dev) * (L - ns) + B + 1)[:, None],
                 rows_u=(torch.arange(W, dtype=torch.int32, device=dev)[:, None] * (B + 1) + j[None, :]).reshape(-1),
                 merged=self._merged[W * cap])
         for k, v in self._plans[key].items():
@@ -223,10 +227,11 @@ class DPExchange:
             self.send_da[:nb].copy_(da[:nb])
 
     def communicate_csr(self) -> None:
+        csr = self.send[self.ns:]  # the packet past the small-gradient words (unused in this exchange)
         if self.world == 1:
-            self.recv[0].copy_(self.send)
+            self.recv_csr[0].copy_(csr)
             return
-        self._all_gather(self.recv.reshape(-1), self.send)
+        self._all_gather(self.recv_csr.reshape(-1), csr)
 
     def communicate_grads(self) -> None:
         if self.world == 1:
@@ -241,9 +246,9 @@ class DPExchange:
         from . import ops
         W, B = self.world, self.B
         rp = self.rp_u.view(W, B + 1)
-        rp.copy_(self.recv[:, self.off_rp:self.off_rp + B + 1].view(torch.int32))
-        rp.add_(self.base)
-        flat = self.recv.reshape(-1)
+        rp.copy_(self.recv_csr[:, :B + 1].view(torch.int32))
+        rp.add_(self.base_csr)
+        flat = self.recv_csr.reshape(-1)
         self._union = ops.Csr(self.rp_u, flat.view(torch.int32), flat[self.cap:], self.n_items, rows=self.rows_u,
                               nb=W * B)
         ops.w1_rowgrad_plan(self._union, self.merged)

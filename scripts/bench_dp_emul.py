@@ -51,8 +51,8 @@ def make_emul_exchange(world, device, n_items, H, n_small, packets_fn):
 
         def communicate_csr(self):
             pk = packets_fn(self.B, self.cap, self.L)  # [W - 1, batches, L] on the device
-            self.recv[0].copy_(self.send)
-            self.recv[1:].copy_(pk[:, self.step_i % pk.shape[1]])
+            self.recv_csr[0].copy_(self.send[self.ns:])
+            self.recv_csr[1:].copy_(pk[:, self.step_i % pk.shape[1], self.ns:])
 
         def communicate_grads(self):
             self.recv_g[0].copy_(self.send_g)
@@ -154,7 +154,8 @@ def main():
             info["union_unique_rows_last_step"] = int(fused.dp.merged.n_unique.item())
             # the bytes rank 0 receives per step through the two all-gathers (CSR packets, small gradients, da)
             L = fused.dp.L
-            info["allgather_recv_bytes_per_step"] = int((W - 1) * (4 * L + 4 * fused.layout.n_small + 4 * B * H))
+            info["allgather_recv_bytes_per_step"] = int((W - 1) * (4 * (L - fused.layout.n_small) + 4 * fused.layout.n_small
+                                                                 + 4 * B * H))
         out = {"probe": "dp_emul", "workload": args.workload, "world": W, "B": B, "steps": args.steps,
                "ms_per_step": round(el / args.steps * 1e3, 4), **info}
         print(json.dumps(out), flush=True)
