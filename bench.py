@@ -212,7 +212,7 @@ def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int,
     n_small = fused.layout.n_small
     if fused.lazy_adam:
         from hvae._lib import lib
-        swept = -(-N // int(lib().hvae_adam_lazy_sweep_period()))
+        swept = -(-N // int(lib().hvae_adam_lazy_sweep_period(N)))
         adam_bytes = 24.0 * H * (uniq + swept) + 8.0 * swept + 28.0 * n_small
     else:
         adam_bytes = 24.0 * N * H + 4.0 * N + 28.0 * n_small

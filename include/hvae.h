@@ -427,7 +427,10 @@ int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v, const hva
  * step, with g = 0 for rows outside the batch; those steps are a fixed map per
  * step, so they are deferred and replayed -- the same float operations in the
  * same order, bitwise equal to updating eagerly -- when the row is next needed.
- *   last_step [N] int32: steps already applied to each row (start at 0)
+ *   last_step [N] int32: steps already applied to each row (start at 0): bits 0-23 to m and v, bits 24-29 how
+ *                        many steps further p is (hvae_adam_lazy_catchup_csr moves p alone when weight_decay
+ *                        is 0: the forward reads only p, and the step's hvae_adam_lazy replays m and v itself);
+ *                        steps stay below 2^24 (tab_len <= 2^24)
  *   tab [tab_len][2] float: per-step (lr / bc1_t, 1 / sqrt(bc2_t)), entry t written
  *                           by step t's hvae_adam_lazy; tab_len > total steps
  * hvae_adam_lazy: step t = *cfg->step_dev + 1 for the dense segment and for the
@@ -437,9 +440,11 @@ int hvae_adam_flat(const hvae_adam* cfg, float* p, float* m, float* v, const hva
  *   or all N rows when rows == NULL (before anything else reads W1t, m or v).
  * hvae_adam_lazy_catchup_csr: the same for the rows the CSR batch x lists (duplicates
  *   replayed once), without the W1-gradient plan: the plan can then run beside
- *   the forward. Bitwise equal to hvae_adam_lazy_catchup on the plan's rows. */
-/* Rows of W1t the hvae_adam_lazy sweep brings up to date per step: ceil(N / period) (the longest replay). */
-int hvae_adam_lazy_sweep_period(void);
+ *   the forward. Its p is bitwise that of hvae_adam_lazy_catchup on the plan's rows (m and v may stay behind,
+ *   as last_step records, until the step's hvae_adam_lazy or a catch-up over all rows). */
+/* The hvae_adam_lazy sweep period for N items: ceil(N / period) W1t rows are brought up to date per step, and
+ * no replay is longer than period steps (32 from 65,536 items, else 8). */
+int hvae_adam_lazy_sweep_period(int64_t N);
 int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
                    int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense, int64_t dense_off,
                    int64_t n_dense, void* stream);

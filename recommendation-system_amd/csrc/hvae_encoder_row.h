@@ -59,7 +59,7 @@ __device__ __forceinline__ void ln_gelu_drop_row(float4 (&acc)[NV], int lane, in
       const uint64_t idx = (uint64_t)(row * H + e + i);
       o[i] = train ? g * dropout_mult(p_drop, scale, drop_mult, idx, seed, step, tag) : g;
     }
-    *reinterpret_cast<float4*>(h_out + row * H + e) = make_float4(o[0], o[1], o[2], o[3]);
+    if (h_out) *reinterpret_cast<float4*>(h_out + row * H + e) = make_float4(o[0], o[1], o[2], o[3]);
     if (h_lds) *reinterpret_cast<float4*>(h_lds + e) = make_float4(o[0], o[1], o[2], o[3]);
   }
 }

@@ -43,9 +43,14 @@ constexpr int kRegStages = 12;  // k-tiles a block keeps in flight at once (K pe
 // (248 VGPRs + 24 AGPRs at 64 x 64): long-K products (K = d = 768 at the Syn-10M shard) ran with one tile of
 // lookahead at that occupancy (MFMA busy 27 %, profiles/r04_pmc_sq_gemm_syn10m_summary.txt).
 constexpr int kRingStages = 4;
-static int nst_class(int64_t kps) {
+// The 4-tile ring pays for the x W^T products (row-major A, B^T: the forward layers, K = d = 768: 4096x768x768
+// 77 -> 68 us); the [k][n] B of the x W data gradients ran slower on it (4096x768x768 79 -> 82 us), so those keep
+// one tile of lookahead (profiles/r04_gemm_ring_shapes.jsonl).
+static int nst_class(bool ta, bool tb, int64_t kps) {
   const int64_t n = (kps + GBK - 1) / GBK;
-  return (n > kRingStages && n <= kRegStages) ? kRegStages : kRingStages;
+  if (n <= kRingStages) return kRingStages;
+  if (n <= kRegStages) return kRegStages;
+  return (!ta && tb) ? kRingStages : kRegStages;
 }
 
 struct EpiArgs {
@@ -398,6 +403,23 @@ __device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned
         compute(st & 1);
       }
     }
+  } else if (nst > 0 && NST != kRingStages) {
+    // long k range, one k-tile of lookahead (the kRegStages instantiation keeps its registers for the short path)
+    float4 ra[LA], rb[LB];
+    gload(kb, ra, rb);
+    lstore(0, ra, rb);
+    __syncthreads();
+    int buf = 0;
+    for (int64_t k0 = kb; k0 < ke; k0 += GBK) {
+      const bool more = k0 + GBK < ke;
+      if (more) gload(k0 + GBK, ra, rb);
+      compute(buf);
+      if (more) {
+        lstore(buf ^ 1, ra, rb);
+        __syncthreads();
+        buf ^= 1;
+      }
+    }
   } else if (nst > 0) {
     // long k range: a ring of NST register-staged k-tiles, each slot refilled NST tiles ahead as soon as it
     // has been copied to LDS (LDS buffer st & 1 was last read by compute(st - 2), which every wave finished
@@ -736,7 +758,20 @@ static FastPlan fast_plan(bool ta, bool tb, int64_t M, int64_t N, int64_t K, con
   FastPlan f;
   const char* e = ab_getenv("HVAE_GEMM_FAST");
   if (e && std::atoi(e) == 0) return f;
-  if (!ta || tb) return f;
+  if (!ta) {
+    // HVAE_GEMM_FAST_SHORT=1 (A/B): the batch GEMMs (x W^T, x W; K = d, H or 2L) on the fast path too, one k range
+    const char* fs = ab_getenv("HVAE_GEMM_FAST_SHORT");
+    if (!fs || std::atoi(fs) == 0) return f;
+    if (K % FBK || ((uintptr_t)A) % 16 || ((uintptr_t)B) % 16 || lda % 4 || ldb % 4) return f;
+    int bt = cdiv(M, 64) * cdiv(N, 64) >= 256 ? 64 : 32;
+    if (const char* t = ab_getenv("HVAE_GEMM_FAST_TILE")) bt = std::atoi(t) == 64 ? 64 : 32;
+    if (M % bt || N % bt) return f;
+    f.bm = f.bn = bt;
+    f.splits = 1;
+    f.kps = K;
+    return f;
+  }
+  if (tb) return f;
   if (K < 1024 || K % FBK || ((uintptr_t)A) % 16 || ((uintptr_t)B) % 16 || lda % 4 || ldb % 4) return f;
   int bt = cdiv(M, 32) * cdiv(N, 32) <= 256 ? 32 : 64;
   if (const char* t = ab_getenv("HVAE_GEMM_FAST_TILE")) bt = std::atoi(t) == 64 ? 64 : 32;
@@ -861,13 +896,20 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
   hipStream_t st = as_stream(stream);
   dim3 grid(g.gx, g.gy, g.gz);
   ProbeScope probe("gemm", st);
-  if (f.bm) {  // trans_a && !trans_b
-    if (f.bm == 64) k_gemm_fast<true, false, 64, 64><<<grid, 256, 0, st>>>(g);
-    else k_gemm_fast<true, false, 32, 32><<<grid, 256, 0, st>>>(g);
+  if (f.bm) {  // trans_a && !trans_b (or, under HVAE_GEMM_FAST_SHORT, !trans_a)
+#define HVAE_FAST_CALL(TA_, TB_)                                                  \
+  (f.bm == 64 ? (k_gemm_fast<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(g))        \
+              : (k_gemm_fast<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(g)))
+    if (trans_a) HVAE_FAST_CALL(true, false);
+#ifdef HVAE_AB
+    else if (trans_b) HVAE_FAST_CALL(false, true);
+    else HVAE_FAST_CALL(false, false);
+#endif
+#undef HVAE_FAST_CALL
     HVAE_LAUNCH_CHECK("k_gemm_fast");
     return HVAE_OK;
   }
-  const int nstc = nst_class(g.kps);
+  const int nstc = nst_class(trans_a, trans_b, g.kps);
 #define HVAE_GEMM_CALL(TA_, TB_)                                                                  \
   (bt == 64 ? (nstc == kRegStages ? (k_gemm_f32<TA_, TB_, 64, 64, kRegStages><<<grid, 256, 0, st>>>(g))  \
                                   : (k_gemm_f32<TA_, TB_, 64, 64, kRingStages><<<grid, 256, 0, st>>>(g))) \
@@ -915,7 +957,7 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
     }
     const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
     ProbeScope probe("gemm", st);
-    const bool r1 = nst_class(g1.kps) == kRegStages;
+    const bool r1 = nst_class(false, false, g1.kps) == kRegStages;
 #define HVAE_MIXED(F0_, BT1_)                                                                            \
   (r1 ? (k_gemm_mixed_pair<F0_, BT1_, kRegStages><<<nblk, 256, 0, st>>>(g0, g1))                         \
       : (k_gemm_mixed_pair<F0_, BT1_, kRingStages><<<nblk, 256, 0, st>>>(g0, g1)))
@@ -929,7 +971,7 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
   }
   const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
   ProbeScope probe("gemm", st);
-  const bool q0 = nst_class(g0.kps) == kRegStages, q1 = nst_class(g1.kps) == kRegStages;
+  const bool q0 = nst_class(true, false, g0.kps) == kRegStages, q1 = nst_class(false, false, g1.kps) == kRegStages;
 #define HVAE_PAIR(B0_, B1_)                                                                              \
   (q0 ? (q1 ? (k_gemm_f32_pair<B0_, B1_, kRegStages, kRegStages><<<nblk, 256, 0, st>>>(g0, g1))          \
             : (k_gemm_f32_pair<B0_, B1_, kRegStages, kRingStages><<<nblk, 256, 0, st>>>(g0, g1)))        \

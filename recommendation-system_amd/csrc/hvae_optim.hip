@@ -129,6 +129,24 @@ __device__ __forceinline__ void adam_elem0(float& p, float& m, float& v, const A
   p = p - k.lr_over_bc1 * (m * __builtin_amdgcn_rcpf(denom));
 }
 
+// the m, v half of adam_elem0 / adam_elem at g = 0 (wd only enters through g, which m and v see as
+// g + wd p: with wd != 0 a p-only replay is not possible, and the CSR catch-up does not use it then)
+__device__ __forceinline__ void adam_mv0(float& m, float& v, const AdamK& k) {
+#pragma clang fp contract(off)
+  m = m - k.omb1 * m;
+  v = v * k.b2;
+}
+
+// last_step[j] of a W1t row: bits 0-23 the steps applied to m and v, bits 24-29 how many steps further p is
+// (set by the CSR catch-up, which moves p alone: the forward reads only p, and the update that follows in the
+// same step replays m and v itself, so the catch-up stores 4 B per element instead of 12); 0 in bits 24-29
+// means p is where m and v are. Steps stay below 2^24 (hvae_adam_lazy's table length).
+constexpr int kStepBits = 24;
+constexpr int32_t kStepMask = (1 << kStepBits) - 1;
+constexpr int kPAheadMax = 63;
+__device__ __forceinline__ int ls_mv(int32_t ls) { return ls & kStepMask; }
+__device__ __forceinline__ int ls_p(int32_t ls) { return (ls & kStepMask) + ((ls >> kStepBits) & kPAheadMax); }
+
 struct AdamArgs {
   double lr, b1, b2, eps, wd;
   const int64_t* step_dev;
@@ -280,22 +298,41 @@ static inline RowMap row_map(int64_t H) {
 }
 
 // float4 column i of a row: replay steps (from, to] with g = 0 (constants from the step table,
-// loaded 8 at a time), then, if `step`, one more step with constants kx and gradient gx.
-__device__ __forceinline__ void col_update(const AdamArgs& a, const float2* __restrict__ tab, float* __restrict__ p,
-                                           float* __restrict__ m, float* __restrict__ v, int64_t i, int from, int to,
-                                           bool step, const AdamK& kx, float4 gx) {
-  float4 pp = reinterpret_cast<float4*>(p)[i];
-  float4 mm = reinterpret_cast<float4*>(m)[i];
-  float4 vv = reinterpret_cast<float4*>(v)[i];
-  for (int s0 = from + 1; s0 <= to; s0 += 8) {
-    float2 c[8];
+// loaded 8 at a time), then, if `step`, one more step with constants kx and gradient gx. Split into load / math /
+// store so that the row loops below keep kAdamUnroll rows' loads in flight together (one row group per barrier
+// was one memory round trip per iteration: the row kernels ran at ~4.3 TB/s).
+struct ColState {
+  float4 p, m, v;
+};
+__device__ __forceinline__ ColState col_load(const float* p, const float* m, const float* v, int64_t i) {
+  return ColState{reinterpret_cast<const float4*>(p)[i], reinterpret_cast<const float4*>(m)[i],
+                  reinterpret_cast<const float4*>(v)[i]};
+}
+__device__ __forceinline__ void col_store(float* p, float* m, float* v, int64_t i, const ColState& c) {
+  reinterpret_cast<float4*>(p)[i] = c.p;
+  reinterpret_cast<float4*>(m)[i] = c.m;
+  reinterpret_cast<float4*>(v)[i] = c.v;
+}
+// m, v at step `from`, p at step `pstep` >= from (the CSR catch-up moves p ahead alone, below): steps from + 1 ..
+// pstep move m and v only, the rest all three -- the same float operations on m and v either way
+constexpr int kTabAhead = 4;  // step-table entries loaded ahead per replay round
+__device__ __forceinline__ void col_math_lazy(const AdamArgs& a, const float2* __restrict__ tab, ColState& cs, int from,
+                                              int pstep, int to, bool step, const AdamK& kx, float4 gx) {
+  float4 &pp = cs.p, &mm = cs.m, &vv = cs.v;
+  for (int s0 = from + 1; s0 <= to; s0 += kTabAhead) {
+    float2 c[kTabAhead];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) c[u] = (s0 + u <= to) ? tab[s0 + u] : make_float2(0.f, 1.f);
+    for (int u = 0; u < kTabAhead; ++u) c[u] = (s0 + u <= to) ? tab[s0 + u] : make_float2(0.f, 1.f);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < kTabAhead; ++u) {
       if (s0 + u > to) break;
       const AdamK k = adam_consts_tab(a, c[u]);
-      if (k.wd == 0.f) {
+      if (s0 + u <= pstep) {
+        adam_mv0(mm.x, vv.x, k);
+        adam_mv0(mm.y, vv.y, k);
+        adam_mv0(mm.z, vv.z, k);
+        adam_mv0(mm.w, vv.w, k);
+      } else if (k.wd == 0.f) {
         adam_elem0(pp.x, mm.x, vv.x, k);
         adam_elem0(pp.y, mm.y, vv.y, k);
         adam_elem0(pp.z, mm.z, vv.z, k);
@@ -314,10 +351,20 @@ __device__ __forceinline__ void col_update(const AdamArgs& a, const float2* __re
     adam_elem(pp.z, mm.z, vv.z, gx.z, kx);
     adam_elem(pp.w, mm.w, vv.w, gx.w, kx);
   }
-  reinterpret_cast<float4*>(p)[i] = pp;
-  reinterpret_cast<float4*>(m)[i] = mm;
-  reinterpret_cast<float4*>(v)[i] = vv;
 }
+__device__ __forceinline__ void col_math(const AdamArgs& a, const float2* __restrict__ tab, ColState& cs, int from,
+                                         int to, bool step, const AdamK& kx, float4 gx) {
+  col_math_lazy(a, tab, cs, from, from, to, step, kx, gx);
+}
+__device__ __forceinline__ void col_update(const AdamArgs& a, const float2* __restrict__ tab, float* __restrict__ p,
+                                           float* __restrict__ m, float* __restrict__ v, int64_t i, int from, int to,
+                                           bool step, const AdamK& kx, float4 gx) {
+  ColState c = col_load(p, m, v, i);
+  col_math(a, tab, c, from, to, step, kx, gx);
+  col_store(p, m, v, i, c);
+}
+constexpr int kCatchupBlocks = 1024;  // k_adam_catchup_csr: blocks to aim for over a small batch
+constexpr int kAdamUnroll = 4;  // row groups (rows x float4 columns) per barrier in the row kernels
 
 // Bring rows up to the completed step count *step: the batch's rows (item_of /
 // n_unique) or, with item_of == NULL, all N rows.
@@ -331,16 +378,37 @@ __global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* 
   const int64_t H4 = H / 4;
   const int rr = threadIdx.x / rm.h4s, c0 = threadIdx.x % rm.h4s;
   const AdamK none{};
-  for (int64_t g0 = (int64_t)blockIdx.x * rm.rpb; g0 < nrows; g0 += (int64_t)gridDim.x * rm.rpb) {
-    const int64_t r = g0 + rr;
-    const bool act = rr < rm.rpb && r < nrows;
-    const int64_t j = act ? (item_of ? (int64_t)item_of[r] : r) : 0;
-    const int from = act ? last_step[j] : to;
-    if (from < to)
-      for (int64_t c = c0; c < H4; c += rm.h4s)
-        col_update(a, tab, p, m, v, j * H4 + c, from, to, false, none, make_float4(0.f, 0.f, 0.f, 0.f));
+  constexpr int U = kAdamUnroll;
+  const int64_t span = (int64_t)rm.rpb * U;
+  for (int64_t g0 = (int64_t)blockIdx.x * span; g0 < nrows; g0 += (int64_t)gridDim.x * span) {
+    int64_t j[U];
+    int from[U], pst[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t r = g0 + (int64_t)u * rm.rpb + rr;
+      const bool act = rr < rm.rpb && r < nrows;
+      j[u] = act ? (item_of ? (int64_t)item_of[r] : r) : 0;
+      const int32_t ls = act ? last_step[j[u]] : to;
+      from[u] = ls_mv(ls);
+      pst[u] = ls_p(ls);
+    }
+    for (int64_t c = c0; c < H4; c += rm.h4s) {
+      ColState cs[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (from[u] < to) cs[u] = col_load(p, m, v, j[u] * H4 + c);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (from[u] < to)
+          col_math_lazy(a, tab, cs[u], from[u], pst[u], to, false, none, make_float4(0.f, 0.f, 0.f, 0.f));
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (from[u] < to) col_store(p, m, v, j[u] * H4 + c, cs[u]);
+    }
     __syncthreads();
-    if (act && c0 == 0 && from < to) last_step[j] = to;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (c0 == 0 && from[u] < to) last_step[j[u]] = to;
   }
 }
 
@@ -348,39 +416,75 @@ __global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* 
 // that it does not wait for the plan (which then runs beside the forward on another stream). A row listed
 // by several entries is claimed once: the entry's thread moves last_step[j] from its value to `to` with an
 // atomicCAS, and only the winner's row is replayed; the replayed arithmetic is the same, so the result is
-// bitwise that of k_adam_catchup. One block per batch row (grid-stride): all its entries claim at once,
-// then every thread walks the claimed rows' float4 columns (no barrier between rows).
+// bitwise that of k_adam_catchup. Blocks take (batch row, slice) pairs: slice s of a row is its entries
+// s, s + S, s + 2 S, .. (S slices per row, so that a small batch still spreads its rows' replays over the
+// machine: at B = 64 one block per row left 64 blocks walking ~20 rows each, one memory round trip after
+// another); all of a group's entries claim at once, then every thread walks the claimed rows' float4 columns.
 __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const float2* __restrict__ tab, float* p,
                                                           float* m, float* v, int32_t* __restrict__ last_step,
-                                                          hvae_csr_batch x, int64_t H) {
-  __shared__ int s_j[256], s_from[256];
+                                                          hvae_csr_batch x, int64_t H, int S) {
+  __shared__ int s_j[256], s_from[256], s_pst[256];
   __shared__ int s_n;
   const int to = (int)load_step(a.step_dev);
   const int64_t H4 = H / 4;
   const AdamK none{};
-  for (int64_t b = blockIdx.x; b < x.nb; b += gridDim.x) {
+  // p alone moves ahead unless weight decay couples m, v to p, or m, v are too far behind to say so in the stamp
+  const bool p_only_ok = a.wd == 0.0;
+  const int sl = (int)(blockIdx.x % (unsigned)S);
+  for (int64_t b = blockIdx.x / S; b < x.nb; b += gridDim.x / S) {
     const int64_t r = batch_row(x.rows, x.rows_offset, b);
     const int64_t e0 = x.row_ptr[r], e1 = x.row_ptr[r + 1];
-    for (int64_t g0 = e0; g0 < e1; g0 += 256) {
+    const int64_t cnt = e1 - e0 > sl ? (e1 - e0 - sl + S - 1) / S : 0;  // this slice's entries
+    for (int64_t g0 = 0; g0 < cnt; g0 += 256) {
       if (threadIdx.x == 0) s_n = 0;
       __syncthreads();
-      const int64_t e = g0 + threadIdx.x;
-      if (e < e1) {
-        const int j = x.col_idx[e];
-        // one atomic claims the row: the block that raises last_step[j] to `to` replays steps from..to - 1
-        const int from = atomicMax(last_step + j, to);
-        if (from < to) {
-          const int k = atomicAdd(&s_n, 1);
-          s_j[k] = j;
-          s_from[k] = from;
+      const int64_t i = g0 + threadIdx.x;
+      if (i < cnt) {
+        const int j = x.col_idx[e0 + sl + i * S];
+        // one compare-and-swap claims the row: the entry that moves last_step[j] from its value to the caught-up
+        // stamp replays it; entries that find p already at `to` (another entry claimed it) do nothing
+        int32_t old = __hip_atomic_load(last_step + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (ls_p(old) < to) {
+          const int mv = ls_mv(old);
+          const bool p_only = p_only_ok && to - mv <= kPAheadMax;
+          const int32_t want = p_only ? (int32_t)(mv | ((to - mv) << kStepBits)) : (int32_t)to;
+          if (__hip_atomic_compare_exchange_strong(last_step + j, &old, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT)) {
+            const int k = atomicAdd(&s_n, 1);
+            s_j[k] = j;
+            s_from[k] = p_only ? -1 - mv : mv;  // negative: store p only
+            s_pst[k] = ls_p(old);
+            break;
+          }
         }
       }
       __syncthreads();
       const int64_t work = (int64_t)s_n * H4;
-      for (int64_t idx = threadIdx.x; idx < work; idx += blockDim.x) {
-        const int k = (int)(idx / H4);
-        col_update(a, tab, p, m, v, (int64_t)s_j[k] * H4 + idx % H4, s_from[k], to, false, none,
-                   make_float4(0.f, 0.f, 0.f, 0.f));
+      constexpr int U = kAdamUnroll;
+      for (int64_t i0 = threadIdx.x; i0 < work; i0 += (int64_t)blockDim.x * U) {
+        ColState cs[U];
+        int64_t col[U];
+        int fr[U], ps[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t idx = i0 + (int64_t)u * blockDim.x;
+          const int k = idx < work ? (int)(idx / H4) : 0;
+          col[u] = idx < work ? (int64_t)s_j[k] * H4 + idx % H4 : -1;
+          fr[u] = s_from[k];
+          ps[u] = s_pst[k];
+          if (col[u] >= 0) cs[u] = col_load(p, m, v, col[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (col[u] >= 0)
+            col_math_lazy(a, tab, cs[u], fr[u] < 0 ? -1 - fr[u] : fr[u], ps[u], to, false, none,
+                          make_float4(0.f, 0.f, 0.f, 0.f));
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (col[u] < 0) continue;
+          if (fr[u] < 0) reinterpret_cast<float4*>(p)[col[u]] = cs[u].p;
+          else col_store(p, m, v, col[u], cs[u]);
+        }
       }
       __syncthreads();
     }
@@ -389,18 +493,25 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
 
 // The step's update with lazy W1t. Blocks [0, nb_rows) take the gradient rows
 // (replay missed steps, then step t = *step + 1 with the clipped gradient);
-// blocks [nb_rows, nb_rows + nb_sweep) bring one of kLazySweep row ranges (rotating
+// blocks [nb_rows, nb_rows + nb_sweep) bring one of `period` row ranges (rotating
 // with t) through step t with g = 0 -- skipping rows with a gradient, which the first
-// group owns -- so that no row ever lags more than kLazySweep steps; the rest run the
+// group owns -- so that no row ever lags more than `period` steps; the rest run the
 // dense segment. Row work is column-parallel (RowMap).
 // The period trades the sweep's bytes (24 H B per swept row) against longer replays in the catch-up: with the
 // hardware square root and reciprocal (adam_elem) the replays are cheap, and at the Syn-10M shard a period of
 // 8 / 16 / 32 ran 11.74 / 11.59 / 11.53 ms per step (adam_rows 457 / 318 / 251 us, catch-up 168 / 172 / 186 us;
-// profiles/r04_lazy_sweep_period_ab.jsonl). Replays stay at most 32 steps long.
+// profiles/r04_lazy_sweep_period_ab.jsonl), at Syn-1M (N = 100 K) 32 saved 11 us; but where a batch touches a
+// large share of the items (All_Beauty, N = 12,101: ~500 rows a step) the catch-up's longer replays cost more
+// than the sweep saves (0.136 -> 0.146 ms per step at 32), so small item counts keep 8. Replays stay at most
+// `period` steps long. HVAE_LAZY_SWEEP forces one period for every N.
 #ifndef HVAE_LAZY_SWEEP
-#define HVAE_LAZY_SWEEP 32
+#define HVAE_LAZY_SWEEP 0
 #endif
-constexpr int kLazySweep = HVAE_LAZY_SWEEP;
+constexpr int64_t kLazySweepLargeN = 65536;
+static int lazy_sweep_period(int64_t N) {
+  if (HVAE_LAZY_SWEEP > 0) return HVAE_LAZY_SWEEP;
+  return N >= kLazySweepLargeN ? 32 : 8;
+}
 __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restrict__ tab, float* __restrict__ p,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    int32_t* __restrict__ last_step, const float* __restrict__ rows,
@@ -408,7 +519,8 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
                                                    const int32_t* __restrict__ item_of,
                                                    const int32_t* __restrict__ n_unique, int64_t N, int64_t H,
                                                    const float* __restrict__ g_dense, int64_t dense_off,
-                                                   int64_t n_dense, int nb_rows, int nb_sweep, RowMap rm) {
+                                                   int64_t n_dense, int nb_rows, int nb_sweep, int period,
+                                                   RowMap rm) {
   const int t = (int)load_step(a.step_dev) + 1;
   // tab[t] is written by hvae_clip_grad_norm_step_adam just before; a zero entry means no one did
   const float2 c0t = tab[t];
@@ -419,39 +531,87 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
   const int nu = *n_unique;
   const int64_t H4 = H / 4;
   const int rr = threadIdx.x / rm.h4s, cc = threadIdx.x % rm.h4s;
+  constexpr int U = kAdamUnroll;
+  const int64_t span = (int64_t)rm.rpb * U;
   if ((int)blockIdx.x < nb_rows) {
-    for (int64_t g0 = (int64_t)blockIdx.x * rm.rpb; g0 < nu; g0 += (int64_t)nb_rows * rm.rpb) {
-      const int64_t sidx = g0 + rr;
-      const bool act = rr < rm.rpb && sidx < nu;
-      const int64_t j = act ? (int64_t)item_of[sidx] : 0;
-      const int from = act ? last_step[j] : t;
-      if (act)
-        for (int64_t c = cc; c < H4; c += rm.h4s) {
-          float4 gv = *reinterpret_cast<const float4*>(rows + sidx * H + 4 * c);
-          gv.x *= coef; gv.y *= coef; gv.z *= coef; gv.w *= coef;
-          col_update(a, tab, p, m, v, j * H4 + c, from, t - 1, true, k, gv);
-        }
+    for (int64_t g0 = (int64_t)blockIdx.x * span; g0 < nu; g0 += (int64_t)nb_rows * span) {
+      int64_t sidx[U], j[U];
+      int from[U], pst[U];
+      bool act[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        sidx[u] = g0 + (int64_t)u * rm.rpb + rr;
+        act[u] = rr < rm.rpb && sidx[u] < nu;
+        j[u] = act[u] ? (int64_t)item_of[sidx[u]] : 0;
+        const int32_t ls = act[u] ? last_step[j[u]] : t;
+        from[u] = ls_mv(ls);
+        pst[u] = ls_p(ls);
+      }
+      for (int64_t c = cc; c < H4; c += rm.h4s) {
+        ColState cs[U];
+        float4 gv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (act[u]) {
+            cs[u] = col_load(p, m, v, j[u] * H4 + c);
+            gv[u] = *reinterpret_cast<const float4*>(rows + sidx[u] * H + 4 * c);
+          }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (act[u]) {
+            float4 g = gv[u];
+            g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
+            col_math_lazy(a, tab, cs[u], from[u], pst[u], t - 1, true, k, g);
+          }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (act[u]) col_store(p, m, v, j[u] * H4 + c, cs[u]);
+      }
       __syncthreads();
-      if (act && cc == 0) last_step[j] = t;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (act[u] && cc == 0) last_step[j[u]] = t;
     }
   } else if ((int)blockIdx.x < nb_rows + nb_sweep) {
-    const int64_t chunk = (N + kLazySweep - 1) / kLazySweep;
-    const int64_t r0 = (int64_t)((t - 1) % kLazySweep) * chunk, r1 = min(N, r0 + chunk);
-    for (int64_t g0 = r0 + (int64_t)(blockIdx.x - nb_rows) * rm.rpb; g0 < r1; g0 += (int64_t)nb_sweep * rm.rpb) {
-      const int64_t j = g0 + rr;
-      bool act = rr < rm.rpb && j < r1;
-      int from = t;
-      if (act) {
-        const int sl = slot_of[j];
-        if (sl >= 0 && sl < nu && item_of[sl] == (int32_t)j) act = false;  // has a gradient: first group's row
-        else from = last_step[j];
+    const int64_t chunk = (N + period - 1) / period;
+    const int64_t r0 = (int64_t)((t - 1) % period) * chunk, r1 = min(N, r0 + chunk);
+    for (int64_t g0 = r0 + (int64_t)(blockIdx.x - nb_rows) * span; g0 < r1; g0 += (int64_t)nb_sweep * span) {
+      int64_t j[U];
+      int from[U], pst[U];
+      bool act[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        j[u] = g0 + (int64_t)u * rm.rpb + rr;
+        act[u] = rr < rm.rpb && j[u] < r1;
+        from[u] = pst[u] = t;
+        if (act[u]) {
+          const int sl = slot_of[j[u]];
+          if (sl >= 0 && sl < nu && item_of[sl] == (int32_t)j[u]) {
+            act[u] = false;  // has a gradient: first group's row
+          } else {
+            const int32_t ls = last_step[j[u]];
+            from[u] = ls_mv(ls);
+            pst[u] = ls_p(ls);
+          }
+        }
+        act[u] = act[u] && from[u] < t;
       }
-      act = act && from < t;
-      if (act)
-        for (int64_t c = cc; c < H4; c += rm.h4s)
-          col_update(a, tab, p, m, v, j * H4 + c, from, t - 1, true, k, make_float4(0.f, 0.f, 0.f, 0.f));
+      for (int64_t c = cc; c < H4; c += rm.h4s) {
+        ColState cs[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (act[u]) cs[u] = col_load(p, m, v, j[u] * H4 + c);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (act[u]) col_math_lazy(a, tab, cs[u], from[u], pst[u], t - 1, true, k, make_float4(0.f, 0.f, 0.f, 0.f));
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (act[u]) col_store(p, m, v, j[u] * H4 + c, cs[u]);
+      }
       __syncthreads();
-      if (act && cc == 0) last_step[j] = t;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (act[u] && cc == 0) last_step[j[u]] = t;
     }
   } else {
     // the small dense parameters: float4 where the segment is 16-B aligned, scalar tail
@@ -615,7 +775,7 @@ extern "C" int hvae_adam_lazy_catchup(const hvae_adam* cfg, const float* tab, fl
   if (N == 0) return HVAE_OK;
   const int64_t nrows = rows ? rows->cap : N;
   const RowMap rm = row_map(H);
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(nrows, rm.rpb), 16384));
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(nrows, (int64_t)rm.rpb * kAdamUnroll), 16384));
   ProbeScope probe("adam_catchup", as_stream(stream));
   k_adam_catchup<<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v, last_step,
                                                       rows ? rows->item_of : nullptr,
@@ -630,9 +790,12 @@ extern "C" int hvae_adam_lazy_catchup_csr(const hvae_adam* cfg, const float* tab
                    x->col_idx,
                "hvae_adam_lazy_catchup_csr: bad args");
   if (x->nb == 0) return HVAE_OK;
-  const unsigned grid = (unsigned)std::min<int64_t>(x->nb, 16384);
+  // slices per batch row: about kCatchupBlocks blocks in all (1 from that many batch rows up)
+  const int S = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(kCatchupBlocks, x->nb), 64));
+  const unsigned grid = (unsigned)(std::min<int64_t>(x->nb, 16384) * S);
   ProbeScope probe("adam_catchup", as_stream(stream));
-  k_adam_catchup_csr<<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v, last_step, *x, H);
+  k_adam_catchup_csr<<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v, last_step, *x, H,
+                                                          S);
   HVAE_LAUNCH_CHECK("k_adam_catchup_csr");
   return HVAE_OK;
 }
@@ -647,18 +810,20 @@ extern "C" int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len,
                "hvae_adam_lazy: H %% 4 and 16-B alignment required");
   HVAE_REQUIRE(n_dense == 0 || (g_dense && dense_off >= rg->n_items * H), "hvae_adam_lazy: dense overlaps W1t");
   HVAE_REQUIRE(tab_len >= 2, "hvae_adam_lazy: step table too short");
+  HVAE_REQUIRE(tab_len <= ((int64_t)1 << kStepBits), "hvae_adam_lazy: step table longer than last_step's 2^24 steps");
   const int64_t N = rg->n_items;
   HVAE_REQUIRE(rg->slot_of, "hvae_adam_lazy: rowgrad without slot_of");
   const RowMap rm = row_map(H);
-  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, rm.rpb), 4096));
-  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, kLazySweep), rm.rpb), 4096));
+  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, (int64_t)rm.rpb * kAdamUnroll), 4096));
+  const int period = lazy_sweep_period(N);
+  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, period), (int64_t)rm.rpb * kAdamUnroll), 4096));
   const int64_t b_dense = std::min<int64_t>(cdiv(cdiv(n_dense, 4), 256), 512);
   ProbeScope probe("adam_rows", as_stream(stream));
   k_adam_lazy<<<(unsigned)(b_rows + b_sweep + b_dense), 256, 0, as_stream(stream)>>>(
       to_args(cfg), (float2*)tab, p, m, v, last_step, rg->rows, rg->slot_of, rg->item_of, rg->n_unique, N, H,
-      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep, rm);
+      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep, period, rm);
   HVAE_LAUNCH_CHECK("k_adam_lazy");
   return HVAE_OK;
 }
 
-extern "C" int hvae_adam_lazy_sweep_period(void) { return hvae::kLazySweep; }
+extern "C" int hvae_adam_lazy_sweep_period(int64_t N) { return hvae::lazy_sweep_period(N); }

@@ -154,7 +154,7 @@ SIGNATURES = {
     "hvae_adam_lazy": (cint, [P(Adam), vp, i64, vp, vp, vp, vp, P(RowGrad), i64, vp, i64, i64, vp]),
     "hvae_adam_lazy_catchup": (cint, [P(Adam), vp, vp, vp, vp, vp, P(RowGrad), i64, i64, vp]),
     "hvae_adam_lazy_catchup_csr": (cint, [P(Adam), vp, vp, vp, vp, vp, P(CsrBatch), i64, vp]),
-    "hvae_adam_lazy_sweep_period": (cint, []),
+    "hvae_adam_lazy_sweep_period": (cint, [i64]),
     "hvae_counter_add": (cint, [vp, i64, vp]),
     "hvae_counters_add": (cint, [vp, i64, vp, i64, vp]),
     "hvae_score_candidates": (cint, [vp, i64, vp, vp, i64, vp, i64, i64, vp, vp]),
