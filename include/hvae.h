@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define HVAE_ABI_VERSION 2
+#define HVAE_ABI_VERSION 3
 
 enum {
   HVAE_OK = 0,
@@ -134,6 +134,9 @@ typedef struct hvae_rowgrad {
   int32_t* contrib_slot;/* [cap] slot of each (sorted) contribution             */
   float* part;          /* [part_floats] scratch of the chunked row gather      */
   int64_t part_floats;  /* >= hvae_rowgrad_part_floats(cap, H)                  */
+  double* rowsq;        /* [cap] or NULL: sum over h of rows[s, h]^2 (fp64, lane */
+                        /*       order), written by the apply with each row, so */
+                        /*       the clip reads 8 B per row instead of 4 H      */
 } hvae_rowgrad;
 /* Scratch the row gather needs for hidden width H (chunk partials, and the
  * staging copy of the long-segment sort). */

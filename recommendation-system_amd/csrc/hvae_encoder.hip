@@ -615,6 +615,19 @@ __global__ void __launch_bounds__(256) k_rg_sort(const int32_t* __restrict__ n_u
 // partials up in chunk order (the first chunk's head or tail, then the heads) into
 // the row and re-zeroes the ticket -- the same sums in the same order as a separate
 // pass would, in one launch. Loads are batched 8 contributions deep.
+// Σ over the row of x^2 in fp64 (lane order, then the wave's butterfly), lane 0 stores it: the clip's share of
+// the row, taken while the row is in registers
+template <int NV>
+__device__ __forceinline__ void row_sumsq(const float4 (&v)[NV], int lane, int64_t H, double* dst) {
+  double q = 0.0;
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+    if (4 * (int64_t)(lane + 64 * k) < H)
+      q += ((double)v[k].x * v[k].x + (double)v[k].y * v[k].y) + ((double)v[k].z * v[k].z + (double)v[k].w * v[k].w);
+  q = wave_sum_d(q);
+  if (lane == 0) *dst = q;
+}
+
 template <int NV>
 __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_unique,
                                                   const int32_t* __restrict__ seg_off,
@@ -623,7 +636,7 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
                                                   const int32_t* __restrict__ contrib_slot,
                                                   const float* __restrict__ da, int64_t H, int CH,
                                                   float* __restrict__ out_rows, float* __restrict__ part,
-                                                  int32_t* __restrict__ ticket) {
+                                                  int32_t* __restrict__ ticket, double* __restrict__ rowsq) {
   const int nu = *n_unique;
   const int total = seg_off[nu];
   const int nchunks = (total + CH - 1) / CH;
@@ -672,6 +685,7 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
               const int64_t col = 4 * (int64_t)(lane + 64 * k);
               if (col < H) *reinterpret_cast<float4*>(dst + col) = acc[k];
             }
+            if (rowsq) row_sumsq<NV>(acc, lane, H, rowsq + si);
           } else {
             const __amdgpu_buffer_rsrc_t prs = coherent_rsrc(part);
             const uint32_t dst = (uint32_t)((run_lo == 0 ? 2 * c : 2 * c + 1) * H) * 4u;
@@ -694,9 +708,11 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
               __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
               const __amdgpu_buffer_rsrc_t prs = coherent_rsrc(part);
               const uint32_t first = (uint32_t)((2 * ca + (beg % CH == 0 ? 0 : 1)) * H) * 4u;
+              float4 tot[NV];
 #pragma unroll
               for (int k = 0; k < NV; ++k) {
                 const int64_t col = 4 * (int64_t)(lane + 64 * k);
+                tot[k] = make_float4(0.f, 0.f, 0.f, 0.f);
                 if (col >= H) continue;
                 float4 sum = ld_sc1_f4(prs, first + (uint32_t)col * 4u);
                 for (int cc = ca + 1; cc <= cb; ++cc) {
@@ -704,7 +720,9 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
                   sum.x += v.x; sum.y += v.y; sum.z += v.z; sum.w += v.w;
                 }
                 *reinterpret_cast<float4*>(out_rows + (int64_t)si * H + col) = sum;
+                tot[k] = sum;
               }
+              if (rowsq) row_sumsq<NV>(tot, lane, H, rowsq + si);
               if (lane == 0) __hip_atomic_store(ticket + si, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           }
@@ -725,7 +743,7 @@ __global__ void __launch_bounds__(256) k_rg_apply_seg(const int32_t* __restrict_
                                                       const int32_t* __restrict__ contrib_row,
                                                       const float* __restrict__ contrib_val,
                                                       const float* __restrict__ da, int64_t H,
-                                                      float* __restrict__ out_rows) {
+                                                      float* __restrict__ out_rows, double* __restrict__ rowsq) {
   const int nu = *n_unique;
   const int lane = threadIdx.x & 63;
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), nw = gridDim.x * 4;
@@ -766,6 +784,7 @@ __global__ void __launch_bounds__(256) k_rg_apply_seg(const int32_t* __restrict_
       const int64_t col = 4 * (int64_t)(lane + 64 * k);
       if (col < H) *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + col) = acc[k];
     }
+    if (rowsq) row_sumsq<NV>(acc, lane, H, rowsq + s);
   }
 }
 
@@ -1009,7 +1028,7 @@ extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowg
   if (rg->cap <= kPlanSmallCap) {
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, 4), 1024));
     HVAE_NV_DISPATCH(H, (k_rg_apply_seg<NV><<<grid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
-                                                                  rg->contrib_val, da, H, rg->rows)));
+                                                                  rg->contrib_val, da, H, rg->rows, rg->rowsq)));
     HVAE_LAUNCH_CHECK("k_rg_apply_seg");
     return HVAE_OK;
   }
@@ -1017,7 +1036,7 @@ extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowg
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(rg->cap, ch), 4), 4096));
   HVAE_NV_DISPATCH(H, (k_rg_apply<NV><<<grid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
                                                             rg->contrib_val, rg->contrib_slot, da, H, ch, rg->rows,
-                                                            rg->part, rg->fill)));
+                                                            rg->part, rg->fill, rg->rowsq)));
   HVAE_LAUNCH_CHECK("k_rg_apply");
   return HVAE_OK;
 }

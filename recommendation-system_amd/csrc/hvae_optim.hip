@@ -33,6 +33,7 @@ __device__ __forceinline__ float2 adam_step_consts(double lr, double b1, double 
 struct ClipArgs {
   const float* g; int64_t n;
   const float* rows; const int32_t* n_unique; int64_t H;
+  const double* rowsq;  // per-row sums of squares from the apply (then rows is not read), or NULL
   double* part; unsigned* ticket;
   float max_norm; float* norm_out; float* coef_out;
   int64_t* step; int64_t* step_snap; int64_t* boff; int64_t advance;
@@ -65,7 +66,12 @@ __global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
     for (int64_t i = 4 * n4 + gtid; i < n; i += stride) s += (double)x[i] * (double)x[i];
   };
   if (a.n) seg(a.g, a.n);
-  if (nr) seg(a.rows, nr);
+  if (a.rowsq) {
+    const int64_t nu = a.rows ? (int64_t)(*a.n_unique) : 0;
+    for (int64_t i = gtid; i < nu; i += stride) s += a.rowsq[i];
+  } else if (nr) {
+    seg(a.rows, nr);
+  }
   s = wave_sum_d(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
@@ -669,6 +675,7 @@ static int clip_launch(const float* g_dense, int64_t n_dense, const hvae_rowgrad
   ClipArgs a{};
   a.g = g_dense; a.n = n_dense;
   a.rows = rg ? rg->rows : nullptr; a.n_unique = rg ? rg->n_unique : nullptr; a.H = H;
+  a.rowsq = rg ? rg->rowsq : nullptr;
   a.part = (double*)ws;
   if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   a.max_norm = max_norm; a.norm_out = norm_out; a.coef_out = coef_out;
@@ -710,6 +717,7 @@ extern "C" int hvae_clip_grad_norm_step_adam(const float* g_dense, int64_t n_den
   ClipArgs a{};
   a.g = g_dense; a.n = n_dense;
   a.rows = rg ? rg->rows : nullptr; a.n_unique = rg ? rg->n_unique : nullptr; a.H = H;
+  a.rowsq = rg ? rg->rowsq : nullptr;
   a.part = (double*)ws;
   if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   a.max_norm = max_norm; a.norm_out = norm_out; a.coef_out = coef_out;

@@ -15,7 +15,7 @@ import torch
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("HVAE_LIB", _HERE / "libhvae.so"))
 
-ABI_VERSION = 2  # include/hvae.h HVAE_ABI_VERSION
+ABI_VERSION = 3  # include/hvae.h HVAE_ABI_VERSION
 HVAE_OK = 0
 HVAE_F32 = 0
 HVAE_BF16 = 1
@@ -52,7 +52,7 @@ class RowGrad(C.Structure):
     _fields_ = [
         ("cnt", vp), ("slot_of", vp), ("item_of", vp), ("seg_off", vp), ("fill", vp),
         ("contrib_row", vp), ("contrib_val", vp), ("rows", vp), ("n_unique", vp),
-        ("cap", i64), ("n_items", i64), ("contrib_slot", vp), ("part", vp), ("part_floats", i64),
+        ("cap", i64), ("n_items", i64), ("contrib_slot", vp), ("part", vp), ("part_floats", i64), ("rowsq", vp),
     ]
 
 

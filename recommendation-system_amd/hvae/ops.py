@@ -135,10 +135,11 @@ class RowGradBuffers:
         self.n_unique = torch.zeros(1, **i32)
         self.contrib_slot = torch.zeros(cap, **i32)
         self.part = torch.empty(int(lib().hvae_rowgrad_part_floats(cap, H)), dtype=torch.float32, device=device)
+        self.rowsq = torch.zeros(cap, dtype=torch.float64, device=device)
         self.cap, self.n_items, self.H = cap, n_items, H
         self.struct = RowGrad(ptr(self.cnt), ptr(self.slot_of), ptr(self.item_of), ptr(self.seg_off), ptr(self.fill),
                               ptr(self.contrib_row), ptr(self.contrib_val), ptr(self.rows), ptr(self.n_unique), cap,
-                              n_items, ptr(self.contrib_slot), ptr(self.part), self.part.numel())
+                              n_items, ptr(self.contrib_slot), ptr(self.part), self.part.numel(), ptr(self.rowsq))
         self.ws = torch.empty(max(int(lib().hvae_w1_rowgrad_workspace(n_items)), 256), dtype=torch.uint8,
                               device=device)
 

@@ -42,6 +42,8 @@ for d in 384 768; do
   HVAE_LIB=build_var/libhvae_ab.so HVAE_GEMM_FAST_SHORT=1 HVAE_GEMM_FAST_TILE=64 timeout -k 10 200 python -u scripts/bench_gemm.py \
     --batch 4096 --d $d --reps 50 --no-torch > $O/gemm_fs1t64_d$d.jsonl 2>> $O/gemm.log || exit 8
 done
+HVAE_LIB=build_var/libhvae_ab.so HVAE_GEMM_TILE64_MIN=256 timeout -k 10 200 python -u scripts/bench_gemm.py --batch 4096 --d 384 \
+  --reps 50 --no-torch > $O/gemm_t64min256_d384.jsonl 2>> $O/gemm.log || exit 8
 echo "dp emul"
 timeout -k 10 400 python -u scripts/bench_dp_emul.py --world 1 8 --steps 20 --warmup 6 > $O/dp_emul.jsonl 2> $O/dp_emul.log || exit 9
 cat $O/dp_emul.jsonl
