@@ -118,6 +118,7 @@ size_t hvae_ln_gelu_drop_bwd_workspace(int64_t nb, int64_t H);
  * src/ml/train.py:90). Only the items present in the batch get a row; rows
  * are summed in ascending batch-row order, so the result is bitwise
  * reproducible. Slots are assigned in ascending item order. */
+#define HVAE_ROWSQ_PARTS 16
 typedef struct hvae_rowgrad {
   int32_t* cnt;         /* [N]   scratch; must be zero on entry, left zero      */
   int32_t* slot_of;     /* [N]   item -> slot, valid iff slot < *n_unique and   */
@@ -134,9 +135,10 @@ typedef struct hvae_rowgrad {
   int32_t* contrib_slot;/* [cap] slot of each (sorted) contribution             */
   float* part;          /* [part_floats] scratch of the chunked row gather      */
   int64_t part_floats;  /* >= hvae_rowgrad_part_floats(cap, H)                  */
-  double* rowsq;        /* [cap] or NULL: sum over h of rows[s, h]^2 (fp64, lane */
-                        /*       order), written by the apply with each row, so */
-                        /*       the clip reads 8 B per row instead of 4 H      */
+  double* rowsq;        /* [cap, HVAE_ROWSQ_PARTS] or NULL: partial sums over h */
+                        /*       of rows[s, h]^2 (fp64), written by the apply   */
+                        /*       with each row, so the clip reads 128 B per row */
+                        /*       instead of 4 H                                 */
 } hvae_rowgrad;
 /* Scratch the row gather needs for hidden width H (chunk partials, and the
  * staging copy of the long-segment sort). */

@@ -58,6 +58,7 @@ static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream
 // kTicketSlice tickets in rotation, so launches that may run concurrently on
 // different streams (the nodes of one captured graph) never share one.
 constexpr int kTicketPool = 1 << 16, kTicketSlice = 256;
+constexpr int kRowSqParts = HVAE_ROWSQ_PARTS;  // fp64 partial sums of squares per W1 gradient row (hvae_rowgrad.rowsq)
 unsigned* ticket_slice();  // nullptr (error set) on failure
 
 // A/B knobs (HVAE_DEC_*, HVAE_TOPK_*, HVAE_TK_*, HVAE_GEMM_* in the environment) are read only by variant builds

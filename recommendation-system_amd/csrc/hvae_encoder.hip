@@ -10,6 +10,7 @@
 //
 // Reference: src/ml/model.py:103-127 (_build_encoder), 138-155 (encode).
 #include <algorithm>
+#include <cstdlib>
 
 #include <type_traits>
 
@@ -615,8 +616,17 @@ __global__ void __launch_bounds__(256) k_rg_sort(const int32_t* __restrict__ n_u
 // partials up in chunk order (the first chunk's head or tail, then the heads) into
 // the row and re-zeroes the ticket -- the same sums in the same order as a separate
 // pass would, in one launch. Loads are batched 8 contributions deep.
-// Σ over the row of x^2 in fp64 (lane order, then the wave's butterfly), lane 0 stores it: the clip's share of
-// the row, taken while the row is in registers
+// The clip's share of a W1 gradient row, taken while the row is in registers: each lane's sum of its x^2 in fp64,
+// then the four lanes of a quad added by two DPP exchanges (no LDS round trips: a whole-wave shuffle reduction per
+// row cost the apply 11-13 us at B = 4096), and lane 4 g stores quad g's sum: 16 fp64 partials per row
+// (kRowSqParts), which the clip adds up in a fixed order.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
 template <int NV>
 __device__ __forceinline__ void row_sumsq(const float4 (&v)[NV], int lane, int64_t H, double* dst) {
   double q = 0.0;
@@ -624,8 +634,9 @@ __device__ __forceinline__ void row_sumsq(const float4 (&v)[NV], int lane, int64
   for (int k = 0; k < NV; ++k)
     if (4 * (int64_t)(lane + 64 * k) < H)
       q += ((double)v[k].x * v[k].x + (double)v[k].y * v[k].y) + ((double)v[k].z * v[k].z + (double)v[k].w * v[k].w);
-  q = wave_sum_d(q);
-  if (lane == 0) *dst = q;
+  q += dpp_d<0xB1>(q);  // quad_perm [1, 0, 3, 2]
+  q += dpp_d<0x4E>(q);  // quad_perm [2, 3, 0, 1]
+  if ((lane & 3) == 0) dst[lane >> 2] = q;
 }
 
 template <int NV>
@@ -685,7 +696,7 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
               const int64_t col = 4 * (int64_t)(lane + 64 * k);
               if (col < H) *reinterpret_cast<float4*>(dst + col) = acc[k];
             }
-            if (rowsq) row_sumsq<NV>(acc, lane, H, rowsq + si);
+            if (rowsq) row_sumsq<NV>(acc, lane, H, rowsq + (int64_t)si * kRowSqParts);
           } else {
             const __amdgpu_buffer_rsrc_t prs = coherent_rsrc(part);
             const uint32_t dst = (uint32_t)((run_lo == 0 ? 2 * c : 2 * c + 1) * H) * 4u;
@@ -722,7 +733,7 @@ __global__ void __launch_bounds__(256) k_rg_apply(const int32_t* __restrict__ n_
                 *reinterpret_cast<float4*>(out_rows + (int64_t)si * H + col) = sum;
                 tot[k] = sum;
               }
-              if (rowsq) row_sumsq<NV>(tot, lane, H, rowsq + si);
+              if (rowsq) row_sumsq<NV>(tot, lane, H, rowsq + (int64_t)si * kRowSqParts);
               if (lane == 0) __hip_atomic_store(ticket + si, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           }
@@ -784,7 +795,7 @@ __global__ void __launch_bounds__(256) k_rg_apply_seg(const int32_t* __restrict_
       const int64_t col = 4 * (int64_t)(lane + 64 * k);
       if (col < H) *reinterpret_cast<float4*>(out_rows + (int64_t)s * H + col) = acc[k];
     }
-    if (rowsq) row_sumsq<NV>(acc, lane, H, rowsq + s);
+    if (rowsq) row_sumsq<NV>(acc, lane, H, rowsq + (int64_t)s * kRowSqParts);
   }
 }
 
@@ -1025,10 +1036,12 @@ extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowg
                "hvae_w1_rowgrad_apply: part scratch too small for H");
   hipStream_t st = as_stream(stream);
   ProbeScope probe("rowgrad_apply", st);
+  double* rowsq = rg->rowsq;
+  if (const char* e = ab_getenv("HVAE_ROWSQ")) if (std::atoi(e) == 0) rowsq = nullptr;  // A/B: the clip reads rows
   if (rg->cap <= kPlanSmallCap) {
     const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, 4), 1024));
     HVAE_NV_DISPATCH(H, (k_rg_apply_seg<NV><<<grid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
-                                                                  rg->contrib_val, da, H, rg->rows, rg->rowsq)));
+                                                                  rg->contrib_val, da, H, rg->rows, rowsq)));
     HVAE_LAUNCH_CHECK("k_rg_apply_seg");
     return HVAE_OK;
   }
@@ -1036,7 +1049,7 @@ extern "C" int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowg
   const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(rg->cap, ch), 4), 4096));
   HVAE_NV_DISPATCH(H, (k_rg_apply<NV><<<grid, 256, 0, st>>>(rg->n_unique, rg->seg_off, rg->contrib_row,
                                                             rg->contrib_val, rg->contrib_slot, da, H, ch, rg->rows,
-                                                            rg->part, rg->fill, rg->rowsq)));
+                                                            rg->part, rg->fill, rowsq)));
   HVAE_LAUNCH_CHECK("k_rg_apply");
   return HVAE_OK;
 }

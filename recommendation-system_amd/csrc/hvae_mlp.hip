@@ -47,12 +47,6 @@ struct MlpP {
   float ks; const float* ks_dev;
   float* dp1; float* dheads; float* dh;
   int rot;  // rotate each block's walk over the weights (A/B: HVAE_MLP_ROT=0 walks them in one order)
-  // Q blocks per row group, each computing a 1/Q slice of every layer's outputs (mlp_group_blocks); the
-  // slices meet through the layers' own output buffers (grp_ctr: one arrival counter per group; dh_ctr: the
-  // backward's last-arrival ticket per group before the LayerNorm)
-  int Q;
-  int64_t ngroups;
-  unsigned* grp_ctr; unsigned* dh_ctr;
   // the row-gradient plan of the batch, run by block gridDim.x - 1 when plan_slot_of != NULL
   const int64_t* pl_row_ptr; const int32_t* pl_col_idx; const float* pl_vals; const int32_t* pl_rows;
   const int64_t* pl_rows_offset; int64_t pl_nb;
@@ -81,15 +75,15 @@ __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
 // from L2: 1.3 MB at d = 384), so every lane keeps kMlpLoads 16-B loads outstanding.
 constexpr int kMlpLoads = 16;
 
-// ys[r][n] = sum_k xs[r][k] W[n][k] for n in [n_lo, n_lo + n_cnt) (n_cnt % 8 == 0, K % 32 == 0); ys rows are N wide.
+// ys[r][n] = sum_k xs[r][k] W[n][k] for n < N (N % 8 == 0, K % 32 == 0).
 // G output groups of 8 per wave at once, so that kMlpLoads loads are in flight per lane; chunks past K re-read
 // the last one and add it with a zero activation (every load unconditional)
 template <int R, int G, int LOADS>
 __device__ __forceinline__ void rows_nt_g(const float* __restrict__ W, int N, int K, const float* xs, float* ys,
-                                          int rotate, int n_lo, int n_cnt) {
+                                          int rotate) {
   constexpr int KCH = LOADS / G;  // 32-k chunks per pass
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, j = lane >> 3, c = lane & 7;
-  const int NG = n_cnt / 8;
+  const int NG = N / 8;
   // blocks start at different output groups, so that the blocks of an XCD stream different lines at a time
   // (all of them walking the matrix in the same order camp on the same L2 channels)
   const int rot = rotate ? (int)((blockIdx.x * 8u) % (unsigned)NG) : 0;
@@ -101,7 +95,7 @@ __device__ __forceinline__ void rows_nt_g(const float* __restrict__ W, int N, in
       for (int r = 0; r < R; ++r) acc[gi][r] = 0.f;
     const float* wrow[G];
 #pragma unroll
-    for (int gi = 0; gi < G; ++gi) wrow[gi] = W + (int64_t)(n_lo + 8 * ((min(g0 + gi, NG - 1) + rot) % NG) + j) * K + 4 * c;
+    for (int gi = 0; gi < G; ++gi) wrow[gi] = W + (int64_t)(8 * ((min(g0 + gi, NG - 1) + rot) % NG) + j) * K + 4 * c;
     auto pass = [&](int k0, auto full) {
       constexpr bool FULL = decltype(full)::value;
       float4 wv[G][KCH];
@@ -138,29 +132,27 @@ __device__ __forceinline__ void rows_nt_g(const float* __restrict__ W, int N, in
       float v = acc[gi][0];
 #pragma unroll
       for (int r = 1; r < R; ++r) v = (c == r) ? acc[gi][r] : v;
-      if (c < R && g0 + gi < NG) ys[c * N + n_lo + 8 * ((g0 + gi + rot) % NG) + j] = v;
+      if (c < R && g0 + gi < NG) ys[c * N + 8 * ((g0 + gi + rot) % NG) + j] = v;
     }
   }
 }
 
 template <int R>
 __device__ __forceinline__ void rows_nt(const float* __restrict__ W, int N, int K, const float* xs, float* ys,
-                                        int rotate, int n_lo, int n_cnt) {
+                                        int rotate) {
   constexpr int LOADS = R == 1 ? kMlpLoads : kMlpLoads / 2;  // more rows: more arithmetic per byte, fewer registers
-  if (K >= 32 * LOADS * 3 / 4) rows_nt_g<R, 1, LOADS>(W, N, K, xs, ys, rotate, n_lo, n_cnt);
-  else if (K >= 32 * LOADS * 3 / 8) rows_nt_g<R, 2, LOADS>(W, N, K, xs, ys, rotate, n_lo, n_cnt);
-  else rows_nt_g<R, 4, LOADS>(W, N, K, xs, ys, rotate, n_lo, n_cnt);
+  if (K >= 32 * LOADS * 3 / 4) rows_nt_g<R, 1, LOADS>(W, N, K, xs, ys, rotate);
+  else if (K >= 32 * LOADS * 3 / 8) rows_nt_g<R, 2, LOADS>(W, N, K, xs, ys, rotate);
+  else rows_nt_g<R, 4, LOADS>(W, N, K, xs, ys, rotate);
 }
 
-// out[r][n] = sum_k xs[r][k] W[k][n] for n in [n_lo, n_lo + n_cnt) (n_cnt % 4 == 0, n_cnt / 4 <= threads): thread t
-// takes outputs 4 (t % NQ).. over k-slice t / NQ of S = min(threads / NQ, kMlpNnSlices) slices; part: LDS of
-// S * R * n_cnt <= 4 * threads * R floats. epi(r, n, v) for every (r < R, n in the slice).
+// out[r][n] = sum_k xs[r][k] W[k][n] for n < N (N % 4 == 0, N / 4 <= threads); part: LDS of
+// (threads / (N / 4)) * R * N <= 4 * threads * R floats. epi(r, n, v) for every (r < R, n).
 // Rows past the slice re-read its last row and add it with a zero activation (every load unconditional)
-constexpr int kMlpNnSlices = 32;  // partials an output sums in the epilogue (one LDS read each, in slice order)
 template <int R, class Epi>
 __device__ __forceinline__ void rows_nn(const float* __restrict__ W, int N, int K, const float* xs, float* part,
-                                        int rotate, int n_lo, int n_cnt, Epi epi) {
-  const int t = threadIdx.x, NQ = n_cnt / 4, S = min(kMlpThreads / NQ, kMlpNnSlices);
+                                        int rotate, Epi epi) {
+  const int t = threadIdx.x, NQ = N / 4, S = kMlpThreads / NQ;
   const int qd = t % NQ, s = t / NQ;
   if (s < S) {
     // blocks take the k slices in rotated order (L2 channels, as in rows_nt_g); partials keep slice order
@@ -169,7 +161,7 @@ __device__ __forceinline__ void rows_nn(const float* __restrict__ W, int N, int 
     float4 acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* wp = W + n_lo + 4 * qd;
+    const float* wp = W + 4 * qd;
     constexpr int LOADS = kMlpLoads / R;  // more rows: more arithmetic per byte, fewer registers
     for (int k = k_lo; k < k_hi; k += LOADS) {
       float4 wv[LOADS];
@@ -192,60 +184,16 @@ __device__ __forceinline__ void rows_nn(const float* __restrict__ W, int N, int 
       }
     }
 #pragma unroll
-    for (int r = 0; r < R; ++r) *reinterpret_cast<float4*>(part + (sk * R + r) * n_cnt + 4 * qd) = acc[r];
+    for (int r = 0; r < R; ++r) *reinterpret_cast<float4*>(part + (sk * R + r) * N + 4 * qd) = acc[r];
   }
   __syncthreads();
-  for (int i = t; i < R * n_cnt; i += kMlpThreads) {
-    const int r = i / n_cnt, n = i % n_cnt;
+  for (int i = t; i < R * N; i += kMlpThreads) {
+    const int r = i / N, n = i % N;
     float v = 0.f;
-    for (int s2 = 0; s2 < S; ++s2) v += part[(s2 * R + r) * n_cnt + n];
-    epi(r, n_lo + n, v);
+    for (int s2 = 0; s2 < S; ++s2) v += part[(s2 * R + r) * N + n];
+    epi(r, n, v);
   }
   __syncthreads();
-}
-
-// ---- the slices of a row group (Q > 1) meet through global memory. A block publishes its slice of a layer's
-// output rows with 16-B sc1 stores (mlp_publish), and every block waits for its stores (vmcnt 0) before it
-// arrives at the group's counter; a reader takes the rows back with 16-B sc1 loads after an agent acquire
-// (mlp_gather) -- the hand-off form of k_rg_apply's chunk partials (MI355X_MICROARCH's measured valid form).
-// The counter of a group only grows within a launch: the k-th all-wait exchange waits for k Q arrivals, and a
-// block that has passed the last one arrives once more (mlp_group_leave); the arrival that completes
-// (exchanges + 1) Q resets it to 0 for the next launch -- no block can still be waiting then.
-__device__ __forceinline__ void mlp_publish(float* dst, int64_t ld, int64_t b0, int64_t nb, const float* lds,
-                                            int lds_ld, int R, int c_lo, int c_cnt) {
-  const __amdgpu_buffer_rsrc_t rs = coherent_rsrc(dst + b0 * ld);
-  const int q4 = c_cnt / 4;
-  for (int i = threadIdx.x; i < R * q4; i += kMlpThreads) {
-    const int r = i / q4, c = c_lo + 4 * (i % q4);
-    if (b0 + r < nb) st_sc1_f4(rs, (uint32_t)((r * ld + c) * 4), *reinterpret_cast<const float4*>(lds + r * lds_ld + c));
-  }
-}
-__device__ __forceinline__ void mlp_gather(const float* src, int64_t ld, int64_t b0, int64_t nb, float* lds, int lds_ld,
-                                           int R, int cols) {
-  const __amdgpu_buffer_rsrc_t rs = coherent_rsrc(src + b0 * ld);
-  const int q4 = cols / 4;
-  for (int i = threadIdx.x; i < R * q4; i += kMlpThreads) {
-    const int r = i / q4, c = 4 * (i % q4);
-    *reinterpret_cast<float4*>(lds + r * lds_ld + c) =
-        b0 + r < nb ? ld_sc1_f4(rs, (uint32_t)((r * ld + c) * 4)) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  __syncthreads();
-}
-__device__ __forceinline__ void mlp_group_exchange(unsigned* ctr, unsigned target) {
-  __builtin_amdgcn_s_waitcnt(0);  // this thread's slice stores have reached the coherence point
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
-  }
-  __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-}
-__device__ __forceinline__ void mlp_group_leave(unsigned* ctr, unsigned total) {
-  if (threadIdx.x == 0) {
-    const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == total - 1) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
 }
 
 template <int R>
@@ -269,12 +217,7 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
     return;
   }
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  // row group grp (rows b0 .. b0 + R - 1), output slice qs_ of Q; block 0 of a group writes the row-wide outputs
-  const int Q = p.Q, qs_ = (int)(blockIdx.x % (unsigned)Q);
-  const int64_t grp = blockIdx.x / Q;
-  const int64_t b0 = grp * R;
-  const bool lead = qs_ == 0;
-  unsigned* ctr = Q > 1 ? p.grp_ctr + grp : nullptr;
+  const int64_t b0 = (int64_t)blockIdx.x * R;
   const int64_t step = load_step(p.step_dev);
   if (p.enc_w1t) {  // the first encoder layer: wave w gathers, normalises and activates row w
     if (w < R) {
@@ -283,9 +226,8 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
         auto enc = [&](auto nv) {
           encoder_sparse_row<decltype(nv)::value, false>(p.e_row_ptr, p.e_col_idx, p.e_vals, p.e_rows, p.e_rows_offset, b,
                                                   p.enc_w1t, p.enc_b1, p.ln_w, p.ln_b, H, p.p_drop, p.scale,
-                                                  p.enc_drop_mult, p.seed, step, p.train, lead ? p.h_out : nullptr,
-                                                  lead ? p.xhat_out : nullptr, lead ? p.rstd_out : nullptr,
-                                                  xs + w * H);
+                                                  p.enc_drop_mult, p.seed, step, p.train, p.h_out, p.xhat_out,
+                                                  p.rstd_out, xs + w * H);
         };
         if (H <= 256) enc(std::integral_constant<int, 1>{});
         else enc(std::integral_constant<int, 2>{});  // H <= 512 (host check)
@@ -301,21 +243,15 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
     }
   }
   __syncthreads();
-  const int h_cnt = L2 / Q, h_lo = qs_ * h_cnt;
-  rows_nt<R>(p.Wh, L2, H, xs, hs, p.rot, h_lo, h_cnt);
+  rows_nt<R>(p.Wh, L2, H, xs, hs, p.rot);
   __syncthreads();
-  for (int i = t; i < R * h_cnt; i += kMlpThreads) {
-    const int r = i / h_cnt, n = h_lo + i % h_cnt;
-    const float v = hs[r * L2 + n] + p.bh[n];
-    hs[r * L2 + n] = v;
-    if (Q == 1 && b0 + r < p.nb) p.heads[(b0 + r) * L2 + n] = v;
+  for (int i = t; i < R * L2; i += kMlpThreads) {
+    const int r = i / L2, n = i % L2;
+    const float v = hs[i] + p.bh[n];
+    hs[i] = v;
+    if (b0 + r < p.nb) p.heads[(b0 + r) * L2 + n] = v;
   }
   __syncthreads();
-  if (Q > 1) {  // the heads rows of the group, through p.heads
-    mlp_publish(p.heads, L2, b0, p.nb, hs, L2, R, h_lo, h_cnt);
-    mlp_group_exchange(ctr, (unsigned)Q);
-    mlp_gather(p.heads, L2, b0, p.nb, hs, L2, R, L2);
-  }
   // reparameterisation + KL of row w (k_reparam_kl_fwd's arithmetic and lane order)
   if (w < R) {
     const int64_t b = b0 + w;
@@ -328,45 +264,38 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
       float zv = m;
       if (p.train) {
         const float e = !valid ? 0.f : p.eps_in ? p.eps_in[b * L + l] : normal_f(p.seed, step, kTagEps, (uint64_t)(b * L + l));
-        if (valid && lead && p.eps) p.eps[b * L + l] = e;
+        if (valid && p.eps) p.eps[b * L + l] = e;
         zv = m + e * expf(0.5f * v);
       }
       zs[w * L + l] = zv;
-      if (valid && lead) p.z[b * L + l] = zv;
+      if (valid) p.z[b * L + l] = zv;
     }
     kl = wave_sum(kl);
-    if (lane == 0 && valid && lead) p.kl_rows[b] = -0.5f * kl;
+    if (lane == 0 && valid) p.kl_rows[b] = -0.5f * kl;
   }
   __syncthreads();
-  const int d_cnt = D / Q, d_lo = qs_ * d_cnt;
-  rows_nt<R>(p.Wa, D, L, zs, ys, p.rot, d_lo, d_cnt);
+  rows_nt<R>(p.Wa, D, L, zs, ys, p.rot);
   __syncthreads();
-  for (int i = t; i < R * d_cnt; i += kMlpThreads) {
-    const int r = i / d_cnt, n = d_lo + i % d_cnt;
+  for (int i = t; i < R * D; i += kMlpThreads) {
+    const int r = i / D, n = i % D;
     const int64_t b = b0 + r;
-    const float pre = ys[r * D + n] + p.ba[n];
+    const float pre = ys[i] + p.ba[n];
     const float g = gelu_f(pre);
     float qv = g;
     if (p.train && b < p.nb)
       qv = g * dropout_mult(p.p_drop, p.scale, p.drop_mult, (uint64_t)(b * D + n), p.seed, step, kTagProjDrop);
-    qs[r * D + n] = qv;
+    qs[i] = qv;
     if (b < p.nb) {
       p.p1[b * D + n] = pre;
-      if (Q == 1) p.q[b * D + n] = qv;
+      p.q[b * D + n] = qv;
     }
   }
   __syncthreads();
-  if (Q > 1) {  // the q rows of the group, through p.q
-    mlp_publish(p.q, D, b0, p.nb, qs, D, R, d_lo, d_cnt);
-    mlp_group_exchange(ctr, 2u * Q);
-    mlp_gather(p.q, D, b0, p.nb, qs, D, R, D);
-    mlp_group_leave(ctr, 3u * Q);
-  }
-  rows_nt<R>(p.Wb, D, D, qs, ys, p.rot, d_lo, d_cnt);
+  rows_nt<R>(p.Wb, D, D, qs, ys, p.rot);
   __syncthreads();
-  for (int i = t; i < R * d_cnt; i += kMlpThreads) {
-    const int r = i / d_cnt, n = d_lo + i % d_cnt;
-    if (b0 + r < p.nb) p.u[(b0 + r) * D + n] = ys[r * D + n] + p.bb[n];
+  for (int i = t; i < R * D; i += kMlpThreads) {
+    const int r = i / D, n = i % D;
+    if (b0 + r < p.nb) p.u[(b0 + r) * D + n] = ys[i] + p.bb[n];
   }
 }
 
@@ -381,13 +310,9 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
   float* dxs = dhs + R * H;    // [R][H]  dxhat (LayerNorm backward)
   float* part = dxs + R * H;   // slice partials of rows_nn; then the LayerNorm column terms [3][R][H]
   const int t = threadIdx.x;
-  const int Q = p.Q, qs_ = (int)(blockIdx.x % (unsigned)Q);
-  const int64_t grp = blockIdx.x / Q;
-  const int64_t b0 = grp * R;
-  unsigned* ctr = Q > 1 ? p.grp_ctr + grp : nullptr;
+  const int64_t b0 = (int64_t)blockIdx.x * R;
   const int64_t step = load_step(p.step_dev);
   const float ks = p.ks_dev ? *p.ks_dev : p.ks;
-  const int d_cnt = D / Q, d_lo = qs_ * d_cnt, l_cnt = L / Q, l_lo = qs_ * l_cnt, h_cnt = H / Q, h_lo = qs_ * h_cnt;
   for (int i = t; i < R * D / 4; i += kMlpThreads) {
     const int r = i / (D / 4), k4 = i % (D / 4);
     reinterpret_cast<float4*>(gs)[i] = (b0 + r < p.nb)
@@ -395,7 +320,7 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
   }
   __syncthreads();
   // dp1 = (dU W_b) * dropmult * GELU'(p1)   (HVAE_EPI_GELU_DROP_BWD)
-  rows_nn<R>(p.Wb, D, D, gs, part, p.rot, d_lo, d_cnt, [&](int r, int n, float v) {
+  rows_nn<R>(p.Wb, D, D, gs, part, p.rot, [&](int r, int n, float v) {
     const int64_t b = b0 + r;
     float g = 0.f;
     if (b < p.nb) {
@@ -403,17 +328,12 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
                                               kTagProjDrop)
                                : 1.f;
       g = v * dm * gelu_grad_f(p.p1[b * D + n]);
-      if (Q == 1) p.dp1[b * D + n] = g;
+      p.dp1[b * D + n] = g;
     }
     ps[r * D + n] = g;
   });
-  if (Q > 1) {  // the dp1 rows of the group, through p.dp1
-    mlp_publish(p.dp1, D, b0, p.nb, ps, D, R, d_lo, d_cnt);
-    mlp_group_exchange(ctr, (unsigned)Q);
-    mlp_gather(p.dp1, D, b0, p.nb, ps, D, R, D);
-  }
   // dz = dp1 W_a -> dheads (HVAE_EPI_REPARAM_BWD)
-  rows_nn<R>(p.Wa, L, D, ps, part, p.rot, l_lo, l_cnt, [&](int r, int l, float v) {
+  rows_nn<R>(p.Wa, L, D, ps, part, p.rot, [&](int r, int l, float v) {
     const int64_t b = b0 + r;
     float dmu = 0.f, dlv = 0.f;
     if (b < p.nb) {
@@ -421,35 +341,17 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
       const float gz = p.train ? v * p.eps[b * L + l] * 0.5f * expf(0.5f * lv) : 0.f;
       dlv = gz + ks * 0.5f * (expf(lv) - 1.f);
       dmu = v + ks * m;
-      if (Q == 1) {
-        p.dheads[b * L2 + l] = dmu;
-        p.dheads[b * L2 + L + l] = dlv;
-      }
+      p.dheads[b * L2 + l] = dmu;
+      p.dheads[b * L2 + L + l] = dlv;
     }
     ds[r * L2 + l] = dmu;
     ds[r * L2 + L + l] = dlv;
   });
-  if (Q > 1) {  // the dheads rows of the group (both halves of the slice), through p.dheads
-    mlp_publish(p.dheads, L2, b0, p.nb, ds, L2, R, l_lo, l_cnt);
-    mlp_publish(p.dheads, L2, b0, p.nb, ds, L2, R, L + l_lo, l_cnt);
-    mlp_group_exchange(ctr, 2u * Q);
-    mlp_gather(p.dheads, L2, b0, p.nb, ds, L2, R, L2);
-    mlp_group_leave(ctr, 3u * Q);
-  }
   // dh = dheads W_heads
-  rows_nn<R>(p.Wh, H, L2, ds, part, p.rot, h_lo, h_cnt, [&](int r, int n, float v) {
-    if (b0 + r < p.nb) {
-      if (Q == 1) p.dh[(b0 + r) * H + n] = v;
-    }
+  rows_nn<R>(p.Wh, H, L2, ds, part, p.rot, [&](int r, int n, float v) {
+    if (b0 + r < p.nb) p.dh[(b0 + r) * H + n] = v;
     dhs[r * H + n] = v;
   });
-  if (Q > 1) {  // dh slices out; the group's last block to arrive takes the rows back and runs the LayerNorm
-    mlp_publish(p.dh, H, b0, p.nb, dhs, H, R, h_lo, h_cnt);
-    if (!p.ln_w) return;
-    if (!last_block_arrives(p.dh_ctr + grp, (unsigned)Q)) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    mlp_gather(p.dh, H, b0, p.nb, dhs, H, R, H);
-  }
   if (!p.ln_w) return;
   // ---- the last hidden layer's Dropout(GELU(LayerNorm(a))) backward (k_ln_gelu_drop_bwd's per-row arithmetic
   // and lane order, so da is the same): wave w takes row w; its column terms go to LDS, the block sums its rows
@@ -506,10 +408,10 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
     float v = src[0];
 #pragma unroll
     for (int r = 1; r < R; ++r) v += src[r * H];
-    st_shared_f(&gpart[grp * 3 * H + i], v);
+    st_shared_f(&gpart[(int64_t)blockIdx.x * 3 * H + i], v);
   }
-  if (!last_block_arrives(p.ln_ticket, (unsigned)p.ngroups)) return;
-  const int np = (int)p.ngroups;
+  if (!last_block_arrives(p.ln_ticket, gridDim.x)) return;
+  const int np = gridDim.x;
   for (int i = t; i < 3 * H; i += kMlpThreads) {
     float sum = 0.f;
     int q = 0;
@@ -536,18 +438,6 @@ static int mlp_rows_per_block(int64_t nb) {
     if (r == 1 || r == 2 || r == 4) return r;
   }
   return nb <= 32 ? 1 : nb <= 512 ? 2 : 4;
-}
-
-// blocks per row group: at small batches the R-row groups alone leave most CUs idle while each streams all three
-// weight matrices (1.3 MB at d = 384), so Q blocks split every layer's outputs and exchange the slices; Q is 4 up
-// to 64 groups, 2 up to 128 (at most ~256 blocks, one per CU, all resident together), else 1.
-// HVAE_MLP_Q (A/B build): force 1, 2 or 4
-static int mlp_group_blocks(int64_t ngroups) {
-  if (const char* e = ab_getenv("HVAE_MLP_Q")) {
-    const int q = std::atoi(e);
-    if (q == 1 || q == 2 || q == 4) return q;
-  }
-  return ngroups <= 64 ? 4 : ngroups <= 128 ? 2 : 1;
 }
 
 static size_t mlp_fwd_smem(int R, const hvae_mlp_rows* a) { return (size_t)R * (a->H + 3 * a->L + 2 * a->D) * 4; }
@@ -617,10 +507,7 @@ extern "C" int hvae_mlp_fwd_rows(const hvae_mlp_rows* a, void* stream) {
   const int R = mlp_rows_per_block(a->nb);
   size_t smem = mlp_fwd_smem(R, a);
   HVAE_REQUIRE(smem <= kMlpLdsMax, "hvae_mlp_fwd_rows: activations exceed the LDS");
-  p.ngroups = cdiv(a->nb, R);
-  p.Q = mlp_group_blocks(p.ngroups);
-  if (p.Q > 1 && !(p.grp_ctr = ticket_slice())) return HVAE_ERR_HIP;
-  unsigned nblk = (unsigned)(p.ngroups * p.Q);
+  unsigned nblk = (unsigned)cdiv(a->nb, R);
   HVAE_REQUIRE(!a->plan_x == !a->plan_rg, "hvae_mlp_fwd_rows: plan_x and plan_rg go together");
   if (a->plan_x) {
     const hvae_csr_batch* x = a->plan_x;
@@ -692,11 +579,7 @@ extern "C" int hvae_mlp_bwd_rows(const hvae_mlp_rows* a, void* stream) {
   const int R = mlp_rows_per_block(a->nb);
   const size_t smem = mlp_bwd_smem(R, a);
   HVAE_REQUIRE(smem <= kMlpLdsMax, "hvae_mlp_bwd_rows: activations exceed the LDS");
-  p.ngroups = cdiv(a->nb, R);
-  p.Q = mlp_group_blocks(p.ngroups);
-  if (p.Q > 1 && !(p.grp_ctr = ticket_slice())) return HVAE_ERR_HIP;
-  if (p.Q > 1 && a->ln_w && !(p.dh_ctr = ticket_slice())) return HVAE_ERR_HIP;
-  const dim3 grid((unsigned)(p.ngroups * p.Q));
+  const dim3 grid((unsigned)cdiv(a->nb, R));
   hipStream_t st = as_stream(stream);
   ProbeScope probe("mlp_bwd", st);
   if (R == 1) HVAE_MLP_LAUNCH(k_mlp_bwd_rows<1>);

@@ -6,6 +6,7 @@
 // src/ml/train.py:63. Both passes are HBM-bound; the clip multiplier never
 // takes its own pass over the gradients -- it is read by the Adam launches.
 #include <algorithm>
+#include <cstdlib>
 
 #include "hvae_common.h"
 
@@ -67,8 +68,8 @@ __global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
   };
   if (a.n) seg(a.g, a.n);
   if (a.rowsq) {
-    const int64_t nu = a.rows ? (int64_t)(*a.n_unique) : 0;
-    for (int64_t i = gtid; i < nu; i += stride) s += a.rowsq[i];
+    const int64_t np = a.rows ? (int64_t)(*a.n_unique) * kRowSqParts : 0;
+    for (int64_t i = gtid; i < np; i += stride) s += a.rowsq[i];
   } else if (nr) {
     seg(a.rows, nr);
   }
@@ -304,9 +305,8 @@ static inline RowMap row_map(int64_t H) {
 }
 
 // float4 column i of a row: replay steps (from, to] with g = 0 (constants from the step table,
-// loaded 8 at a time), then, if `step`, one more step with constants kx and gradient gx. Split into load / math /
-// store so that the row loops below keep kAdamUnroll rows' loads in flight together (one row group per barrier
-// was one memory round trip per iteration: the row kernels ran at ~4.3 TB/s).
+// loaded kTabAhead at a time), then, if `step`, one more step with constants kx and gradient gx. Split into load /
+// math / store so that the row loops below can keep U row groups' loads in flight together.
 struct ColState {
   float4 p, m, v;
 };
@@ -370,10 +370,31 @@ __device__ __forceinline__ void col_update(const AdamArgs& a, const float2* __re
   col_store(p, m, v, i, c);
 }
 constexpr int kCatchupBlocks = 1024;  // k_adam_catchup_csr: blocks to aim for over a small batch
-constexpr int kAdamUnroll = 4;  // row groups (rows x float4 columns) per barrier in the row kernels
+// Row groups (rows x float4 columns) per barrier in the row kernels. Four groups' loads in flight per barrier
+// (HVAE_ADAM_UNROLL=4, A/B build) ran slower than one everywhere -- Syn-10M 11.55-11.62 vs 11.52 ms per step,
+// Syn-1M 1.208 vs 1.194, All_Beauty 0.143 vs 0.134 (adam_rows 20 vs 13 us; profiles/r04_adam_unroll_ab.jsonl):
+// the unrolled kernels hold 164 VGPRs (3 waves per SIMD) and a quarter of the blocks.
+constexpr int kAdamUnroll = 1;
+// A/B (HVAE_AB builds): HVAE_ADAM_UNROLL=4 keeps four row groups in flight, HVAE_CATCHUP_PONLY=0 stores m, v in
+// the CSR catch-up too
+static int adam_unroll() {
+  const char* e = ab_getenv("HVAE_ADAM_UNROLL");
+  return e && std::atoi(e) == 4 ? 4 : kAdamUnroll;
+}
+static int catchup_p_only() {
+  const char* e = ab_getenv("HVAE_CATCHUP_PONLY");
+  return e && std::atoi(e) == 0 ? 0 : 1;
+}
+#ifdef HVAE_AB
+#define HVAE_ADAM_U_CALL(U_, CALL) \
+  do { if ((U_) == 4) { constexpr int U = 4; CALL; } else { constexpr int U = kAdamUnroll; CALL; } } while (0)
+#else
+#define HVAE_ADAM_U_CALL(U_, CALL) do { constexpr int U = kAdamUnroll; CALL; } while (0)
+#endif
 
 // Bring rows up to the completed step count *step: the batch's rows (item_of /
 // n_unique) or, with item_of == NULL, all N rows.
+template <int U>
 __global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* __restrict__ tab, float* p, float* m,
                                                       float* v, int32_t* __restrict__ last_step,
                                                       const int32_t* __restrict__ item_of,
@@ -384,7 +405,6 @@ __global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* 
   const int64_t H4 = H / 4;
   const int rr = threadIdx.x / rm.h4s, c0 = threadIdx.x % rm.h4s;
   const AdamK none{};
-  constexpr int U = kAdamUnroll;
   const int64_t span = (int64_t)rm.rpb * U;
   for (int64_t g0 = (int64_t)blockIdx.x * span; g0 < nrows; g0 += (int64_t)gridDim.x * span) {
     int64_t j[U];
@@ -426,16 +446,17 @@ __global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* 
 // s, s + S, s + 2 S, .. (S slices per row, so that a small batch still spreads its rows' replays over the
 // machine: at B = 64 one block per row left 64 blocks walking ~20 rows each, one memory round trip after
 // another); all of a group's entries claim at once, then every thread walks the claimed rows' float4 columns.
+template <int U>
 __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const float2* __restrict__ tab, float* p,
                                                           float* m, float* v, int32_t* __restrict__ last_step,
-                                                          hvae_csr_batch x, int64_t H, int S) {
+                                                          hvae_csr_batch x, int64_t H, int S, int p_only_arg) {
   __shared__ int s_j[256], s_from[256], s_pst[256];
   __shared__ int s_n;
   const int to = (int)load_step(a.step_dev);
   const int64_t H4 = H / 4;
   const AdamK none{};
   // p alone moves ahead unless weight decay couples m, v to p, or m, v are too far behind to say so in the stamp
-  const bool p_only_ok = a.wd == 0.0;
+  const bool p_only_ok = a.wd == 0.0 && p_only_arg;
   const int sl = (int)(blockIdx.x % (unsigned)S);
   for (int64_t b = blockIdx.x / S; b < x.nb; b += gridDim.x / S) {
     const int64_t r = batch_row(x.rows, x.rows_offset, b);
@@ -466,7 +487,6 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
       }
       __syncthreads();
       const int64_t work = (int64_t)s_n * H4;
-      constexpr int U = kAdamUnroll;
       for (int64_t i0 = threadIdx.x; i0 < work; i0 += (int64_t)blockDim.x * U) {
         ColState cs[U];
         int64_t col[U];
@@ -518,6 +538,7 @@ static int lazy_sweep_period(int64_t N) {
   if (HVAE_LAZY_SWEEP > 0) return HVAE_LAZY_SWEEP;
   return N >= kLazySweepLargeN ? 32 : 8;
 }
+template <int U>
 __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restrict__ tab, float* __restrict__ p,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    int32_t* __restrict__ last_step, const float* __restrict__ rows,
@@ -537,7 +558,6 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
   const int nu = *n_unique;
   const int64_t H4 = H / 4;
   const int rr = threadIdx.x / rm.h4s, cc = threadIdx.x % rm.h4s;
-  constexpr int U = kAdamUnroll;
   const int64_t span = (int64_t)rm.rpb * U;
   if ((int)blockIdx.x < nb_rows) {
     for (int64_t g0 = (int64_t)blockIdx.x * span; g0 < nu; g0 += (int64_t)nb_rows * span) {
@@ -676,6 +696,7 @@ static int clip_launch(const float* g_dense, int64_t n_dense, const hvae_rowgrad
   a.g = g_dense; a.n = n_dense;
   a.rows = rg ? rg->rows : nullptr; a.n_unique = rg ? rg->n_unique : nullptr; a.H = H;
   a.rowsq = rg ? rg->rowsq : nullptr;
+  if (const char* e = ab_getenv("HVAE_ROWSQ")) if (std::atoi(e) == 0) a.rowsq = nullptr;
   a.part = (double*)ws;
   if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   a.max_norm = max_norm; a.norm_out = norm_out; a.coef_out = coef_out;
@@ -718,6 +739,7 @@ extern "C" int hvae_clip_grad_norm_step_adam(const float* g_dense, int64_t n_den
   a.g = g_dense; a.n = n_dense;
   a.rows = rg ? rg->rows : nullptr; a.n_unique = rg ? rg->n_unique : nullptr; a.H = H;
   a.rowsq = rg ? rg->rowsq : nullptr;
+  if (const char* e = ab_getenv("HVAE_ROWSQ")) if (std::atoi(e) == 0) a.rowsq = nullptr;
   a.part = (double*)ws;
   if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   a.max_norm = max_norm; a.norm_out = norm_out; a.coef_out = coef_out;
@@ -783,11 +805,12 @@ extern "C" int hvae_adam_lazy_catchup(const hvae_adam* cfg, const float* tab, fl
   if (N == 0) return HVAE_OK;
   const int64_t nrows = rows ? rows->cap : N;
   const RowMap rm = row_map(H);
-  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(nrows, (int64_t)rm.rpb * kAdamUnroll), 16384));
+  const int uu = adam_unroll();
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(nrows, (int64_t)rm.rpb * uu), 16384));
   ProbeScope probe("adam_catchup", as_stream(stream));
-  k_adam_catchup<<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v, last_step,
-                                                      rows ? rows->item_of : nullptr,
-                                                      rows ? rows->n_unique : nullptr, N, H, rm);
+  HVAE_ADAM_U_CALL(uu, (k_adam_catchup<U><<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v,
+                                                      last_step, rows ? rows->item_of : nullptr,
+                                                      rows ? rows->n_unique : nullptr, N, H, rm)));
   HVAE_LAUNCH_CHECK("k_adam_catchup");
   return HVAE_OK;
 }
@@ -802,8 +825,9 @@ extern "C" int hvae_adam_lazy_catchup_csr(const hvae_adam* cfg, const float* tab
   const int S = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(kCatchupBlocks, x->nb), 64));
   const unsigned grid = (unsigned)(std::min<int64_t>(x->nb, 16384) * S);
   ProbeScope probe("adam_catchup", as_stream(stream));
-  k_adam_catchup_csr<<<grid, 256, 0, as_stream(stream)>>>(to_args(cfg), (const float2*)tab, p, m, v, last_step, *x, H,
-                                                          S);
+  const int pon = catchup_p_only();
+  HVAE_ADAM_U_CALL(adam_unroll(), (k_adam_catchup_csr<U><<<grid, 256, 0, as_stream(stream)>>>(
+                                      to_args(cfg), (const float2*)tab, p, m, v, last_step, *x, H, S, pon)));
   HVAE_LAUNCH_CHECK("k_adam_catchup_csr");
   return HVAE_OK;
 }
@@ -822,14 +846,15 @@ extern "C" int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len,
   const int64_t N = rg->n_items;
   HVAE_REQUIRE(rg->slot_of, "hvae_adam_lazy: rowgrad without slot_of");
   const RowMap rm = row_map(H);
-  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, (int64_t)rm.rpb * kAdamUnroll), 4096));
+  const int uu = adam_unroll();
+  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, (int64_t)rm.rpb * uu), 4096));
   const int period = lazy_sweep_period(N);
-  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, period), (int64_t)rm.rpb * kAdamUnroll), 4096));
+  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, period), (int64_t)rm.rpb * uu), 4096));
   const int64_t b_dense = std::min<int64_t>(cdiv(cdiv(n_dense, 4), 256), 512);
   ProbeScope probe("adam_rows", as_stream(stream));
-  k_adam_lazy<<<(unsigned)(b_rows + b_sweep + b_dense), 256, 0, as_stream(stream)>>>(
+  HVAE_ADAM_U_CALL(uu, (k_adam_lazy<U><<<(unsigned)(b_rows + b_sweep + b_dense), 256, 0, as_stream(stream)>>>(
       to_args(cfg), (float2*)tab, p, m, v, last_step, rg->rows, rg->slot_of, rg->item_of, rg->n_unique, N, H,
-      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep, period, rm);
+      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep, period, rm)));
   HVAE_LAUNCH_CHECK("k_adam_lazy");
   return HVAE_OK;
 }

@@ -28,6 +28,8 @@ TAG_ENC_DROP = 0x100
 TAG_PROJ_DROP = 0x200
 TAG_EPS = 0x300
 
+ROWSQ_PARTS = 16  # include/hvae.h HVAE_ROWSQ_PARTS
+
 vp = C.c_void_p
 i64 = C.c_int64
 u64 = C.c_uint64

@@ -13,7 +13,7 @@ import ctypes as C
 import torch
 
 from . import _lib
-from ._lib import (CsrBatch, Epilogue, RowGrad, Adam, check, lib, ptr, require_hip, stream_of)
+from ._lib import (ROWSQ_PARTS, CsrBatch, Epilogue, RowGrad, Adam, check, lib, ptr, require_hip, stream_of)
 
 _WS: dict[torch.device, torch.Tensor] = {}
 
@@ -135,7 +135,7 @@ class RowGradBuffers:
         self.n_unique = torch.zeros(1, **i32)
         self.contrib_slot = torch.zeros(cap, **i32)
         self.part = torch.empty(int(lib().hvae_rowgrad_part_floats(cap, H)), dtype=torch.float32, device=device)
-        self.rowsq = torch.zeros(cap, dtype=torch.float64, device=device)
+        self.rowsq = torch.zeros(cap * ROWSQ_PARTS, dtype=torch.float64, device=device)
         self.cap, self.n_items, self.H = cap, n_items, H
         self.struct = RowGrad(ptr(self.cnt), ptr(self.slot_of), ptr(self.item_of), ptr(self.seg_off), ptr(self.fill),
                               ptr(self.contrib_row), ptr(self.contrib_val), ptr(self.rows), ptr(self.n_unique), cap,
