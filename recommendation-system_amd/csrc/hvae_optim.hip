@@ -685,6 +685,15 @@ extern "C" size_t hvae_clip_grad_norm_workspace(int64_t, int64_t, int64_t) {
   return kNormBlocks * sizeof(double);
 }
 
+// Blocks of the clip: enough for four 16-B loads in flight per thread over the largest possible input (the dense
+// gradient plus the cap's row partials or rows), at most kNormBlocks -- a small batch's clip is one memory round
+// trip and a last-block reduction, which fewer partials shorten
+static unsigned clip_blocks(const ClipArgs& a, const hvae_rowgrad* rg) {
+  int64_t units = a.n / 4;  // float4 of the dense gradient
+  if (rg) units += a.rowsq ? rg->cap * kRowSqParts / 2 : rg->cap * a.H / 4;
+  return (unsigned)std::max<int64_t>(1, std::min<int64_t>(cdiv(units, 256 * 4), kNormBlocks));
+}
+
 static int clip_launch(const float* g_dense, int64_t n_dense, const hvae_rowgrad* rg, int64_t H, float max_norm,
                        float* norm_out, float* coef_out, int64_t* step, int64_t* step_snap, int64_t* boff,
                        int64_t advance, void* ws, size_t ws_bytes, void* stream) {
@@ -702,7 +711,7 @@ static int clip_launch(const float* g_dense, int64_t n_dense, const hvae_rowgrad
   a.max_norm = max_norm; a.norm_out = norm_out; a.coef_out = coef_out;
   a.step = step; a.step_snap = step_snap; a.boff = boff; a.advance = advance;
   ProbeScope probe("clip", as_stream(stream));
-  k_clip_norm<<<kNormBlocks, 256, 0, as_stream(stream)>>>(a);
+  k_clip_norm<<<clip_blocks(a, rg), 256, 0, as_stream(stream)>>>(a);
   HVAE_LAUNCH_CHECK("k_clip_norm");
   return HVAE_OK;
 }
@@ -746,7 +755,7 @@ extern "C" int hvae_clip_grad_norm_step_adam(const float* g_dense, int64_t n_den
   a.step = step_dev; a.step_snap = step_snap; a.boff = boff; a.advance = advance;
   a.tab = (float2*)tab; a.lr = cfg->lr; a.b1 = cfg->beta1; a.b2 = cfg->beta2;
   ProbeScope probe("clip", as_stream(stream));
-  k_clip_norm<<<kNormBlocks, 256, 0, as_stream(stream)>>>(a);
+  k_clip_norm<<<clip_blocks(a, rg), 256, 0, as_stream(stream)>>>(a);
   HVAE_LAUNCH_CHECK("k_clip_norm");
   return HVAE_OK;
 }
