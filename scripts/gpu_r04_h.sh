@@ -11,13 +11,13 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method threa
   tests/test_gpu_kernels.py tests/test_gpu_train.py tests/test_gpu_ndcg.py tests/test_gpu_dp.py tests/test_gpu_large_step.py > $O/pytest.log 2>&1
 rc=$?; tail -3 $O/pytest.log; [ $rc -eq 0 ] || exit $rc
 echo "mlp rows A/B (Q = 1 / 2 / 4)"
-for q in 1 4 2 1 4; do
+for q in 1 4 8 2 1 4 8; do
   HVAE_LIB=build_var/libhvae_ab.so HVAE_MLP_Q=$q timeout -k 10 120 python -u scripts/bench_mlp_rows.py --reps 300 \
     --batches 64,200,512 > $O/mlp_q$q.jsonl 2>> $O/mlp.log || exit 5
   echo "Q=$q $(tr '\n' ' ' < $O/mlp_q$q.jsonl)"
 done
 echo "all_beauty A/B"
-for q in 1 4 1 4; do
+for q in 1 4 8 1 4 8; do
   HVAE_LIB=build_var/libhvae_ab.so HVAE_MLP_Q=$q timeout -k 10 200 python -u bench.py --workload all_beauty --steps 400 \
     --warmup 10 --no-cpu-baseline > $O/ab_q$q.json 2>> $O/ab.log || exit 6
   python3 -c "import json; d=json.load(open('$O/ab_q$q.json')); print('Q=$q', d['ms_per_step'])"
