@@ -270,8 +270,6 @@ class FusedTrainer:
         # before the row-gradient apply (the lazy-Adam catch-up then reads the batch's rows from the CSR)
         self.plan_side = bool(int(os.environ.get("HVAE_PLAN_SIDE", "1")))
         self.plan_stream = torch.cuda.Stream(device) if (self.plan_side and not self.two_streams) else None
-        # small batches: the row-parallel MLP's weight gradients beside the W1 row gather (HVAE_WGRAD_BESIDE=0: in line)
-        self.wgrad_beside_apply = bool(int(os.environ.get("HVAE_WGRAD_BESIDE", "1")))
         # below this batch the plan is short and the CSR catch-up's dependent loads cost more than the overlap
         # saves (All_Beauty B = 64: 0.1815 ms/step with the plan in line, 0.1965 beside; Syn-1M B = 4096:
         # 1.545 -> 1.293 ms/step beside)
@@ -509,7 +507,6 @@ class FusedTrainer:
                                    st2 if side_ else st), "gemm")
 
         ev_plan = None
-        ev_wg = None  # the row-parallel MLP's weight gradients, when they run on the plan stream
         dp = self.dp is not None
         plan_in_rows = (train and not dp and self.side is None and self.plan_in_rows and self._mlp_rows_ok(B)
                         and not (self.plan_stream is not None and B >= self.plan_side_min_batch)
@@ -671,16 +668,9 @@ class FusedTrainer:
                 wdesc(d, Lt, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt,
                       G["projection_layer.0.bias"]),
                 wdesc(2 * Lt, Hl, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl, self.gb_heads))
-            ps = self.plan_stream
-            if (ps is not None and side is main and not dp and len(H) == 1 and self.wgrad_beside_apply):
-                # the three weight gradients on the plan stream beside the W1 row gather (both read only what
-                # hvae_mlp_bwd_rows finished; the clip waits for both)
-                self._fork(main, ps)
-                check(L_.hvae_gemm_f32_multi(descs, 3, ps.cuda_stream), "gemm_multi")
-                ev_wg = torch.cuda.Event()
-                ev_wg.record(ps)
-            else:
-                check(L_.hvae_gemm_f32_multi(descs, 3, st), "gemm_multi")
+            # (on the plan stream beside the W1 row gather this ran slower: All_Beauty 0.147 vs 0.129 ms per step,
+            # profiles/r04_wgrad_beside_ab.jsonl)
+            check(L_.hvae_gemm_f32_multi(descs, 3, st), "gemm_multi")
         elif lay.has_proj:
             epi3 = Epilogue(_lib.EPI_GELU_DROP_BWD, None, None, ptr(bf.p1), p_drop, ptr(ext.get("proj_mask")), seed,
                             step, _lib.TAG_PROJ_DROP, tr, None)
@@ -717,8 +707,6 @@ class FusedTrainer:
             main.wait_event(ev_plan)
         if not dp:
             check(L_.hvae_w1_rowgrad_apply(ptr(bf.da[0]), H[0], bf.rg.ref, st), "w1_rowgrad_apply")
-        if ev_wg is not None:
-            main.wait_event(ev_wg)
         self._fork(side, main)  # join: every gradient is complete on the main stream
 
     def _mlp_rows_ok(self, B: int) -> bool:
