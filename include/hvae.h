@@ -291,7 +291,11 @@ typedef struct hvae_mlp_rows {
   /* backward, optional: the last hidden layer's LayerNorm -> GELU -> Dropout backward on dh, fused
    * (hvae_ln_gelu_drop_bwd's outputs: da, d_ln_w, d_ln_b and, if non-NULL, d_bias; its dropout stream
    * `enc_layer`, multipliers enc_drop_mult [nb, H] or NULL); ln_w == NULL: dh only. ws >=
-   * hvae_mlp_bwd_rows_workspace(nb, H) bytes for the column sums */
+   * hvae_mlp_bwd_rows_workspace(nb, H) bytes for the column sums. With d_ln_w == d_ln_b == d_bias == NULL the
+   * launch stops at the per-block column sums: ws then holds [hvae_mlp_rows_blocks(nb)][3][H] partials
+   * (d(ln_w) | d(ln_b) | d(bias) terms, each block's rows added in order) for the caller to add in block order,
+   * e.g. as three more products of the hvae_gemm_f32_multi launch that follows (partials^T x ones) -- one
+   * launch boundary instead of an in-kernel cross-block hand-off */
   const float* ln_w; const float* ln_b; const float* xhat; const float* rstd;
   const float* enc_drop_mult; uint32_t enc_layer;
   float* da; float* d_ln_w; float* d_ln_b; float* d_bias;
@@ -304,10 +308,12 @@ typedef struct hvae_mlp_rows {
 int hvae_mlp_fwd_rows(const hvae_mlp_rows* a, void* stream);
 int hvae_mlp_bwd_rows(const hvae_mlp_rows* a, void* stream);
 size_t hvae_mlp_bwd_rows_workspace(int64_t nb, int64_t H);
+/* blocks of the row-parallel MLP launches for nb rows (the partial count of the deferred column sums) */
+int64_t hvae_mlp_rows_blocks(int64_t nb);
 /* 1 if hvae_mlp_fwd_rows and hvae_mlp_bwd_rows accept a batch of nb rows at these widths (fused_enc: with the
  * first encoder layer in the forward launch), else 0 -- the caller then runs the GEMM chain */
 int hvae_mlp_rows_supported(int64_t nb, int64_t H, int64_t L, int64_t D, int fused_enc);
-/* Up to 4 independent weight gradients dW = A^T B (each desc trans_a = 1, trans_b = 0, no split-K,
+/* Up to 8 independent weight gradients dW = A^T B (each desc trans_a = 1, trans_b = 0, no split-K,
  * its own epilogue, e.g. opa_rowsum for the bias gradient) in one launch: the three Linear weight
  * gradients of the latent / projection MLP's backward (model.py:126-127,90-95) after hvae_mlp_bwd_rows. */
 int hvae_gemm_f32_multi(const hvae_gemm_desc* d, int n, void* stream);

@@ -141,5 +141,49 @@ __device__ __forceinline__ void encoder_sparse_row(
                        kTagEncDrop + 0u, train, h_out, xhat_out, rstd_out, h_lds);
 }
 
+// The sparse first layer of batch row b split over nsub waves: wave `sub` sums x_e W1t[j_e] over the row's entries
+// e = beg + sub, beg + sub + nsub, ... (entry order within the wave, four rows' loads in flight) into acc (no bias).
+// The caller adds the waves' partials in sub order and applies ln_gelu_drop_row.
+template <int NV>
+__device__ __forceinline__ void encoder_row_partial(const int64_t* __restrict__ row_ptr,
+                                                    const int32_t* __restrict__ col_idx,
+                                                    const float* __restrict__ vals, const int32_t* __restrict__ rows,
+                                                    const int64_t* __restrict__ rows_offset, int64_t b,
+                                                    const float* __restrict__ w1t, int64_t H, int sub, int nsub,
+                                                    float4 (&acc)[NV]) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = batch_row(rows, rows_offset, b);
+  const int64_t beg = row_ptr[r], end = row_ptr[r + 1];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t e0 = beg + sub; e0 < end; e0 += 4 * (int64_t)nsub) {
+    int j[4];
+    float x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t e = e0 + (int64_t)u * nsub;
+      j[u] = e < end ? col_idx[e] : 0;
+      x[u] = e < end ? vals[e] : 0.f;
+    }
+    float4 wv[4][NV];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int64_t c = 4 * (int64_t)(lane + 64 * k);
+        wv[u][k] = (c < H && e0 + (int64_t)u * nsub < end) ? *reinterpret_cast<const float4*>(w1t + (int64_t)j[u] * H + c)
+                                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (e0 + (int64_t)u * nsub >= end) break;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        acc[k].x += x[u] * wv[u][k].x; acc[k].y += x[u] * wv[u][k].y;
+        acc[k].z += x[u] * wv[u][k].z; acc[k].w += x[u] * wv[u][k].w;
+      }
+    }
+  }
+}
 
 }  // namespace hvae

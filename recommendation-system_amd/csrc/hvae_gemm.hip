@@ -661,7 +661,7 @@ __global__ void __launch_bounds__(256) k_gemm_f32_pair(GemmP g0, GemmP g1) {
 // Up to kMultiMax independent weight gradients dW = A^T B in one launch (the latent / projection MLP's three
 // after hvae_mlp_bwd_rows): block b runs the problem whose block range holds it, on the register-staged kernel
 // in 32 x 32 tiles, without split-K.
-constexpr int kMultiMax = 4;
+constexpr int kMultiMax = 8;
 struct GemmMulti {
   GemmP g[kMultiMax];
   unsigned start[kMultiMax + 1];
@@ -987,7 +987,7 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
 }
 
 extern "C" int hvae_gemm_f32_multi(const hvae_gemm_desc* d, int n, void* stream) {
-  HVAE_REQUIRE(d && n >= 1 && n <= kMultiMax, "hvae_gemm_f32_multi: 1..4 descriptors");
+  HVAE_REQUIRE(d && n >= 1 && n <= kMultiMax, "hvae_gemm_f32_multi: 1..8 descriptors");
   GemmMulti m{};
   m.n = 0;
   unsigned nblk = 0;

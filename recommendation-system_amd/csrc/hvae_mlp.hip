@@ -71,6 +71,16 @@ __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
   return fmaf(w.w, x.w, acc);
 }
 
+// A block barrier that orders LDS only: this wave's LDS writes have landed (lgkmcnt 0), its global loads stay in
+// flight (__syncthreads' workgroup fence would wait for them too). The layers issue their first weight loads
+// before it, so that their latency overlaps the previous phase (the encoder gather, an epilogue) of other waves.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0); vmcnt, expcnt left at their maxima
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // The layers are bound by how many bytes of weights a CU has in flight (one block streams all three matrices
 // from L2: 1.3 MB at d = 384), so every lane keeps kMlpLoads 16-B loads outstanding.
 constexpr int kMlpLoads = 16;
@@ -78,7 +88,9 @@ constexpr int kMlpLoads = 16;
 // ys[r][n] = sum_k xs[r][k] W[n][k] for n < N (N % 8 == 0, K % 32 == 0).
 // G output groups of 8 per wave at once, so that kMlpLoads loads are in flight per lane; chunks past K re-read
 // the last one and add it with a zero activation (every load unconditional)
-template <int R, int G, int LOADS>
+// PRE: the block barrier that makes xs visible is taken here, after every wave has issued the weight loads of its
+// first pass (by every wave once, outside any branch)
+template <int R, int G, int LOADS, bool PRE>
 __device__ __forceinline__ void rows_nt_g(const float* __restrict__ W, int N, int K, const float* xs, float* ys,
                                           int rotate) {
   constexpr int KCH = LOADS / G;  // 32-k chunks per pass
@@ -87,6 +99,19 @@ __device__ __forceinline__ void rows_nt_g(const float* __restrict__ W, int N, in
   // blocks start at different output groups, so that the blocks of an XCD stream different lines at a time
   // (all of them walking the matrix in the same order camp on the same L2 channels)
   const int rot = rotate ? (int)((blockIdx.x * 8u) % (unsigned)NG) : 0;
+  auto row_ptr = [&](int g0, int gi) {
+    return W + (int64_t)(8 * ((min(g0 + gi, NG - 1) + rot) % NG) + j) * K + 4 * c;
+  };
+  // the first pass of this wave's first output groups (k0 = 0; the clamp covers a K shorter than the pass), into
+  // the registers that pass then uses
+  float4 wv[G][KCH];
+  if (PRE && w * G < NG) {
+#pragma unroll
+    for (int gi = 0; gi < G; ++gi)
+#pragma unroll
+      for (int s = 0; s < KCH; ++s) wv[gi][s] = *reinterpret_cast<const float4*>(row_ptr(w * G, gi) + min(32 * s, K - 32));
+  }
+  if (PRE) lds_barrier();
   for (int g0 = w * G; g0 < NG; g0 += kMlpWaves * G) {
     float acc[G][R];
 #pragma unroll
@@ -95,15 +120,16 @@ __device__ __forceinline__ void rows_nt_g(const float* __restrict__ W, int N, in
       for (int r = 0; r < R; ++r) acc[gi][r] = 0.f;
     const float* wrow[G];
 #pragma unroll
-    for (int gi = 0; gi < G; ++gi) wrow[gi] = W + (int64_t)(8 * ((min(g0 + gi, NG - 1) + rot) % NG) + j) * K + 4 * c;
+    for (int gi = 0; gi < G; ++gi) wrow[gi] = row_ptr(g0, gi);
     auto pass = [&](int k0, auto full) {
       constexpr bool FULL = decltype(full)::value;
-      float4 wv[G][KCH];
+      if (!(PRE && g0 == w * G && k0 == 0)) {
 #pragma unroll
-      for (int gi = 0; gi < G; ++gi)
+        for (int gi = 0; gi < G; ++gi)
 #pragma unroll
-        for (int s = 0; s < KCH; ++s)
-          wv[gi][s] = *reinterpret_cast<const float4*>(wrow[gi] + (FULL ? k0 + 32 * s : min(k0 + 32 * s, K - 32)));
+          for (int s = 0; s < KCH; ++s)
+            wv[gi][s] = *reinterpret_cast<const float4*>(wrow[gi] + (FULL ? k0 + 32 * s : min(k0 + 32 * s, K - 32)));
+      }
 #pragma unroll
       for (int s = 0; s < KCH; ++s) {
         const int k = FULL ? k0 + 32 * s : min(k0 + 32 * s, K - 32);
@@ -137,13 +163,16 @@ __device__ __forceinline__ void rows_nt_g(const float* __restrict__ W, int N, in
   }
 }
 
-template <int R>
+// PRE (R > 1): the first weight loads before the barrier that publishes xs; R = 1 takes the barrier first (its 16
+// loads per lane leave no room for them to wait across it)
+template <int R, bool PRE = (R > 1)>
 __device__ __forceinline__ void rows_nt(const float* __restrict__ W, int N, int K, const float* xs, float* ys,
                                         int rotate) {
+  if (!PRE) __syncthreads();
   constexpr int LOADS = R == 1 ? kMlpLoads : kMlpLoads / 2;  // more rows: more arithmetic per byte, fewer registers
-  if (K >= 32 * LOADS * 3 / 4) rows_nt_g<R, 1, LOADS>(W, N, K, xs, ys, rotate);
-  else if (K >= 32 * LOADS * 3 / 8) rows_nt_g<R, 2, LOADS>(W, N, K, xs, ys, rotate);
-  else rows_nt_g<R, 4, LOADS>(W, N, K, xs, ys, rotate);
+  if (K >= 32 * LOADS * 3 / 4) rows_nt_g<R, 1, LOADS, PRE>(W, N, K, xs, ys, rotate);
+  else if (K >= 32 * LOADS * 3 / 8) rows_nt_g<R, 2, LOADS, PRE>(W, N, K, xs, ys, rotate);
+  else rows_nt_g<R, 4, LOADS, PRE>(W, N, K, xs, ys, rotate);
 }
 
 // out[r][n] = sum_k xs[r][k] W[k][n] for n < N (N % 4 == 0, N / 4 <= threads); part: LDS of
@@ -154,23 +183,32 @@ __device__ __forceinline__ void rows_nn(const float* __restrict__ W, int N, int 
                                         int rotate, Epi epi) {
   const int t = threadIdx.x, NQ = N / 4, S = kMlpThreads / NQ;
   const int qd = t % NQ, s = t / NQ;
-  if (s < S) {
-    // blocks take the k slices in rotated order (L2 channels, as in rows_nt_g); partials keep slice order
-    const int sk = rotate ? (int)((s + blockIdx.x) % (unsigned)S) : s;
-    const int k_lo = (int)((int64_t)K * sk / S), k_hi = (int)((int64_t)K * (sk + 1) / S);
+  constexpr int LOADS = kMlpLoads / R;  // more rows: more arithmetic per byte, fewer registers
+  // blocks take the k slices in rotated order (L2 channels, as in rows_nt_g); partials keep slice order
+  const bool act = s < S;
+  const int sk = !act ? 0 : rotate ? (int)((s + blockIdx.x) % (unsigned)S) : s;
+  const int k_lo = act ? (int)((int64_t)K * sk / S) : 0, k_hi = act ? (int)((int64_t)K * (sk + 1) / S) : 0;
+  const float* wp = W + 4 * qd;
+  float4 wv[LOADS];
+  auto load = [&](int k) {
+    const float* pk = wp + (int64_t)k * N;
+#pragma unroll
+    for (int e = 0; e < LOADS; ++e) {
+      wv[e] = *reinterpret_cast<const float4*>(pk);
+      pk += (k + e + 1 < k_hi) ? N : 0;
+    }
+  };
+  // the first chunk's weight loads go out before the barrier that makes xs visible (taken by every thread once,
+  // outside any branch); R = 1 (16 loads per lane) takes the barrier first
+  constexpr bool PRE = R > 1;
+  if (PRE && k_lo < k_hi) load(k_lo);
+  lds_barrier();
+  if (act) {
     float4 acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* wp = W + 4 * qd;
-    constexpr int LOADS = kMlpLoads / R;  // more rows: more arithmetic per byte, fewer registers
     for (int k = k_lo; k < k_hi; k += LOADS) {
-      float4 wv[LOADS];
-      const float* pk = wp + (int64_t)k * N;
-#pragma unroll
-      for (int e = 0; e < LOADS; ++e) {
-        wv[e] = *reinterpret_cast<const float4*>(pk);
-        pk += (k + e + 1 < k_hi) ? N : 0;
-      }
+      if (!PRE || k != k_lo) load(k);
 #pragma unroll
       for (int e = 0; e < LOADS; ++e) {
 #pragma unroll
@@ -219,35 +257,76 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * R;
   const int64_t step = load_step(p.step_dev);
-  if (p.enc_w1t) {  // the first encoder layer: wave w gathers, normalises and activates row w
-    if (w < R) {
-      const int64_t b = b0 + w;
-      if (b < p.nb) {
-        auto enc = [&](auto nv) {
-          encoder_sparse_row<decltype(nv)::value, false>(p.e_row_ptr, p.e_col_idx, p.e_vals, p.e_rows, p.e_rows_offset, b,
-                                                  p.enc_w1t, p.enc_b1, p.ln_w, p.ln_b, H, p.p_drop, p.scale,
-                                                  p.enc_drop_mult, p.seed, step, p.train, p.h_out, p.xhat_out,
-                                                  p.rstd_out, xs + w * H);
-        };
-        if (H <= 256) enc(std::integral_constant<int, 1>{});
-        else enc(std::integral_constant<int, 2>{});  // H <= 512 (host check)
-      } else {
-        for (int e = lane; e < H; e += 64) xs[w * H + e] = 0.f;
+  float* bsh = qs + R * D;  // [2L] b_heads | [D] b_a | [D] b_b: the epilogues' biases, fetched ahead (below)
+  auto fetch_biases = [&](int t0, int nt) {
+    for (int i = t0; i < L2 + 2 * D; i += nt) bsh[i] = i < L2 ? p.bh[i] : i < L2 + D ? p.ba[i - L2] : p.bb[i - L2 - D];
+  };
+  if (p.enc_w1t) {
+    // the first encoder layer, each row's entries dealt over kMlpWaves / R waves (one memory round trip each at
+    // ~10 entries a row, where one wave per row walked them four at a time): partials into LDS, then the row's
+    // first wave adds them in wave order to the bias and runs the LayerNorm / GELU / dropout
+    constexpr int WPR = kMlpWaves / R;
+    float* encp = bsh + L2 + 2 * D;  // [R][WPR][H]
+    const int r = w / WPR, sub = w % WPR;
+    const int64_t b = b0 + r;
+    auto part = [&](auto nv) {
+      constexpr int NV = decltype(nv)::value;
+      float4 acc[NV];
+      encoder_row_partial<NV>(p.e_row_ptr, p.e_col_idx, p.e_vals, p.e_rows, p.e_rows_offset, b, p.enc_w1t, H, sub,
+                              WPR, acc);
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        if (c < H) *reinterpret_cast<float4*>(encp + (r * WPR + sub) * H + c) = acc[k];
       }
+    };
+    auto fin = [&](auto nv) {
+      constexpr int NV = decltype(nv)::value;
+      float4 acc[NV];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int c = 4 * (lane + 64 * k);
+        acc[k] = c < H ? *reinterpret_cast<const float4*>(p.enc_b1 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      for (int s2 = 0; s2 < WPR; ++s2)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          const int c = 4 * (lane + 64 * k);
+          if (c >= H) continue;
+          const float4 v = *reinterpret_cast<const float4*>(encp + (r * WPR + s2) * H + c);
+          acc[k].x += v.x; acc[k].y += v.y; acc[k].z += v.z; acc[k].w += v.w;
+        }
+      ln_gelu_drop_row<NV>(acc, lane, H, b, p.ln_w, p.ln_b, p.p_drop, p.scale, p.enc_drop_mult, p.seed, step,
+                           kTagEncDrop + 0u, p.train, p.h_out, p.xhat_out, p.rstd_out, xs + r * H);
+    };
+    if (b < p.nb) {
+      if (H <= 256) part(std::integral_constant<int, 1>{});
+      else part(std::integral_constant<int, 2>{});  // H <= 512 (host check)
+    }
+    __syncthreads();
+    if (sub == 0) {
+      if (b < p.nb) {
+        if (H <= 256) fin(std::integral_constant<int, 1>{});
+        else fin(std::integral_constant<int, 2>{});
+      } else {
+        for (int e = lane; e < H; e += 64) xs[r * H + e] = 0.f;
+      }
+    } else {  // the waves the LayerNorm leaves idle fetch the biases meanwhile
+      fetch_biases((r * (WPR - 1) + sub - 1) * 64 + lane, R * (WPR - 1) * 64);
     }
   } else {
+    fetch_biases(t, kMlpThreads);
     for (int i = t; i < R * H / 4; i += kMlpThreads) {
       const int r = i / (H / 4), k4 = i % (H / 4);
       reinterpret_cast<float4*>(xs)[i] = (b0 + r < p.nb)
           ? reinterpret_cast<const float4*>(p.h + (b0 + r) * H)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  __syncthreads();
-  rows_nt<R>(p.Wh, L2, H, xs, hs, p.rot);
+  rows_nt<R>(p.Wh, L2, H, xs, hs, p.rot);  // (its barrier publishes xs)
   __syncthreads();
   for (int i = t; i < R * L2; i += kMlpThreads) {
     const int r = i / L2, n = i % L2;
-    const float v = hs[i] + p.bh[n];
+    const float v = hs[i] + bsh[n];
     hs[i] = v;
     if (b0 + r < p.nb) p.heads[(b0 + r) * L2 + n] = v;
   }
@@ -273,13 +352,12 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
     kl = wave_sum(kl);
     if (lane == 0 && valid) p.kl_rows[b] = -0.5f * kl;
   }
-  __syncthreads();
-  rows_nt<R>(p.Wa, D, L, zs, ys, p.rot);
+  rows_nt<R>(p.Wa, D, L, zs, ys, p.rot);  // (its barrier publishes zs)
   __syncthreads();
   for (int i = t; i < R * D; i += kMlpThreads) {
     const int r = i / D, n = i % D;
     const int64_t b = b0 + r;
-    const float pre = ys[i] + p.ba[n];
+    const float pre = ys[i] + bsh[L2 + n];
     const float g = gelu_f(pre);
     float qv = g;
     if (p.train && b < p.nb)
@@ -290,12 +368,11 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
       p.q[b * D + n] = qv;
     }
   }
-  __syncthreads();
-  rows_nt<R>(p.Wb, D, D, qs, ys, p.rot);
+  rows_nt<R>(p.Wb, D, D, qs, ys, p.rot);  // (its barrier publishes qs)
   __syncthreads();
   for (int i = t; i < R * D; i += kMlpThreads) {
     const int r = i / D, n = i % D;
-    if (b0 + r < p.nb) p.u[(b0 + r) * D + n] = ys[i] + p.bb[n];
+    if (b0 + r < p.nb) p.u[(b0 + r) * D + n] = ys[i] + bsh[L2 + D + n];
   }
 }
 
@@ -309,16 +386,34 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
   float* dhs = ds + R * L2;    // [R][H]  dh (LayerNorm backward)
   float* dxs = dhs + R * H;    // [R][H]  dxhat (LayerNorm backward)
   float* part = dxs + R * H;   // slice partials of rows_nn; then the LayerNorm column terms [3][R][H]
+  // the epilogues' row inputs, fetched with dU so that no epilogue waits on its own loads
+  float* pf_p1 = part + 4 * kMlpThreads * R;  // [R][D]
+  float* pf_heads = pf_p1 + R * D;             // [R][2L]
+  float* pf_eps = pf_heads + R * L2;           // [R][L]
+  float* pf_xhat = pf_eps + R * L;             // [R][H]
+  float* pf_lnw = pf_xhat + R * H;             // [H]
+  float* pf_lnb = pf_lnw + H;                  // [H]
+  float* pf_rstd = pf_lnb + H;                 // [R]
   const int t = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * R;
   const int64_t step = load_step(p.step_dev);
   const float ks = p.ks_dev ? *p.ks_dev : p.ks;
-  for (int i = t; i < R * D / 4; i += kMlpThreads) {
-    const int r = i / (D / 4), k4 = i % (D / 4);
-    reinterpret_cast<float4*>(gs)[i] = (b0 + r < p.nb)
-        ? reinterpret_cast<const float4*>(p.dU + (b0 + r) * D)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  auto rows4 = [&](float* dst, const float* src, int w4) {  // R rows of w4 float4 (zero past the batch)
+    for (int i = t; i < R * w4; i += kMlpThreads) {
+      const int r = i / w4, k4 = i % w4;
+      reinterpret_cast<float4*>(dst)[i] = (b0 + r < p.nb)
+          ? reinterpret_cast<const float4*>(src + (b0 + r) * (int64_t)w4 * 4)[k4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  rows4(gs, p.dU, D / 4);
+  rows4(pf_p1, p.p1, D / 4);
+  rows4(pf_heads, p.heads, L2 / 4);
+  if (p.train) rows4(pf_eps, p.eps, L / 4);
+  if (p.ln_w) {
+    rows4(pf_xhat, p.xhat, H / 4);
+    for (int i = t; i < 2 * H; i += kMlpThreads) pf_lnw[i] = i < H ? p.ln_w[i] : p.ln_b[i - H];  // (pf_lnb follows)
+    if (t < R) pf_rstd[t] = b0 + t < p.nb ? p.rstd[b0 + t] : 0.f;
   }
-  __syncthreads();
   // dp1 = (dU W_b) * dropmult * GELU'(p1)   (HVAE_EPI_GELU_DROP_BWD)
   rows_nn<R>(p.Wb, D, D, gs, part, p.rot, [&](int r, int n, float v) {
     const int64_t b = b0 + r;
@@ -327,7 +422,7 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
       const float dm = p.train ? dropout_mult(p.p_drop, p.scale, p.drop_mult, (uint64_t)(b * D + n), p.seed, step,
                                               kTagProjDrop)
                                : 1.f;
-      g = v * dm * gelu_grad_f(p.p1[b * D + n]);
+      g = v * dm * gelu_grad_f(pf_p1[r * D + n]);
       p.dp1[b * D + n] = g;
     }
     ps[r * D + n] = g;
@@ -337,8 +432,8 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
     const int64_t b = b0 + r;
     float dmu = 0.f, dlv = 0.f;
     if (b < p.nb) {
-      const float m = p.heads[b * L2 + l], lv = p.heads[b * L2 + L + l];
-      const float gz = p.train ? v * p.eps[b * L + l] * 0.5f * expf(0.5f * lv) : 0.f;
+      const float m = pf_heads[r * L2 + l], lv = pf_heads[r * L2 + L + l];
+      const float gz = p.train ? v * pf_eps[r * L + l] * 0.5f * expf(0.5f * lv) : 0.f;
       dlv = gz + ks * 0.5f * (expf(lv) - 1.f);
       dmu = v + ks * m;
       p.dheads[b * L2 + l] = dmu;
@@ -363,12 +458,12 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
   if (w < R) {
     const int64_t b = b0 + w;
     if (b < p.nb) {
-      const float invH = 1.0f / (float)H, rs = p.rstd[b];
+      const float invH = 1.0f / (float)H, rs = pf_rstd[w];
       float s1 = 0.f, s2 = 0.f;
       for (int e = 4 * lane; e < H; e += 256) {
-        const float4 xh = *reinterpret_cast<const float4*>(p.xhat + b * H + e);
-        const float4 lw = *reinterpret_cast<const float4*>(p.ln_w + e);
-        const float4 lb = *reinterpret_cast<const float4*>(p.ln_b + e);
+        const float4 xh = *reinterpret_cast<const float4*>(pf_xhat + w * H + e);
+        const float4 lw = *reinterpret_cast<const float4*>(pf_lnw + e);
+        const float4 lb = *reinterpret_cast<const float4*>(pf_lnb + e);
         const float xv[4] = {xh.x, xh.y, xh.z, xh.w}, wv[4] = {lw.x, lw.y, lw.z, lw.w};
         const float bv[4] = {lb.x, lb.y, lb.z, lb.w};
 #pragma unroll
@@ -387,7 +482,7 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
       }
       const float m1 = wave_sum(s1) * invH, m2 = wave_sum(s2) * invH;
       for (int e = 4 * lane; e < H; e += 256) {
-        const float4 xh = *reinterpret_cast<const float4*>(p.xhat + b * H + e);
+        const float4 xh = *reinterpret_cast<const float4*>(pf_xhat + w * H + e);
         float4 o;
         o.x = rs * (dxs[w * H + e + 0] - m1 - xh.x * m2);
         o.y = rs * (dxs[w * H + e + 1] - m1 - xh.y * m2);
@@ -402,6 +497,17 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
   }
   __syncthreads();
   float* gpart = p.ln_part;  // [blocks][3][H]
+  if (!p.d_ln_w) {  // deferred: the block's partials only, added in block order by the caller's next launch
+    for (int i = t; i < 3 * H; i += kMlpThreads) {
+      const int kind = i / H, col = i % H;
+      const float* src = part + kind * R * H + col;
+      float v = src[0];
+#pragma unroll
+      for (int r = 1; r < R; ++r) v += src[r * H];
+      gpart[(int64_t)blockIdx.x * 3 * H + i] = v;
+    }
+    return;
+  }
   for (int i = t; i < 3 * H; i += kMlpThreads) {
     const int kind = i / H, col = i % H;
     const float* src = part + kind * R * H + col;
@@ -413,16 +519,16 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_bwd_rows(MlpP p) {
   if (!last_block_arrives(p.ln_ticket, gridDim.x)) return;
   const int np = gridDim.x;
   for (int i = t; i < 3 * H; i += kMlpThreads) {
+    // the blocks' partials in block order, 32 loads in flight (one round trip at B = 64)
     float sum = 0.f;
-    int q = 0;
-    for (; q + 8 <= np; q += 8) {
-      float v[8];
+    for (int q = 0; q < np; q += 32) {
+      float v[32];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = ld_shared_f(&gpart[(int64_t)(q + j) * 3 * H + i]);
+      for (int j = 0; j < 32; ++j) v[j] = q + j < np ? ld_shared_f(&gpart[(int64_t)(q + j) * 3 * H + i]) : 0.f;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sum += v[j];
+      for (int j = 0; j < 32; ++j)
+        if (q + j < np) sum += v[j];
     }
-    for (; q < np; ++q) sum += ld_shared_f(&gpart[(int64_t)q * 3 * H + i]);
     if (i < H) p.d_ln_w[i] = sum;
     else if (i < 2 * H) p.d_ln_b[i - H] = sum;
     else if (p.d_bias) p.d_bias[i - 2 * H] = sum;
@@ -440,9 +546,13 @@ static int mlp_rows_per_block(int64_t nb) {
   return nb <= 32 ? 1 : nb <= 512 ? 2 : 4;
 }
 
-static size_t mlp_fwd_smem(int R, const hvae_mlp_rows* a) { return (size_t)R * (a->H + 3 * a->L + 2 * a->D) * 4; }
+static size_t mlp_fwd_smem(int R, const hvae_mlp_rows* a) {
+  // + the biases, + the encoder layer's per-wave partials (kMlpWaves rows of H)
+  return ((size_t)R * (a->H + 3 * a->L + 2 * a->D) + 2 * a->L + 2 * a->D + (a->enc_x ? (size_t)kMlpWaves * a->H : 0)) * 4;
+}
 static size_t mlp_bwd_smem(int R, const hvae_mlp_rows* a) {
-  return (size_t)R * (2 * a->D + 2 * a->L + 2 * a->H) * 4 + (size_t)4 * kMlpThreads * R * 4;
+  return (size_t)R * (2 * a->D + 2 * a->L + 2 * a->H) * 4 + (size_t)4 * kMlpThreads * R * 4 +
+         ((size_t)R * (a->D + 3 * a->L + a->H) + 2 * a->H + 4) * 4;  // + the prefetched epilogue inputs
 }
 
 constexpr size_t kMlpLdsMax = 159 * 1024;  // gfx950 LDS per CU (160 KiB) less the kernels' static LDS
@@ -544,10 +654,14 @@ extern "C" int hvae_mlp_rows_supported(int64_t nb, int64_t H, int64_t L, int64_t
     if (v < 32 || v > 1024 || v % 32) return 0;
   if (fused_enc && H > 512) return 0;
   hvae_mlp_rows a{};
+  hvae_csr_batch x{};  // (only its presence counts: the fused encoder layer's LDS)
   a.nb = nb; a.H = H; a.L = L; a.D = D;
+  if (fused_enc) a.enc_x = &x;
   const int R = mlp_rows_per_block(nb);
   return mlp_fwd_smem(R, &a) <= kMlpLdsMax && mlp_bwd_smem(R, &a) <= kMlpLdsMax;
 }
+
+extern "C" int64_t hvae_mlp_rows_blocks(int64_t nb) { return nb > 0 ? cdiv(nb, mlp_rows_per_block(nb)) : 0; }
 
 extern "C" size_t hvae_mlp_bwd_rows_workspace(int64_t nb, int64_t H) {
   return nb > 0 ? (size_t)cdiv(nb, mlp_rows_per_block(nb)) * 3 * H * sizeof(float) : 0;
@@ -557,10 +671,13 @@ extern "C" int hvae_mlp_bwd_rows(const hvae_mlp_rows* a, void* stream) {
   MlpP p{};
   if (int rc = mlp_setup(a, false, p)) return rc;
   if (a->ln_w) {
-    HVAE_REQUIRE(a->ln_b && a->xhat && a->rstd && a->da && a->d_ln_w && a->d_ln_b,
-                 "hvae_mlp_bwd_rows: LayerNorm backward needs ln_b, xhat, rstd, da, d_ln_w, d_ln_b");
+    const bool deferred = !a->d_ln_w && !a->d_ln_b && !a->d_bias;
+    HVAE_REQUIRE(a->ln_b && a->xhat && a->rstd && a->da && ((a->d_ln_w && a->d_ln_b) || deferred),
+                 "hvae_mlp_bwd_rows: LayerNorm backward needs ln_b, xhat, rstd, da and d_ln_w, d_ln_b (or none of "
+                 "d_ln_w, d_ln_b, d_bias: deferred column sums)");
     if (a->nb == 0) {
       hipStream_t st = as_stream(stream);
+      if (deferred) return HVAE_OK;  // no blocks, no partials
       HVAE_HIP(hipMemsetAsync(a->d_ln_w, 0, a->H * sizeof(float), st));
       HVAE_HIP(hipMemsetAsync(a->d_ln_b, 0, a->H * sizeof(float), st));
       if (a->d_bias) HVAE_HIP(hipMemsetAsync(a->d_bias, 0, a->H * sizeof(float), st));
@@ -573,7 +690,7 @@ extern "C" int hvae_mlp_bwd_rows(const hvae_mlp_rows* a, void* stream) {
     p.enc_tag = kTagEncDrop + a->enc_layer;
     p.da = a->da; p.d_ln_w = a->d_ln_w; p.d_ln_b = a->d_ln_b; p.d_bias = a->d_bias;
     p.ln_part = (float*)a->ws;
-    if (!(p.ln_ticket = ticket_slice())) return HVAE_ERR_HIP;
+    if (!deferred && !(p.ln_ticket = ticket_slice())) return HVAE_ERR_HIP;
   }
   if (a->nb == 0) return HVAE_OK;
   const int R = mlp_rows_per_block(a->nb);

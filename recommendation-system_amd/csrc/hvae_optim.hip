@@ -564,12 +564,20 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
       int64_t sidx[U], j[U];
       int from[U], pst[U];
       bool act[U];
+      // the row's stamp, its first column's (p, m, v) and gradient are loaded together (one round trip after
+      // item_of instead of two)
+      ColState cs0[U];
+      float4 gv0[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         sidx[u] = g0 + (int64_t)u * rm.rpb + rr;
         act[u] = rr < rm.rpb && sidx[u] < nu;
         j[u] = act[u] ? (int64_t)item_of[sidx[u]] : 0;
         const int32_t ls = act[u] ? last_step[j[u]] : t;
+        if (act[u] && cc < H4) {
+          cs0[u] = col_load(p, m, v, j[u] * H4 + cc);
+          gv0[u] = *reinterpret_cast<const float4*>(rows + sidx[u] * H + 4 * cc);
+        }
         from[u] = ls_mv(ls);
         pst[u] = ls_p(ls);
       }
@@ -579,8 +587,13 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
 #pragma unroll
         for (int u = 0; u < U; ++u)
           if (act[u]) {
-            cs[u] = col_load(p, m, v, j[u] * H4 + c);
-            gv[u] = *reinterpret_cast<const float4*>(rows + sidx[u] * H + 4 * c);
+            if (c == cc) {
+              cs[u] = cs0[u];
+              gv[u] = gv0[u];
+            } else {
+              cs[u] = col_load(p, m, v, j[u] * H4 + c);
+              gv[u] = *reinterpret_cast<const float4*>(rows + sidx[u] * H + 4 * c);
+            }
           }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -605,6 +618,10 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
       int64_t j[U];
       int from[U], pst[U];
       bool act[U];
+      // the row's slot, stamp and first column's (p, m, v) are loaded together, before it is known whether the row
+      // is this group's (no gradient) and stale: the speculative loads of the skipped rows cost bytes, not a round
+      // trip
+      ColState cs0[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         j[u] = g0 + (int64_t)u * rm.rpb + rr;
@@ -612,10 +629,11 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
         from[u] = pst[u] = t;
         if (act[u]) {
           const int sl = slot_of[j[u]];
+          const int32_t ls = last_step[j[u]];
+          if (cc < H4) cs0[u] = col_load(p, m, v, j[u] * H4 + cc);
           if (sl >= 0 && sl < nu && item_of[sl] == (int32_t)j[u]) {
             act[u] = false;  // has a gradient: first group's row
           } else {
-            const int32_t ls = last_step[j[u]];
             from[u] = ls_mv(ls);
             pst[u] = ls_p(ls);
           }
@@ -626,7 +644,7 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
         ColState cs[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (act[u]) cs[u] = col_load(p, m, v, j[u] * H4 + c);
+          if (act[u]) cs[u] = c == cc ? cs0[u] : col_load(p, m, v, j[u] * H4 + c);
 #pragma unroll
         for (int u = 0; u < U; ++u)
           if (act[u]) col_math_lazy(a, tab, cs[u], from[u], pst[u], t - 1, true, k, make_float4(0.f, 0.f, 0.f, 0.f));

@@ -131,6 +131,7 @@ SIGNATURES = {
     "hvae_mlp_fwd_rows": (cint, [P(MlpRows), vp]),
     "hvae_mlp_bwd_rows": (cint, [P(MlpRows), vp]),
     "hvae_mlp_bwd_rows_workspace": (sz, [i64, i64]),
+    "hvae_mlp_rows_blocks": (i64, [i64]),
     "hvae_mlp_rows_supported": (cint, [i64, i64, i64, i64, cint]),
     "hvae_gemm_f32_multi": (cint, [P(GemmDesc), cint, vp]),
     "hvae_decoder_image_bytes": (sz, [cint, i64, i64]),

@@ -279,6 +279,10 @@ class FusedTrainer:
         self._mlp_rows_cache: dict[int, bool] = {}
         # and, when the batch's row-gradient plan fits one block, that plan as one more block of the same launch
         self.plan_in_rows = bool(int(os.environ.get("HVAE_PLAN_IN_ROWS", "1")))
+        # the row-parallel MLP backward's LayerNorm column sums finished by the weight-gradient launch
+        # (HVAE_LN_COLS_DEFERRED=0: in the backward launch, a last-block reduction)
+        self.ln_cols_deferred = bool(int(os.environ.get("HVAE_LN_COLS_DEFERRED", "1")))
+        self.ones = torch.ones(1024, dtype=torch.float32, device=device)
         self.boff = torch.zeros(1, dtype=torch.int64, device=device)
         self.norm = torch.zeros(1, device=device)
         self.coef = torch.ones(1, device=device)
@@ -652,25 +656,36 @@ class FusedTrainer:
             rows.ln_w, rows.ln_b = ptr(self.P[f"encoder.{il + 1}.weight"]), ptr(self.P[f"encoder.{il + 1}.bias"])
             rows.xhat, rows.rstd, rows.enc_drop_mult = ptr(bf.xhat[kl_]), ptr(bf.rstd[kl_]), ptr(encm[kl_])
             rows.enc_layer = kl_
-            rows.da, rows.d_ln_w = ptr(bf.da[kl_]), ptr(G[f"encoder.{il + 1}.weight"])
-            rows.d_ln_b, rows.d_bias = ptr(G[f"encoder.{il + 1}.bias"]), ptr(G[f"encoder.{il}.bias"])
+            ln_grads = (G[f"encoder.{il + 1}.weight"], G[f"encoder.{il + 1}.bias"], G[f"encoder.{il}.bias"])
+            rows.da = ptr(bf.da[kl_])
+            if self.ln_cols_deferred:
+                # the LayerNorm column sums stop at per-block partials in ws; the weight-gradient launch below adds
+                # them in block order (partials^T x ones), instead of an in-kernel cross-block hand-off
+                rows.d_ln_w = rows.d_ln_b = rows.d_bias = None
+            else:
+                rows.d_ln_w, rows.d_ln_b, rows.d_bias = (ptr(g) for g in ln_grads)
             rows.ws, rows.ws_bytes = ws, wsn
             check(L_.hvae_mlp_bwd_rows(C.byref(rows), st), "mlp_bwd_rows")
             keep = []
 
-            def wdesc(M, N, A, lda, Bm, ldb, Cm, ldc, rowsum):
+            def wdesc(M, N, A, lda, Bm, ldb, Cm, ldc, rowsum, K=B):
                 e = Epilogue(_lib.EPI_NONE, None, None, None, 0.0, None, 0, None, 0, 0, ptr(rowsum))
                 keep.append(e)
-                return GemmDesc(1, 0, M, N, B, 1.0, A, lda, Bm, ldb, 0.0, Cm, ldc, C.pointer(e), None, 0)
-            descs = (GemmDesc * 3)(
-                wdesc(d, d, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d,
-                      G["projection_layer.3.bias"]),
-                wdesc(d, Lt, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt,
-                      G["projection_layer.0.bias"]),
-                wdesc(2 * Lt, Hl, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl, self.gb_heads))
+                return GemmDesc(1, 0, M, N, K, 1.0, A, lda, Bm, ldb, 0.0, Cm, ldc, C.pointer(e), None, 0)
+            dl = [wdesc(d, d, ptr(bf.dU), d, ptr(bf.q), d, ptr(G["projection_layer.3.weight"]), d,
+                        G["projection_layer.3.bias"]),
+                  wdesc(d, Lt, ptr(bf.dp1), d, ptr(bf.z), Lt, ptr(G["projection_layer.0.weight"]), Lt,
+                        G["projection_layer.0.bias"]),
+                  wdesc(2 * Lt, Hl, ptr(bf.dheads), 2 * Lt, ptr(bf.h[-1]), Hl, ptr(self.gW_heads), Hl, self.gb_heads)]
+            if self.ln_cols_deferred:
+                nblk = int(L_.hvae_mlp_rows_blocks(B))
+                for kind, g in enumerate(ln_grads):  # column sums of the [blocks, 3, H] partials: partials^T ones
+                    dl.append(GemmDesc(1, 0, Hl, 1, nblk, 1.0, ws + 4 * kind * Hl, 3 * Hl,
+                                       ptr(self.ones), 1, 0.0, ptr(g), 1, None, None, 0))
+            descs = (GemmDesc * len(dl))(*dl)
             # (on the plan stream beside the W1 row gather this ran slower: All_Beauty 0.147 vs 0.129 ms per step,
             # profiles/r04_wgrad_beside_ab.jsonl)
-            check(L_.hvae_gemm_f32_multi(descs, 3, st), "gemm_multi")
+            check(L_.hvae_gemm_f32_multi(descs, len(dl), st), "gemm_multi")
         elif lay.has_proj:
             epi3 = Epilogue(_lib.EPI_GELU_DROP_BWD, None, None, ptr(bf.p1), p_drop, ptr(ext.get("proj_mask")), seed,
                             step, _lib.TAG_PROJ_DROP, tr, None)

@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--d", type=int, default=384)
     ap.add_argument("--shapes", default=None,
                     help="H:L:D list (e.g. 512:128:384,32:32:384) timed at the first batch instead of --d")
+    ap.add_argument("--fused", action="store_true", help="time the step's composition (encoder layer, plan block, "
+                    "LayerNorm backward) at the first batch")
+    ap.add_argument("--lam", type=float, default=3.0, help="--fused: synth_csr lam (All_Beauty: 3)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     if args.shapes:
@@ -53,6 +56,48 @@ def main():
                               "weight_bytes": 4 * (2 * L * H + D * L + D * D)}), flush=True)
         return
     H, L, D = 512, 128, args.d
+    if args.fused:
+        # the step's composition at the first batch: + the fused encoder layer (enc_x), + the plan block (plan_x),
+        # + the backward's LayerNorm (ln_w), on an All_Beauty-like CSR batch
+        from gen import synth_csr
+        from hvae import _lib, ops
+        from hvae._lib import ptr
+        B = int(args.batches.split(",")[0])
+        N = 12101
+        X = synth_csr(B, N, lam=args.lam, seed=5)
+        xd = ops.csr_from_scipy(X, dev)
+        g = torch.Generator().manual_seed(9)
+        w1t = (torch.randn(N, H, generator=g) * 0.05).to(dev)
+        b1, lnw, lnb = (torch.randn(H, generator=g) * 0.1).to(dev), (1 + 0.1 * torch.randn(H, generator=g)).to(dev), \
+            (0.1 * torch.randn(H, generator=g)).to(dev)
+        h, xhat, rstd = torch.empty(B, H, device=dev), torch.empty(B, H, device=dev), torch.empty(B, device=dev)
+        rg = ops.RowGradBuffers(N, H, max(int(X.nnz), 1), dev)
+        da, dw, db, dbias = (torch.empty(B, H, device=dev), torch.empty(H, device=dev), torch.empty(H, device=dev),
+                             torch.empty(H, device=dev))
+        ws = torch.empty(max(int(lib().hvae_mlp_bwd_rows_workspace(B, H)), 256), dtype=torch.uint8, device=dev)
+        for enc in (0, 1):
+            for plan in (0, 1):
+                t, d, out = _setup(B, H, L, D, dev, 1)
+                a = _args(B, H, L, D, d, out, True, 0.3, explicit=False, seed=3)
+                if enc:
+                    a.enc_x, a.w1t, a.b1, a.ln_w, a.ln_b = C.pointer(xd.struct), ptr(w1t), ptr(b1), ptr(lnw), ptr(lnb)
+                    a.h, a.xhat, a.rstd = ptr(h), ptr(xhat), ptr(rstd)
+                if plan:
+                    a.plan_x, a.plan_rg = C.pointer(xd.struct), C.pointer(rg.struct)
+                fwd = probe("mlp_fwd", lambda: check(lib().hvae_mlp_fwd_rows(C.byref(a), None), "fwd"), args.reps)
+                print(json.dumps({"B": B, "nnz": int(X.nnz), "enc": enc, "plan": plan, "fwd_us": fwd}), flush=True)
+        for ln in (0, 1):
+            t, d, out = _setup(B, H, L, D, dev, 1)
+            a = _args(B, H, L, D, d, out, True, 0.3, explicit=False, seed=3)
+            check(lib().hvae_mlp_fwd_rows(C.byref(a), None), "fwd")
+            if ln:
+                xhat.normal_()
+                rstd.uniform_(0.5, 1.5)
+                a.ln_w, a.ln_b, a.xhat, a.rstd, a.enc_layer = ptr(lnw), ptr(lnb), ptr(xhat), ptr(rstd), 0
+                a.da, a.d_ln_w, a.d_ln_b, a.d_bias, a.ws, a.ws_bytes = ptr(da), ptr(dw), ptr(db), ptr(dbias), ptr(ws), ws.numel()
+            bwd = probe("mlp_bwd", lambda: check(lib().hvae_mlp_bwd_rows(C.byref(a), None), "bwd"), args.reps)
+            print(json.dumps({"B": B, "ln": ln, "bwd_us": bwd}), flush=True)
+        return
     for B in (int(b) for b in args.batches.split(",")):
         t, d, out = _setup(B, H, L, D, dev, 1)
         a = _args(B, H, L, D, d, out, True, 0.3, explicit=False, seed=3)

@@ -220,3 +220,45 @@ def test_mlp_bwd_fused_layernorm_equals_ln_bwd(hip_device, B, H, train, explicit
                                                  drop_mult=emult, want_dbias=True)
     assert torch.equal(da, da2)
     assert _maxrel(dw, dw2) < 1e-5 and _maxrel(db, db2) < 1e-5 and _maxrel(dbias, dbias2) < 1e-5
+
+
+@pytest.mark.parametrize("B", [64, 300])
+def test_mlp_bwd_deferred_layernorm_columns(hip_device, B):
+    """With d_ln_w = d_ln_b = d_bias = NULL hvae_mlp_bwd_rows leaves its per-block column sums in ws
+    ([hvae_mlp_rows_blocks(B)][3][H]) and hvae_gemm_f32_multi finishes them (partials^T x ones), as the fused
+    trainer does: da bitwise the in-launch reduction's, the three column sums to fp32 rounding of its block-order
+    sums."""
+    from hvae import _lib
+    from hvae._lib import GemmDesc, check, lib, ptr
+    H, L, D = 512, 128, 384
+    t, d, out = _setup(B, H, L, D, hip_device, 13)
+    g = torch.Generator().manual_seed(14)
+    xhat = torch.randn(B, H, generator=g).to(hip_device)
+    rstd = (torch.rand(B, generator=g) + 0.5).to(hip_device)
+    ln_w = (torch.randn(H, generator=g) * 0.2 + 1).to(hip_device)
+    ln_b = (torch.randn(H, generator=g) * 0.1).to(hip_device)
+    step = torch.tensor([4], dtype=torch.int64, device=hip_device)
+    res = []
+    for deferred in (False, True):
+        a = _args(B, H, L, D, d, out, True, 0.3, explicit=True, seed=78, step=step)
+        check(lib().hvae_mlp_fwd_rows(C.byref(a), None), "mlp_fwd_rows")
+        da, dw, db, dbias = (torch.full((B, H), 7.0, device=hip_device), torch.empty(H, device=hip_device),
+                             torch.empty(H, device=hip_device), torch.empty(H, device=hip_device))
+        ws = torch.empty(max(int(lib().hvae_mlp_bwd_rows_workspace(B, H)), 256), dtype=torch.uint8, device=hip_device)
+        a.ln_w, a.ln_b, a.xhat, a.rstd, a.enc_drop_mult, a.enc_layer = ptr(ln_w), ptr(ln_b), ptr(xhat), ptr(rstd), None, 0
+        a.da, a.ws, a.ws_bytes = ptr(da), ptr(ws), ws.numel()
+        if deferred:
+            a.d_ln_w = a.d_ln_b = a.d_bias = None
+        else:
+            a.d_ln_w, a.d_ln_b, a.d_bias = ptr(dw), ptr(db), ptr(dbias)
+        check(lib().hvae_mlp_bwd_rows(C.byref(a), None), "mlp_bwd_rows")
+        if deferred:
+            nblk = int(lib().hvae_mlp_rows_blocks(B))
+            ones = torch.ones(nblk, device=hip_device)
+            descs = (GemmDesc * 3)(*[GemmDesc(1, 0, H, 1, nblk, 1.0, ptr(ws) + 4 * k * H, 3 * H, ptr(ones), 1, 0.0,
+                                              ptr(o), 1, None, None, 0) for k, o in enumerate((dw, db, dbias))])
+            check(lib().hvae_gemm_f32_multi(descs, 3, None), "gemm_multi")
+        res.append((da.clone(), dw.clone(), db.clone(), dbias.clone()))
+    (da0, dw0, db0, dbias0), (da1, dw1, db1, dbias1) = res
+    assert torch.equal(da0, da1)
+    assert _maxrel(dw1, dw0) < 1e-5 and _maxrel(db1, db0) < 1e-5 and _maxrel(dbias1, dbias0) < 1e-5
