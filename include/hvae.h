@@ -265,6 +265,7 @@ int hvae_anneal_beta(int64_t* anneal_step, double beta_min, double beta_max, int
  *   ks = beta / B or *ks_dev) ; dh = dheads W_heads.
  * Every matrix is row-major and dense (ld = its width); H, L, D multiples of 32, at most 1024. */
 #define HVAE_MLP_ROWS_MAX_NB 1024
+struct hvae_adam;  /* below: the Adam hyperparameters (hvae_adam) */
 typedef struct hvae_mlp_rows {
   int64_t nb, H, L, D;
   const float* W_heads; const float* b_heads; /* [2L, H], [2L] */
@@ -304,6 +305,12 @@ typedef struct hvae_mlp_rows {
    * reads enc_x, w1t, b1, ln_w, ln_b, enc_drop_mult; writes h (as h_out), xhat and rstd; NULL: h is an input */
   const hvae_csr_batch* enc_x;
   const float* w1t; const float* b1;
+  /* forward with enc_x, optional: w1t read through exact lazy Adam -- each entry's row is brought from its
+   * last_step stamp to *adam->step_dev steps in registers (hvae_adam_lazy_catchup_csr's replay, nothing stored:
+   * the step's hvae_adam_lazy replays p, m and v itself), so no catch-up launch has to precede the forward;
+   * adam == NULL: w1t is read as it is */
+  const struct hvae_adam* adam;
+  const float* adam_m; const float* adam_v; const int32_t* last_step; const float* adam_tab;
 } hvae_mlp_rows;
 int hvae_mlp_fwd_rows(const hvae_mlp_rows* a, void* stream);
 int hvae_mlp_bwd_rows(const hvae_mlp_rows* a, void* stream);

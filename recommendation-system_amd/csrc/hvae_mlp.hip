@@ -23,6 +23,7 @@
 #include "hvae_common.h"
 #include "hvae_rgplan.h"
 #include "hvae_encoder_row.h"
+#include "hvae_adam.h"
 
 namespace hvae {
 
@@ -62,7 +63,60 @@ struct MlpP {
   const int64_t* e_rows_offset;
   const float* enc_w1t; const float* enc_b1;
   float* h_out; float* xhat_out; float* rstd_out;
+  // forward: w1t through exact lazy Adam (enc_lazy): rows replayed to *aa.step_dev steps in registers
+  int enc_lazy;
+  AdamArgs aa;
+  const float* am; const float* av; const int32_t* ls; const float2* atab;
 };
+
+// The fused encoder layer's share of wave `sub` of row b with W1t read through lazy Adam: each entry's (p, m, v)
+// row and stamp are loaded (two entries in flight) and p is brought to `to` steps by col_math_lazy -- the float
+// operations of the CSR catch-up -- before x p is added; nothing is stored
+template <int NV>
+__device__ __forceinline__ void encoder_row_partial_lazy(const MlpP& p, int64_t b, int H, int sub, int nsub, int to,
+                                                         float4 (&acc)[NV]) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = batch_row(p.e_rows, p.e_rows_offset, b);
+  const int64_t beg = p.e_row_ptr[r], end = p.e_row_ptr[r + 1];
+  const int64_t H4 = H / 4;
+  const AdamK none{};
+#pragma unroll
+  for (int k = 0; k < NV; ++k) acc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+  constexpr int EU = 2;
+  for (int64_t e0 = beg + sub; e0 < end; e0 += EU * (int64_t)nsub) {
+    int64_t j[EU];
+    float x[EU];
+    int32_t st[EU];
+    bool ok[EU];
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      const int64_t e = e0 + (int64_t)u * nsub;
+      ok[u] = e < end;
+      j[u] = ok[u] ? p.e_col_idx[e] : 0;
+      x[u] = ok[u] ? p.e_vals[e] : 0.f;
+      st[u] = ok[u] ? p.ls[j[u]] : to;
+    }
+    ColState cs[EU][NV];
+#pragma unroll
+    for (int u = 0; u < EU; ++u)
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const int64_t c4 = lane + 64 * k;
+        if (ok[u] && c4 < H4) cs[u][k] = col_load(p.enc_w1t, p.am, p.av, j[u] * H4 + c4);
+      }
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      if (!ok[u]) continue;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (lane + 64 * k >= H4) continue;
+        col_math_lazy(p.aa, p.atab, cs[u][k], ls_mv(st[u]), ls_p(st[u]), to, false, none, make_float4(0.f, 0.f, 0.f, 0.f));
+        acc[k].x += x[u] * cs[u][k].p.x; acc[k].y += x[u] * cs[u][k].p.y;
+        acc[k].z += x[u] * cs[u][k].p.z; acc[k].w += x[u] * cs[u][k].p.w;
+      }
+    }
+  }
+}
 
 __device__ __forceinline__ float dot4(float4 w, float4 x, float acc) {
   acc = fmaf(w.x, x.x, acc);
@@ -272,8 +326,11 @@ __global__ void __launch_bounds__(kMlpThreads) k_mlp_fwd_rows(MlpP p) {
     auto part = [&](auto nv) {
       constexpr int NV = decltype(nv)::value;
       float4 acc[NV];
-      encoder_row_partial<NV>(p.e_row_ptr, p.e_col_idx, p.e_vals, p.e_rows, p.e_rows_offset, b, p.enc_w1t, H, sub,
-                              WPR, acc);
+      if (p.enc_lazy)
+        encoder_row_partial_lazy<NV>(p, b, H, sub, WPR, (int)load_step(p.aa.step_dev), acc);
+      else
+        encoder_row_partial<NV>(p.e_row_ptr, p.e_col_idx, p.e_vals, p.e_rows, p.e_rows_offset, b, p.enc_w1t, H, sub,
+                                WPR, acc);
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         const int c = 4 * (lane + 64 * k);
@@ -586,6 +643,13 @@ static int mlp_setup(const hvae_mlp_rows* a, bool fwd, MlpP& p) {
       p.enc_w1t = a->w1t; p.enc_b1 = a->b1; p.ln_w = a->ln_w; p.ln_b = a->ln_b; p.enc_drop_mult = a->enc_drop_mult;
       p.h_out = const_cast<float*>(a->h); p.xhat_out = const_cast<float*>(a->xhat);
       p.rstd_out = const_cast<float*>(a->rstd);
+      if (a->adam) {
+        HVAE_REQUIRE(a->adam->step_dev && a->adam_m && a->adam_v && a->last_step && a->adam_tab && a->H % 4 == 0,
+                     "hvae_mlp_fwd_rows: lazy-Adam reads need adam (step_dev), adam_m, adam_v, last_step, adam_tab");
+        p.enc_lazy = 1;
+        p.aa = to_args(a->adam);
+        p.am = a->adam_m; p.av = a->adam_v; p.ls = a->last_step; p.atab = (const float2*)a->adam_tab;
+      }
     }
   } else {
     HVAE_REQUIRE(a->dU && a->p1 && a->heads && a->dp1 && a->dheads && a->dh, "hvae_mlp_bwd_rows: null buffer");

@@ -85,6 +85,7 @@ class MlpRows(C.Structure):  # hvae_mlp_rows
         ("ln_w", vp), ("ln_b", vp), ("xhat", vp), ("rstd", vp), ("enc_drop_mult", vp), ("enc_layer", u32),
         ("da", vp), ("d_ln_w", vp), ("d_ln_b", vp), ("d_bias", vp), ("ws", vp), ("ws_bytes", sz),
         ("enc_x", C.POINTER(CsrBatch)), ("w1t", vp), ("b1", vp),
+        ("adam", C.c_void_p), ("adam_m", vp), ("adam_v", vp), ("last_step", vp), ("adam_tab", vp),
     ]
 
 

@@ -282,6 +282,8 @@ class FusedTrainer:
         # the row-parallel MLP backward's LayerNorm column sums finished by the weight-gradient launch
         # (HVAE_LN_COLS_DEFERRED=0: in the backward launch, a last-block reduction)
         self.ln_cols_deferred = bool(int(os.environ.get("HVAE_LN_COLS_DEFERRED", "1")))
+        # small batches: the fused encoder layer reads W1t through lazy Adam (HVAE_ENC_LAZY_READ=0: a catch-up launch)
+        self.enc_lazy_read = bool(int(os.environ.get("HVAE_ENC_LAZY_READ", "1")))
         self.ones = torch.ones(1024, dtype=torch.float32, device=device)
         self.boff = torch.zeros(1, dtype=torch.int64, device=device)
         self.norm = torch.zeros(1, device=device)
@@ -515,6 +517,10 @@ class FusedTrainer:
         plan_in_rows = (train and not dp and self.side is None and self.plan_in_rows and self._mlp_rows_ok(B)
                         and not (self.plan_stream is not None and B >= self.plan_side_min_batch)
                         and bf.rg.struct.cap <= _lib.PLAN_SMALL_CAP and B <= _lib.PLAN_SMALL_CAP)
+        # one hidden layer of H <= 512 with the row-parallel MLP: the encoder layer runs in hvae_mlp_fwd_rows, which
+        # can read W1t through lazy Adam itself (rows replayed in registers), so no catch-up launch precedes it
+        fused_enc = self._mlp_rows_ok(B) and len(H) == 1 and H[0] <= 512
+        enc_lazy = train and not dp and self.lazy_adam and self.enc_lazy_read and fused_enc
         anneal = self._anneal if train else None
         beta_dev = None
         if anneal is not None:  # this step's (beta, beta / B) from the device schedule counter, which it advances
@@ -543,7 +549,7 @@ class FusedTrainer:
         elif train and self.plan_stream is not None and B >= self.plan_side_min_batch:
             # the batch's W1t rows replay their deferred steps (found from the CSR) before the forward reads
             # them, while the row-gradient plan runs on the plan stream
-            if self.lazy_adam:
+            if self.lazy_adam and not enc_lazy:
                 cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
                 check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
                                                     ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
@@ -557,7 +563,7 @@ class FusedTrainer:
         elif train and plan_in_rows:
             # the plan runs as one more block of the row-parallel MLP forward's launch (hvae_mlp_fwd_rows); the
             # batch's W1t rows replay their deferred steps, found from the CSR, before the encoder reads them
-            if self.lazy_adam:
+            if self.lazy_adam and not enc_lazy:
                 cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
                 check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
                                                     ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
@@ -566,7 +572,7 @@ class FusedTrainer:
             self._fork(main, side)
             check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), st2),
                   "w1_rowgrad_plan")
-            if self.lazy_adam:  # the batch's W1t rows replay their deferred steps before the forward reads them
+            if self.lazy_adam and not enc_lazy:  # the batch's W1t rows replay their deferred steps before the forward
                 cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
                 check(L_.hvae_adam_lazy_catchup(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
                                                 ptr(self.v), ptr(self.last_step), bf.rg.ref, lay.n_items, H[0],
@@ -581,6 +587,11 @@ class FusedTrainer:
             rows.enc_x, rows.w1t, rows.b1 = C.pointer(csr), ptr(self.w1t), ptr(self.P["encoder.0.bias"])
             rows.ln_w, rows.ln_b = ptr(self.P["encoder.1.weight"]), ptr(self.P["encoder.1.bias"])
             rows.enc_drop_mult, rows.xhat, rows.rstd = ptr(encm[0]), ptr(bf.xhat[0]), ptr(bf.rstd[0])
+            if enc_lazy:
+                self._enc_adam = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
+                rows.adam = C.addressof(self._enc_adam)
+                rows.adam_m, rows.adam_v = ptr(self.m_w1t), ptr(self.v_w1t)
+                rows.last_step, rows.adam_tab = ptr(self.last_step), ptr(self.adam_tab)
         else:
             check(L_.hvae_encoder_fwd(csr_ref, ptr(self.w1t), ptr(self.P["encoder.0.bias"]),
                                       ptr(self.P["encoder.1.weight"]), ptr(self.P["encoder.1.bias"]), H[0], p_drop,
