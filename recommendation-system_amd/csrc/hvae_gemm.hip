@@ -44,13 +44,19 @@ constexpr int kRegStages = 12;  // k-tiles a block keeps in flight at once (K pe
 // lookahead at that occupancy (MFMA busy 27 %, profiles/r04_pmc_sq_gemm_syn10m_summary.txt).
 constexpr int kRingStages = 4;
 // The 4-tile ring pays for the x W^T products (row-major A, B^T: the forward layers, K = d = 768: 4096x768x768
-// 77 -> 68 us); the [k][n] B of the x W data gradients ran slower on it (4096x768x768 79 -> 82 us), so those keep
-// one tile of lookahead (profiles/r04_gemm_ring_shapes.jsonl).
+// 77 -> 68 us); the [k][n] B of the x W data gradients ran slower on it (4096x768x768 79 -> 82 us), and run on a
+// one-stage instance (NST = 1: one tile of lookahead, 83 VGPRs instead of the 12-stage instance's 221, and every
+// fragment of a k-tile read before its MFMAs): 4096x768x768 79.98 -> 67.72 us (profiles/r04u_gemm_nn1_ab.jsonl).
 static int nst_class(bool ta, bool tb, int64_t kps) {
   const int64_t n = (kps + GBK - 1) / GBK;
   if (n <= kRingStages) return kRingStages;
   if (n <= kRegStages) return kRegStages;
-  return (!ta && tb) ? kRingStages : kRegStages;
+  if (!ta && tb) {
+    const char* t = ab_getenv("HVAE_GEMM_NT1");  // A/B: x W^T long k on the one-stage instance too
+    return t && std::atoi(t) == 1 ? 1 : kRingStages;
+  }
+  const char* e = ab_getenv("HVAE_GEMM_NN1");
+  return e && std::atoi(e) == 0 ? kRegStages : 1;
 }
 
 struct EpiArgs {
@@ -386,6 +392,35 @@ __device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned
     }
   };
 
+  // the long-k loop's stage: every fragment of the k-tile read before its MFMAs (the LDS latency once per tile
+  // instead of once per 4 MFMAs behind an lgkmcnt(0)), used where the instantiation leaves the registers (NST = 1)
+  auto compute_pf = [&](int buf) {
+    const float* a_ = sA(buf);
+    const float* b_ = sB(buf);
+    auto a_at = [&](int m, int k) -> float { return TA ? a_[k * TAo::SK + m] : a_[m * GSR + k]; };
+    auto b_at = [&](int k, int n) -> float { return TB ? b_[n * GSR + k] : b_[k * TBo::SK + n]; };
+    if (do_rowsum && t < BM) {
+#pragma unroll
+      for (int k = 0; k < GBK; ++k) rowsum += a_at(t, k);
+    }
+    float af[GBK / 4][IM], bfr[GBK / 4][JN];
+#pragma unroll
+    for (int kk = 0; kk < GBK / 4; ++kk) {
+      const int kr = 4 * kk + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < IM; ++i) af[kk][i] = a_at(wm + i * 16 + (lane & 15), kr);
+#pragma unroll
+      for (int j = 0; j < JN; ++j) bfr[kk][j] = b_at(kr, wn + j * 16 + (lane & 15));
+    }
+#pragma unroll
+    for (int kk = 0; kk < GBK / 4; ++kk)
+#pragma unroll
+      for (int i = 0; i < IM; ++i)
+#pragma unroll
+        for (int j = 0; j < JN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+  };
+
   const int64_t nst = (ke > kb) ? (ke - kb + GBK - 1) / GBK : 0;
   if (nst > 0 && nst <= NST) {
     // short k range (the batch-sized GEMMs of the path): every global load of the block is issued
@@ -413,7 +448,8 @@ __device__ __forceinline__ void gemm_block(const GemmP& g, unsigned bx, unsigned
     for (int64_t k0 = kb; k0 < ke; k0 += GBK) {
       const bool more = k0 + GBK < ke;
       if (more) gload(k0 + GBK, ra, rb);
-      compute(buf);
+      if (NST == 1) compute_pf(buf);
+      else compute(buf);
       if (more) {
         lstore(buf ^ 1, ra, rb);
         __syncthreads();
@@ -912,9 +948,11 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
   const int nstc = nst_class(trans_a, trans_b, g.kps);
 #define HVAE_GEMM_CALL(TA_, TB_)                                                                  \
   (bt == 64 ? (nstc == kRegStages ? (k_gemm_f32<TA_, TB_, 64, 64, kRegStages><<<grid, 256, 0, st>>>(g))  \
-                                  : (k_gemm_f32<TA_, TB_, 64, 64, kRingStages><<<grid, 256, 0, st>>>(g))) \
+               : nstc == 1 ? (k_gemm_f32<TA_, TB_, 64, 64, 1><<<grid, 256, 0, st>>>(g))                   \
+                           : (k_gemm_f32<TA_, TB_, 64, 64, kRingStages><<<grid, 256, 0, st>>>(g)))        \
             : (nstc == kRegStages ? (k_gemm_f32<TA_, TB_, 32, 32, kRegStages><<<grid, 256, 0, st>>>(g))  \
-                                  : (k_gemm_f32<TA_, TB_, 32, 32, kRingStages><<<grid, 256, 0, st>>>(g))))
+               : nstc == 1 ? (k_gemm_f32<TA_, TB_, 32, 32, 1><<<grid, 256, 0, st>>>(g))                   \
+                           : (k_gemm_f32<TA_, TB_, 32, 32, kRingStages><<<grid, 256, 0, st>>>(g))))
   if (!trans_a && !trans_b) HVAE_GEMM_CALL(false, false);
   else if (!trans_a && trans_b) HVAE_GEMM_CALL(false, true);
   else if (trans_a && !trans_b) HVAE_GEMM_CALL(true, false);
@@ -957,10 +995,11 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
     }
     const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
     ProbeScope probe("gemm", st);
-    const bool r1 = nst_class(false, false, g1.kps) == kRegStages;
+    const int c1 = nst_class(false, false, g1.kps);
 #define HVAE_MIXED(F0_, BT1_)                                                                            \
-  (r1 ? (k_gemm_mixed_pair<F0_, BT1_, kRegStages><<<nblk, 256, 0, st>>>(g0, g1))                         \
-      : (k_gemm_mixed_pair<F0_, BT1_, kRingStages><<<nblk, 256, 0, st>>>(g0, g1)))
+  (c1 == kRegStages ? (k_gemm_mixed_pair<F0_, BT1_, kRegStages><<<nblk, 256, 0, st>>>(g0, g1))           \
+   : c1 == 1 ? (k_gemm_mixed_pair<F0_, BT1_, 1><<<nblk, 256, 0, st>>>(g0, g1))                           \
+             : (k_gemm_mixed_pair<F0_, BT1_, kRingStages><<<nblk, 256, 0, st>>>(g0, g1)))
     if (f0.bm == 64 && bt1 == 64) HVAE_MIXED(64, 64);
     else if (f0.bm == 64) HVAE_MIXED(64, 32);
     else if (bt1 == 64) HVAE_MIXED(32, 64);
@@ -971,7 +1010,8 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
   }
   const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
   ProbeScope probe("gemm", st);
-  const bool q0 = nst_class(true, false, g0.kps) == kRegStages, q1 = nst_class(false, false, g1.kps) == kRegStages;
+  // (the register-staged pair keeps two classes: long k ranges on the kRegStages instance's one-tile lookahead)
+  const bool q0 = nst_class(true, false, g0.kps) != kRingStages, q1 = nst_class(false, false, g1.kps) != kRingStages;
 #define HVAE_PAIR(B0_, B1_)                                                                              \
   (q0 ? (q1 ? (k_gemm_f32_pair<B0_, B1_, kRegStages, kRegStages><<<nblk, 256, 0, st>>>(g0, g1))          \
             : (k_gemm_f32_pair<B0_, B1_, kRegStages, kRingStages><<<nblk, 256, 0, st>>>(g0, g1)))        \
