@@ -51,10 +51,9 @@ static int nst_class(bool ta, bool tb, int64_t kps) {
   const int64_t n = (kps + GBK - 1) / GBK;
   if (n <= kRingStages) return kRingStages;
   if (n <= kRegStages) return kRegStages;
-  if (!ta && tb) {
-    const char* t = ab_getenv("HVAE_GEMM_NT1");  // A/B: x W^T long k on the one-stage instance too
-    return t && std::atoi(t) == 1 ? 1 : kRingStages;
-  }
+  // (x W^T long k on the one-stage instance measured equal to the ring, and fragment prefetch on the short-k
+  // paths changed nothing: profiles/r04v_gemm_prefetch_ab.jsonl)
+  if (!ta && tb) return kRingStages;
   const char* e = ab_getenv("HVAE_GEMM_NN1");
   return e && std::atoi(e) == 0 ? kRegStages : 1;
 }
