@@ -57,6 +57,9 @@ PEAK_HBM_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md, spec)
 PEAK_BF16_TFLOPS = 2500.0  # dense bf16 MFMA
 PEAK_FP8_TFLOPS = 5000.0   # dense fp8 (block-scaled e4m3) MFMA
 PEAK_F32_TFLOPS = 157.3    # f32 MFMA = f32 vector rate
+# L2-served fills into LDS with every CU streaming: 16.8-18.8 TB/s (MI355X_MICROARCH.md, 'Indexed rows: gather into
+# LDS', rows shared by every workgroup); the upper end, so a fraction against it is not flattering
+PEAK_L2_LDS_GBS = 18800.0
 
 
 def log(*a):
@@ -196,11 +199,23 @@ def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int,
     dec_flops = 4.0 * B * N * D
     dec_bytes = {"bf16": 2.0, "fp8": 1.0, "fp32": 4.0}[precision] * N * D + 8.0 * B * D
     dec_peak = {"bf16": PEAK_BF16_TFLOPS, "fp8": PEAK_FP8_TFLOPS, "fp32": PEAK_F32_TFLOPS}[precision]
+    # the second bound of the sweep: every user block streams the whole image from L2 into LDS (the users that
+    # share an E tile: hvae_decoder_users_per_tile), against the L2-served LDS-fill rate
+    from hvae import _lib as L
+    upt = int(L.lib().hvae_decoder_users_per_tile({"bf16": L.HVAE_BF16, "fp8": L.HVAE_FP8, "fp32": L.HVAE_F32}[precision],
+                                                  B, N, D))
+    img = {"bf16": 2.0, "fp8": 1.0, "fp32": 4.0}[precision] * N * D
+    t_dec = kernels["decoder_sweep"][0]
+    l2 = None
+    if upt > 0 and t_dec > 0:
+        l2b = -(-B // upt) * img
+        l2 = {"bound": "l2_lds", "users_per_tile": upt, "bytes_per_launch": l2b, "achieved": l2b / t_dec / 1e9,
+              "peak": PEAK_L2_LDS_GBS, "unit": "GB/s", "frac": round(l2b / t_dec / 1e9 / PEAK_L2_LDS_GBS, 4)}
     if dec_flops / (dec_peak * 1e12) >= dec_bytes / (PEAK_HBM_GBS * 1e9):
-        put("decoder_sweep", "mfma", dec_flops, dec_peak, "TFLOP/s")
+        put("decoder_sweep", "mfma", dec_flops, dec_peak, "TFLOP/s", l2_lds=l2)
     else:
-        put("decoder_sweep", "hbm", dec_bytes, PEAK_HBM_GBS, "GB/s",
-            tflops=round(dec_flops / kernels["decoder_sweep"][0] / 1e12, 3) if kernels["decoder_sweep"][0] else None)
+        put("decoder_sweep", "hbm", dec_bytes, PEAK_HBM_GBS, "GB/s", l2_lds=l2,
+            tflops=round(dec_flops / t_dec / 1e12, 3) if t_dec else None)
     n_gemm = max(kernels["gemm"][1], 1)
     # batches <= 1024 run the latent / projection forward and data gradients in the row-parallel MLP launches
     # (hvae_mlp_*_rows); their GEMM launches are the weight gradients only (one third of the flops)
@@ -224,8 +239,8 @@ def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int,
         R = 1 if B <= 32 else 2 if B <= 512 else 4
         wbytes = 4.0 * (2 * Lt * H + D * Lt + D * D) * -(-B // R)
         enc = 4.0 * nnz * H if len(w["hidden"]) == 1 and H <= 512 else 0.0
-        put("mlp_fwd", "l2", wbytes + enc, None, "GB/s")
-        put("mlp_bwd", "l2", wbytes, None, "GB/s")
+        put("mlp_fwd", "l2", wbytes + enc, PEAK_L2_LDS_GBS, "GB/s")
+        put("mlp_bwd", "l2", wbytes, PEAK_L2_LDS_GBS, "GB/s")
     return out
 
 
@@ -303,7 +318,6 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     run(args.steps)
-    t_enq = time.perf_counter() - t0  # host time to enqueue the K graph replays (== elapsed when host-bound)
     torch.cuda.synchronize()
     if group is not None:
         torch.distributed.barrier()
@@ -337,8 +351,8 @@ def main():
     fused.use_graphs = True
     roof = roofline_models(w, args.precision, B, fused, X, users, rank, kernels)
     # the dominant kernel family: the largest per-step total (average launch x launches per step) among the
-    # families with an algorithmic model
-    # (the row-parallel MLP launches stream weights from L2 and have no HBM / MFMA peak: reported, not dominant)
+    # families with an algorithmic model (the row-parallel MLP launches against the L2-served rate their weight
+    # streams are read at)
     dom = max((k for k in roof if roof[k]["peak"]), key=lambda k: kernels[k][0] * max(kernels[k][1], 1))
     r = roof[dom]
     traffic, stale = None, None
@@ -357,6 +371,8 @@ def main():
                 "frac": round(r["achieved"] / r["peak"], 4), "traffic": traffic, "kernel": dom,
                 "avg_launch_us": round(r["avg_launch_us"], 2),
                 "alg_per_launch": r["alg_per_launch"]}
+    if r.get("l2_lds"):  # the sweep's second bound: L2 -> LDS bytes of its user blocks
+        roofline["l2_lds"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in r["l2_lds"].items()}
     if stale:
         roofline["traffic_stale"] = stale
     launch_us = {k: {"avg_us": round(v[0] * 1e6, 2), "launches_per_step": v[1],
@@ -375,7 +391,6 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
-            "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,

@@ -138,6 +138,10 @@ typedef struct hvae_rowgrad {
   double* rowsq;        /* [cap, HVAE_ROWSQ_PARTS] or NULL: partial sums over h */
                         /*       of rows[s, h]^2 (fp64), written by the apply   */
                         /*       with each row, so the clip reads 128 B per row */
+                        /*       instead of the row. Non-NULL ONLY when         */
+                        /*       hvae_w1_rowgrad_apply produced `rows`: a      */
+                        /*       caller that writes rows itself passes NULL,   */
+                        /*       or the clip adds stale sums                   */
                         /*       instead of 4 H                                 */
 } hvae_rowgrad;
 /* Scratch the row gather needs for hidden width H (chunk partials, and the
@@ -355,6 +359,10 @@ int hvae_decoder_fwd(int dtype, const float* U, int64_t ldu, const void* E, cons
                      int64_t nb, int64_t N, int64_t D, float* lse, float* O, void* ws,
                      size_t ws_bytes, void* stream);
 size_t hvae_decoder_workspace(int dtype, int64_t nb, int64_t N, int64_t D);
+/* Users that share one E tile in LDS in the sweep hvae_decoder_fwd / _train plan for (dtype, nb, N, D): every
+ * user block streams all of E from L2 into LDS once, so a sweep moves ceil(nb / this) x the image bytes
+ * (the L2 -> LDS bound the bench reports beside the MFMA one). Informational; 0 for bad arguments. */
+int64_t hvae_decoder_users_per_tile(int dtype, int64_t nb, int64_t N, int64_t D);
 /* 1 if this build has a streaming decoder kernel for (dtype, D). */
 int hvae_decoder_supported(int dtype, int64_t D);
 /* *out = max_i ||E_i||_2 of an fp32 / bf16 [N, D] matrix (computed once: E is frozen). */

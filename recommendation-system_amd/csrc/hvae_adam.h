@@ -50,6 +50,29 @@ __device__ __forceinline__ void adam_elem0(float& p, float& m, float& v, const A
   p = p - k.lr_over_bc1 * (m * __builtin_amdgcn_rcpf(denom));
 }
 
+// torch.optim.Adam as the reference's optimizer evaluates it on the CPU (src/ml/train.py:63 -> torch/optim/adam.py
+// _single_tensor_adam), operation for operation, for the eager drop-in step (hvae_adam_dense: the fused trainer's
+// optimizer.step() and ModuleAdam): grad.add(param, alpha = wd) = fma(wd, p, g), exp_avg.lerp_ = fma(1 - b1,
+// g - m, m) and addcmul_ = fma((1 - b2) g, g, v b2) -- the contractions torch's vectorised CPU kernels make,
+// probed against torch 2.10's CPU Adam -- then denom = sqrt(v) / bias_correction2_sqrt + eps and
+// param.addcdiv_(m, denom, -step_size) = p + ((-step_size) m) / denom, with the correctly rounded square root
+// and divisions. The only difference left is torch's own CPU sqrt, which is not correctly rounded (AVX-512
+// build: 1 ulp off in ~0.7 % of elements), so on the same inputs p, m, v agree bitwise except where it rounds
+// differently (tests/test_gpu_api.py::test_adam_dense_matches_torch_cpu).
+struct AdamKExact {
+  float neg_step_size;  // -(lr / (1 - b1^t)), rounded to fp32 as addcdiv_'s value is
+  float bc2_sqrt;       // sqrt(1 - b2^t)
+  float omb1, b2, omb2, eps, wd;
+};
+__device__ __forceinline__ void adam_elem_exact(float& p, float& m, float& v, float g, const AdamKExact& k) {
+#pragma clang fp contract(off)
+  if (k.wd != 0.f) g = __builtin_fmaf(k.wd, p, g);
+  m = __builtin_fmaf(k.omb1, g - m, m);
+  v = __builtin_fmaf(k.omb2 * g, g, v * k.b2);
+  const float denom = sqrtf(v) / k.bc2_sqrt + k.eps;  // correctly rounded: hipcc's default
+  p = p + (k.neg_step_size * m) / denom;              // -fhip-fp32-correctly-rounded-divide-sqrt
+}
+
 // the m, v half of adam_elem0 / adam_elem at g = 0 (wd only enters through g, which m and v see as
 // g + wd p: with wd != 0 a p-only replay is not possible, and the CSR catch-up does not use it then)
 __device__ __forceinline__ void adam_mv0(float& m, float& v, const AdamK& k) {
@@ -73,6 +96,21 @@ struct AdamArgs {
   const int64_t* step_dev;
   const float* coef_dev;
 };
+
+__device__ __forceinline__ AdamKExact adam_consts_exact(const AdamArgs& a) {
+  const int64_t t = load_step(a.step_dev) + 1;
+  const double bc1 = 1.0 - pow(a.b1, (double)t);
+  const double bc2 = 1.0 - pow(a.b2, (double)t);
+  AdamKExact k;
+  k.neg_step_size = (float)(-(a.lr / bc1));
+  k.bc2_sqrt = (float)sqrt(bc2);
+  k.omb1 = (float)(1.0 - a.b1);
+  k.b2 = (float)a.b2;
+  k.omb2 = (float)(1.0 - a.b2);
+  k.eps = (float)a.eps;
+  k.wd = (float)a.wd;
+  return k;
+}
 
 __device__ __forceinline__ AdamK adam_consts(const AdamArgs& a) {
   const int64_t t = load_step(a.step_dev) + 1;

@@ -34,6 +34,7 @@
 #include <type_traits>
 
 #include "hvae_common.h"
+#include "hvae_dec6.h"
 
 namespace hvae {
 
@@ -2575,6 +2576,8 @@ struct FinArgs {
   float* lse_out; float* O_out; float* recon_rows; float* dU;
   const float* kl_rows; float beta; const float* beta_dev; float* loss3; double* accum3;  // fused loss (optional)
   unsigned* ticket;
+  // version-6 partials (hvae_dec6.h): user b's slots are dec6_slot_of(.., b / v6_upb, i), rows slot * v6_upb + b % v6_upb
+  int v6_upb, v6_nub, v6_S, v6_main, v6_P;
 };
 
 constexpr int kFinEB = 16;  // CSR entries per batch of the finalize's sparse-term loads
@@ -2611,12 +2614,21 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   __syncthreads();
   float lse_b;
   float o[4] = {0.f, 0.f, 0.f, 0.f};
-  if (a.splits > 1) {
+  int nsp = a.splits;
+  const int v6u = a.v6_upb ? (int)(b / a.v6_upb) : 0;
+  const int64_t v6j = a.v6_upb ? b % a.v6_upb : 0;
+  if (a.v6_upb) nsp = dec6_nslots(a.v6_nub, a.v6_S, a.v6_main, a.v6_P, v6u);
+  auto prow = [&](int s) -> int64_t {  // partial row of user b's s-th split / slot
+    return a.v6_upb ? (int64_t)dec6_slot_of(a.v6_nub, a.v6_S, a.v6_main, a.v6_P, v6u, s) * a.v6_upb + v6j
+                    : (int64_t)s * a.nb + b;
+  };
+  if (a.splits > 1 || a.v6_upb) {
     float M = -INFINITY;
     int fl = 0;
-    for (int s = tid; s < a.splits; s += 256) {
-      M = fmaxf(M, a.pm[(int64_t)s * a.nb + b]);
-      if (a.flag) fl |= a.flag[(int64_t)s * a.nb + b];
+    for (int s = tid; s < nsp; s += 256) {
+      const int64_t r = prow(s);
+      M = fmaxf(M, a.pm[r]);
+      if (a.flag) fl |= a.flag[r];
     }
     if (fl) any_flag = 1;
     M = wave_max(M);
@@ -2624,11 +2636,12 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     __syncthreads();
     M = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
     float L = 0.f;
-    for (int s = tid; s < a.splits; s += 256) {
-      const float ms = a.pm[(int64_t)s * a.nb + b];
+    for (int s = tid; s < nsp; s += 256) {
+      const int64_t r = prow(s);
+      const float ms = a.pm[r];
       const float wv = (ms == -INFINITY) ? 0.f : __expf(ms - M);
       wsh[s] = wv;
-      L += wv * a.pl[(int64_t)s * a.nb + b];
+      L += wv * a.pl[r];
     }
     L = block_sum<256>(L, red);  // its barriers also publish wsh and any_flag
     lse_b = M + logf(L);
@@ -2637,25 +2650,28 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
       // sum_s w_s O_s in split order; loads batched 8 splits x 4 columns deep so that
       // they are in flight together (a one-at-a-time chain is HBM-latency bound)
       const int nk = (int)min<int64_t>(4, (D - tid + 255) / 256);
-      const int64_t sstride = a.nb * D;
-      const float* base = a.pO + b * D + tid;
+      const float* base = a.pO + tid;
       float acc[4] = {0.f, 0.f, 0.f, 0.f};
       int s0 = 0;
-      for (; s0 + 8 <= a.splits; s0 += 8) {
+      for (; s0 + 8 <= nsp; s0 += 8) {
         float v[8][4];
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < 8; ++j) {
+          const float* rp = base + prow(s0 + j) * D;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) v[j][k] = k < nk ? base[(int64_t)(s0 + j) * sstride + 256 * k] : 0.f;
+          for (int k = 0; k < 4; ++k) v[j][k] = k < nk ? rp[256 * k] : 0.f;
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
           for (int k = 0; k < 4; ++k) acc[k] += wsh[s0 + j] * v[j][k];
       }
-      for (; s0 < a.splits; ++s0)
+      for (; s0 < nsp; ++s0) {
+        const float* rp = base + prow(s0) * D;
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          if (k < nk) acc[k] += wsh[s0] * base[(int64_t)s0 * sstride + 256 * k];
+          if (k < nk) acc[k] += wsh[s0] * rp[256 * k];
+      }
 #pragma unroll
       for (int k = 0; k < 4; ++k) o[k] = acc[k] * inv;
     }
@@ -2669,22 +2685,22 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
       float4 acc4[8];
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int s0 = sg; s0 < a.splits; s0 += SG * 4) {
+      for (int s0 = sg; s0 < nsp; s0 += SG * 4) {
         float4 v[4][8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int sj = s0 + SG * j;
-          const float4* row = reinterpret_cast<const float4*>(a.pO + ((int64_t)sj * a.nb + b) * D);
+          const float4* row = reinterpret_cast<const float4*>(a.pO + (sj < nsp ? prow(sj) : 0) * D);
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             const int q = cq + 32 * i;
-            v[j][i] = (sj < a.splits && q < nq) ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[j][i] = (sj < nsp && q < nq) ? row[q] : make_float4(0.f, 0.f, 0.f, 0.f);
           }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int sj = s0 + SG * j;
-          const float wv = sj < a.splits ? wsh[sj] : 0.f;
+          const float wv = sj < nsp ? wsh[sj] : 0.f;
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
             acc4[i].x += wv * v[j][i].x; acc4[i].y += wv * v[j][i].y;
@@ -2899,6 +2915,8 @@ struct DecPlan {
   int v3;    // bf16 version-3 sweep (k_dec3_bf16, D = 768)
   int v4;    // bf16 version-4 sweep (k_dec4_bf16: D = 768 with 4 waves, D = 384 with 8)
   int v5;    // bf16 version-5 sweep (k_dec5_bf16, D = 768: 8 waves, GEMM1 and GEMM2 on different waves)
+  int v6;    // bf16 version-6 sweep (k_dec6_bf16, D = 768: 96 users per E tile, task plan p6)
+  Dec6Plan p6;
   int ds;    // its D split (1 or 2)
   int nw;    // its waves per block (4, or 8 with ds = 2)
   int64_t upb;
@@ -2989,6 +3007,8 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   p.v3 = p.v2 && v3_supported(D);
   p.v4 = (p.v3 && v4_supported(D)) || (p.v2 && v4_384(D, nb));
   p.v5 = p.v4 && v5_supported(D);  // same users per block (64), splits and partial layout as version 4
+  // version 6 (hvae_decoder6.hip) above 64 users: 96 users per E tile; HVAE_DEC_V6=0 (A/B) runs version 5
+  p.v6 = p.v5 && D == 768 && env_int("HVAE_DEC_V6", 1) != 0 && dec6_plan(nb, N, p.p6);
   p.ds = p.v2 && (D > 384 || nb <= 64) ? 2 : 1;
   if (p.v2 && D <= 384 && (dec_forced_ds() == 1 || dec_forced_ds() == 2)) p.ds = dec_forced_ds();
   p.nw = p.v2 && p.ds == 2 && nb > 64 && D <= 384 ? 8 : 4;
@@ -3302,10 +3322,33 @@ extern "C" int hvae_decoder_image(int dtype, const float* E32, int64_t N, int64_
   return HVAE_OK;
 }
 
+// version 6: flags | m | l | O over the slot rows [p6.slots][96], then the O scratch of the other layouts (the
+// workspace also fits version 5's, the fallback when a caller's workspace is short)
+static size_t dec6_ws_bytes(const Dec6Plan& q, int64_t nb, int64_t D) {
+  const size_t rows = (size_t)q.slots * kDec6Users;
+  return (size_t)cdiv((int64_t)(rows * sizeof(int)), 256) * 256 + rows * (2 + (size_t)D) * sizeof(float) +
+         (size_t)nb * D * sizeof(float);
+}
+static size_t plan_ws_bytes(const DecPlan& p, int64_t nb, int64_t D) {
+  const size_t base = dec_ws_bytes(p.splits, nb, D);
+  return p.v6 ? std::max(base, dec6_ws_bytes(p.p6, nb, D)) : base;
+}
+
+extern "C" int64_t hvae_decoder_users_per_tile(int dtype, int64_t nb, int64_t N, int64_t D) {
+  if (nb <= 0 || N <= 0 || D <= 0) return 0;
+  const DecPlan p = dec_plan(dtype, nb, N, D);
+  return p.v6 ? kDec6Users : std::min<int64_t>(p.upb, nb);
+}
+
 extern "C" size_t hvae_decoder_workspace(int dtype, int64_t nb, int64_t N, int64_t D) {
   const DecPlan p = dec_plan(dtype, nb, N, D);
-  return dec_ws_bytes(p.splits, nb, D);
+  return plan_ws_bytes(p, nb, D);
 }
+
+static int decoder_finalize(FinArgs& a, const float* U, int64_t ldu, const void* E, const float* E32,
+                            const hvae_csr_batch* x, int64_t nb, int64_t N, int64_t D, float scale, float* lse,
+                            float* recon_rows, float* dU, const float* kl_rows, float beta, const float* beta_dev,
+                            float* loss3, double* accum3, bool grouped, hipStream_t st);
 
 // flash sweep + finalize; csr / recon_rows / dU optional
 static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
@@ -3336,6 +3379,31 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   }
   const bool bf = dtype != HVAE_F32;  // fixed-offset sweeps (bf16, fp8): flags, bf16 E for the exact fixup
   const bool want_o = O || dU;
+  if (p.v6 && ws_bytes < dec6_ws_bytes(p.p6, nb, D)) p.v6 = 0;
+  FinArgs a{};
+  if (p.v6) {  // version 6: slot-row partials, merged per user by the finalize's slot map
+    const Dec6Plan& q = p.p6;
+    const size_t rows = (size_t)q.slots * kDec6Users;
+    char* w6 = (char*)ws;
+    int* flag6 = (int*)w6;
+    w6 += (size_t)cdiv((int64_t)(rows * sizeof(int)), 256) * 256;
+    float* pm = (float*)w6;
+    float* pl = pm + rows;
+    float* pO = pl + rows;
+    int rc;
+    {
+      ProbeScope probe("decoder_sweep", st);
+      rc = dec6_launch(want_o, U, ldu, E, e_maxnorm, nb, N, q, flag6, pm, pl, want_o ? pO : nullptr, st);
+    }
+    if (rc) return rc;
+    a.splits = q.S;
+    a.pm = pm; a.pl = pl; a.pO = want_o ? pO : nullptr;
+    a.flag = flag6;
+    a.v6_upb = kDec6Users; a.v6_nub = q.nub; a.v6_S = q.S; a.v6_main = q.main; a.v6_P = q.P;
+    a.O_out = O;
+    return decoder_finalize(a, U, ldu, E, E32, x, nb, N, D, scale, lse, recon_rows, dU, kl_rows, beta, beta_dev,
+                            loss3, accum3, q.X > 0 || q.S > 8, st);
+  }
   char* w = (char*)ws;
   DecOut o{};
   o.flag = (int*)w;
@@ -3361,12 +3429,21 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   }
   if (rc) return rc;
   if (p.splits == 1 && !bf && !x) return HVAE_OK;  // fp32 single split: the sweep wrote lse / O already
-  HVAE_REQUIRE(!loss3 || x, "hvae decoder: fused loss needs the batch");
-  FinArgs a{};
   a.splits = p.splits;
   if (p.splits > 1) { a.pm = o.m; a.pl = o.l; a.pO = want_o ? o.O : nullptr; }
   else { a.lse_in = lse; a.O_in = o_scratch; }
   a.flag = bf ? o.flag : nullptr;
+  a.O_out = O ? O : (p.splits == 1 ? o_scratch : nullptr);
+  return decoder_finalize(a, U, ldu, E, E32, x, nb, N, D, scale, lse, recon_rows, dU, kl_rows, beta, beta_dev, loss3,
+                          accum3, p.splits > 8, st);
+}
+
+// the finalize launch of decoder_run (a's partial / direct inputs and O_out set by the caller)
+static int decoder_finalize(FinArgs& a, const float* U, int64_t ldu, const void* E, const float* E32,
+                            const hvae_csr_batch* x, int64_t nb, int64_t N, int64_t D, float scale, float* lse,
+                            float* recon_rows, float* dU, const float* kl_rows, float beta, const float* beta_dev,
+                            float* loss3, double* accum3, bool grouped, hipStream_t st) {
+  HVAE_REQUIRE(!loss3 || x, "hvae decoder: fused loss needs the batch");
   a.U = U; a.ldu = ldu; a.Ebf = (const bf16_t*)E;
   a.E32 = E32; a.N = N; a.D = D; a.nb = nb;
   if (x) {
@@ -3375,7 +3452,6 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   }
   a.scale = scale;
   a.lse_out = lse;
-  a.O_out = O ? O : (p.splits == 1 ? o_scratch : nullptr);
   a.recon_rows = recon_rows;
   a.dU = dU;
   if (loss3) {
@@ -3384,7 +3460,7 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
     if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   }
   ProbeScope probe("decoder_finalize", st);
-  if (p.splits > 8) k_dec_finalize<true><<<(unsigned)nb, 256, 0, st>>>(a);
+  if (grouped) k_dec_finalize<true><<<(unsigned)nb, 256, 0, st>>>(a);
   else k_dec_finalize<false><<<(unsigned)nb, 256, 0, st>>>(a);
   HVAE_LAUNCH_CHECK("k_dec_finalize");
   return HVAE_OK;

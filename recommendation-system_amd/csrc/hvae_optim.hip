@@ -98,12 +98,12 @@ __global__ void __launch_bounds__(256) k_clip_norm(ClipArgs a) {
 __global__ void __launch_bounds__(256) k_adam_dense(AdamArgs a, float* __restrict__ p, float* __restrict__ m,
                                                     float* __restrict__ v, const float* __restrict__ g,
                                                     int64_t n) {
-  const AdamK k = adam_consts(a);
+  const AdamKExact k = adam_consts_exact(a);  // the eager drop-in step: torch's CPU arithmetic (hvae_adam.h)
   const float coef = a.coef_dev ? *a.coef_dev : 1.f;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     float pp = p[i], mm = m[i], vv = v[i];
-    adam_elem(pp, mm, vv, g[i] * coef, k);
+    adam_elem_exact(pp, mm, vv, g[i] * coef, k);
     p[i] = pp; m[i] = mm; v[i] = vv;
   }
 }

@@ -139,6 +139,7 @@ SIGNATURES = {
     "hvae_decoder_image": (cint, [cint, vp, i64, i64, vp, vp]),
     "hvae_decoder_fwd": (cint, [cint, vp, i64, vp, vp, i64, i64, i64, vp, vp, vp, sz, vp]),
     "hvae_decoder_workspace": (sz, [cint, i64, i64, i64]),
+    "hvae_decoder_users_per_tile": (i64, [cint, i64, i64, i64]),
     "hvae_decoder_supported": (cint, [cint, i64]),
     "hvae_row_norm_max": (cint, [cint, vp, i64, i64, vp, vp]),
     "hvae_decoder_bwd": (cint, [P(CsrBatch), vp, i64, vp, i64, vp, vp, f32, vp, vp, vp]),

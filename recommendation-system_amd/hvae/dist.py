@@ -270,6 +270,8 @@ class DPExchange:
         rp.copy_(self.recv[:, self.off_rp:self.off_rp + B + 1].view(torch.int32))
         rp.add_(self.base)
         flat = self.recv.reshape(-1)
+        if self.merge_fn is not _hip_merge and hasattr(self.merged, "rows_from_elsewhere"):
+            self.merged.rows_from_elsewhere()  # no rowsq from an injected merge: the clip reads the rows
         self.merge_fn(self, self.rp_u, flat.view(torch.int32), flat[self.cap:], self.rows_u, W * B, self.recv_da,
                       self.merged)
         return self.merged

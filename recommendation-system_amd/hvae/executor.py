@@ -743,8 +743,11 @@ class FusedTrainer:
         if not self.mlp_rows or not lay.has_proj or B > _lib.MLP_ROWS_MAX_NB:
             return False
         ok = self._mlp_rows_cache.get(B)
-        if ok is None:  # the library's own shape rules (rows per block, LDS of both directions)
-            ok = bool(lib().hvae_mlp_rows_supported(B, lay.hidden[-1], lay.L, lay.d, 0))
+        if ok is None:  # the library's own shape rules (rows per block, LDS of both directions), asked for the
+            # configuration the step launches: the fused encoder layer (one hidden layer of at most 512) needs its
+            # own LDS beside the MLP's
+            fused_enc = int(len(lay.hidden) == 1 and lay.hidden[0] <= 512)
+            ok = bool(lib().hvae_mlp_rows_supported(B, lay.hidden[-1], lay.L, lay.d, fused_enc))
             self._mlp_rows_cache[B] = ok
         return ok
 
@@ -961,9 +964,19 @@ class FusedTrainer:
         dp, W, r = self.dp, self.dp.world, self.dp.rank
         users = data.users_host
         n = len(users)
-        if shuffle:  # one order on every rank: drawn from the shared data-parallel seed, not a per-rank generator
-            rng = np.random.default_rng([self.dp_seed, 0x5EA1, self.dp_val_epoch])
-            self.dp_val_epoch += 1
+        if shuffle:  # one order on every rank
+            if generator is not None:
+                # the caller's generator decides it, as in a single-GPU run: every rank draws (so each
+                # generator advances as the single-GPU one would) and rank 0's draw is broadcast
+                grp = dp.group
+                on_dev = torch.distributed.get_backend(grp) == "nccl"
+                s = torch.randint(0, 2 ** 62, (1,), generator=generator, device=generator.device)
+                s = s.to(self.device if on_dev else "cpu")
+                torch.distributed.broadcast(s, torch.distributed.get_global_rank(grp, 0), group=grp)
+                rng = np.random.default_rng([int(s.item()), 0x5EA1])
+            else:  # the shared data-parallel seed
+                rng = np.random.default_rng([self.dp_seed, 0x5EA1, self.dp_val_epoch])
+                self.dp_val_epoch += 1
             order = users[rng.permutation(n)]
         else:
             order = users

@@ -44,6 +44,12 @@ class Csr:
         self.struct = CsrBatch(ptr(row_ptr), ptr(col_idx), ptr(vals), ptr(rows), ptr(rows_offset), self.nb,
                                self.n_items)
 
+    def rows_from_elsewhere(self):
+        """The rows will be written by something other than the library's row-gradient apply (an injected
+        DPExchange merge_fn): the clip must then read the rows, not the apply's per-row sums of squares
+        (hvae_rowgrad.rowsq, include/hvae.h: non-NULL only where hvae_w1_rowgrad_apply produced the rows)."""
+        self.struct.rowsq = None
+
     @property
     def ref(self):
         return C.byref(self.struct)
@@ -142,6 +148,12 @@ class RowGradBuffers:
                               n_items, ptr(self.contrib_slot), ptr(self.part), self.part.numel(), ptr(self.rowsq))
         self.ws = torch.empty(max(int(lib().hvae_w1_rowgrad_workspace(n_items)), 256), dtype=torch.uint8,
                               device=device)
+
+    def rows_from_elsewhere(self):
+        """The rows will be written by something other than the library's row-gradient apply (an injected
+        DPExchange merge_fn): the clip must then read the rows, not the apply's per-row sums of squares
+        (hvae_rowgrad.rowsq, include/hvae.h: non-NULL only where hvae_w1_rowgrad_apply produced the rows)."""
+        self.struct.rowsq = None
 
     @property
     def ref(self):

@@ -1,0 +1,99 @@
+"""LDS bank-conflict model of the version-6 bf16 sweep (hvae_decoder6.hip, k_dec6_bf16, d = 768) and the
+search that picked its row map and chunk swizzle.
+
+The tile image is version 2's (8-row x 32-column sub-tiles of 512 B per 128-column segment), with a chunk XOR
+swz(r) that is a GF(2)-linear function of the row's low 4 bits (the LDS-DMA writes the image linearly, so the
+swizzle lives on the source side). Reads, per MI355X_MICROARCH.md's LDS table:
+  * GEMM1 A operand (v_mfma_f32_16x16x32_bf16, ds_read_b128): lane (c16, kg) reads image row 16 ib + sigma(c16),
+    16 B at dims 384 h + 32 ks + 8 kg; serviced in 4 groups of 16 lanes;
+  * GEMM2 A operand (E^T, ds_read_b64_tr_b16): lane 16 kg + 4 q + p reads row 16 ib + sigma(4 kg + q), 8 B at
+    dims 16 db + 4 p; serviced in 2 groups of 32 lanes.
+sigma(4 kg + q) = base(kg) + q keeps the 4 rows of a transposed read consecutive (the GEMM1 output rows a lane
+holds are GEMM2's k slots, so both reads share sigma). A group is conflict-free when its lanes touch distinct
+4-byte banks ((addr / 4) mod 64); identical addresses broadcast.
+"""
+import itertools
+import sys
+
+G128 = [list(range(0, 4)) + list(range(12, 16)) + list(range(20, 28)),
+        list(range(4, 12)) + list(range(16, 20)) + list(range(28, 32))]
+G128 = G128 + [[lane + 32 for lane in g] for g in G128]
+G64 = [list(range(32)), list(range(32, 64))]
+
+
+def _worst(groups, addr_of, nbytes):
+    worst = 1
+    for g in groups:
+        banks = {}
+        for lane in g:
+            a = addr_of(lane)
+            for b in range(a // 4, (a + nbytes) // 4):
+                banks.setdefault(b % 64, set()).add(a)
+        worst = max(worst, max(len(v) for v in banks.values()))
+    return worst
+
+
+def swz_of(mask):
+    """2x4 GF(2) matrix (8 bits: row 0 = bits 0..3, row 1 = bits 4..7) -> f(r) on r & 15."""
+    def f(r):
+        b0 = bin((mask & 15) & (r & 15)).count("1") & 1
+        b1 = bin(((mask >> 4) & 15) & (r & 15)).count("1") & 1
+        return b0 | (b1 << 1)
+    return f
+
+
+def image_off(r, d, swz):
+    """Byte offset of E[item r][dim d] in the tile image (d2 layout per 128-column segment)."""
+    s, dd = d // 128, d % 128
+    ch = dd // 8
+    return (s << 13) + ((r >> 3) << 11) + ((ch >> 2) << 9) + ((r & 7) << 6) + (((ch & 3) ^ swz(r)) << 4) + 2 * (d % 8)
+
+
+def sigma_of(bases):
+    return [bases[c >> 2] + (c & 3) for c in range(16)]
+
+
+def gemm1_addr(sigma, swz, h, ib, ks, lane):
+    c16, kg = lane & 15, lane >> 4
+    return image_off(16 * ib + sigma[c16], 384 * h + 32 * ks + 8 * kg, swz)
+
+
+def gemm2_addr(sigma, swz, h, ib, db, lane):
+    kg, q, p = lane >> 4, (lane >> 2) & 3, lane & 3
+    return image_off(16 * ib + sigma[4 * kg + q], 384 * h + 16 * db + 4 * p, swz)
+
+
+def worst_conflicts(bases, mask):
+    sigma, swz = sigma_of(bases), swz_of(mask)
+    w1 = max(_worst(G128, lambda l: gemm1_addr(sigma, swz, h, ib, ks, l), 16)
+             for h in range(2) for ib in range(2) for ks in range(12))
+    w2 = max(_worst(G64, lambda l: gemm2_addr(sigma, swz, h, ib, db, l), 8)
+             for h in range(2) for ib in range(2) for db in range(24))
+    return w1, w2
+
+
+def search():
+    best = None
+    for bases in itertools.permutations((0, 4, 8, 12)):
+        for mask in range(256):
+            f = swz_of(mask)
+            # the XOR must be a function whose values per 8-row group keep each DMA piece's lane -> chunk map a
+            # permutation (any f does: the XOR is applied to the chunk index of a fixed row)
+            w = worst_conflicts(bases, mask)
+            key = (max(w), sum(w))
+            if best is None or key < best[0]:
+                best = (key, bases, mask, w)
+            if w == (1, 1):
+                return bases, mask, w
+    return best[1], best[2], best[3]
+
+
+# the kernel's choice (DEC6_BASES / DEC6_SWZ in hvae_decoder6.hip); test_fp8_layout_cpu.py asserts it is conflict-free
+KERNEL_BASES = (0, 4, 8, 12)
+KERNEL_SWZ = 0x40
+
+if __name__ == "__main__":
+    print("kernel", KERNEL_BASES, hex(KERNEL_SWZ), worst_conflicts(KERNEL_BASES, KERNEL_SWZ))
+    print("search", search())
+    print("version-5 swizzle, natural rows", worst_conflicts((0, 4, 8, 12), 0x84))
+    sys.exit(0)

@@ -58,3 +58,31 @@ def test_gemm_fast_image(R):
     st, rd = gb.worst_conflicts(R, 1)
     assert rd == 1 and st <= 2
     assert gb.worst_conflicts(R, 0) == ((4, 2) if R == 32 else (8, 2))
+
+
+def test_dec6_bf16_reads_conflict_free():
+    """bf16 version-6 sweep (k_dec6_bf16, d = 768): with the image's chunk XOR 2 ((row >> 2) & 1) the GEMM1 row
+    reads (ds_read_b128, 16x16x32 A operand) and the GEMM2 transposed reads (ds_read_b64_tr_b16, E^T, the k slots
+    of a lane group 4 consecutive rows) hit distinct banks in natural row order; version 2's XOR
+    ((row >> 2) & 3) would be 2-way on both."""
+    import check_dec6_banks as d6
+    assert d6.worst_conflicts(d6.KERNEL_BASES, d6.KERNEL_SWZ) == (1, 1)
+    assert d6.worst_conflicts((0, 4, 8, 12), 0x84) == (2, 2)
+
+
+def test_dec6_dma_pieces_cover_the_tile():
+    """Wave w's 12 LDS-DMA pieces of a tile (rows 8 w .. + 7, piece i = 2 seg + half) write every byte of the
+    48-KiB image once, each lane's 16 B the image position of the source chunk it loads."""
+    import check_dec6_banks as d6
+    seen = {}
+    for w in range(4):
+        for i in range(12):
+            lds_base = w * 2048 + (i >> 1) * 8192 + (i & 1) * 1024
+            for lane in range(64):
+                row = 8 * w + ((lane >> 2) & 7)
+                src = 128 * i + 64 * (lane >> 5) + 16 * ((lane & 3) ^ (2 * ((lane >> 4) & 1)))  # bytes in the row
+                d = src // 2  # first dim of the 16-B chunk
+                dst = lds_base + 16 * lane
+                assert dst == d6.image_off(row, d, d6.swz_of(d6.KERNEL_SWZ))
+                seen[dst] = seen.get(dst, 0) + 1
+    assert sorted(seen) == list(range(0, 48 * 1024, 16)) and set(seen.values()) == {1}

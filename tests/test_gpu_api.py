@@ -216,3 +216,52 @@ def test_optimizer_lr_change_reaches_fused_step(hip_device):
         assert t.fused.lr == lr_second
         outs.append(t.fused.flat.clone())
     assert not torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("wd", [0.0, 1e-2])
+def test_adam_dense_matches_torch_cpu(hip_device, wd):
+    """hvae_adam_dense (the eager drop-in step: optimizer.step(), ModuleAdam) evaluates torch.optim.Adam as the
+    reference's CPU build does (hvae_adam.h adam_elem_exact): it equals, bitwise, a float32 restatement of
+    torch/optim/adam.py _single_tensor_adam with the fused multiply-adds of torch's CPU kernels and correctly
+    rounded sqrt / division; against torch's own CPU Adam it agrees bitwise except where torch's CPU sqrt is not
+    correctly rounded (a 1-ulp denominator: p within a few ulp, rare)."""
+    from hvae import ops
+    n, steps = 100_003, 6
+    lr, b1, b2, eps = 1e-3, 0.9, 0.999, 1e-8
+    g = torch.Generator().manual_seed(5)
+    p0 = torch.randn(n, generator=g)
+    grads = [torch.randn(n, generator=g) * 10.0 ** torch.randint(-6, 2, (n,), generator=g).float()
+             for _ in range(steps)]
+    f = np.float32
+
+    def fma(x, y, z):
+        return (np.float64(x) * np.float64(y) + np.float64(z)).astype(f)
+
+    P, M, V = p0.numpy().copy(), np.zeros(n, f), np.zeros(n, f)
+    pt = torch.nn.Parameter(p0.clone())
+    opt = torch.optim.Adam([pt], lr=lr, betas=(b1, b2), eps=eps, weight_decay=wd)
+    pd, md, vd = p0.to(hip_device), torch.zeros(n, device=hip_device), torch.zeros(n, device=hip_device)
+    step_dev = torch.zeros(1, dtype=torch.int64, device=hip_device)
+    for t in range(1, steps + 1):
+        gr = grads[t - 1]
+        pt.grad = gr.clone()
+        opt.step()
+        x = gr.numpy()
+        if wd:
+            x = fma(f(wd), P, x)
+        M = fma(f(1 - b1), (x - M).astype(f), M)
+        V = fma((f(1 - b2) * x).astype(f), x, (V * f(b2)).astype(f))
+        den = ((np.sqrt(V) / f((1 - b2 ** t) ** 0.5)).astype(f) + f(eps)).astype(f)
+        P = (P + ((f(-(lr / (1 - b1 ** t))) * M).astype(f) / den).astype(f)).astype(f)
+        cfg = ops.adam_config(lr, (b1, b2), eps, wd, step_dev, None)
+        ops.adam_dense(cfg, pd, md, vd, gr.to(hip_device))
+        ops.counter_add(step_dev, 1)
+    torch.cuda.synchronize()
+    assert np.array_equal(pd.cpu().numpy(), P) and np.array_equal(md.cpu().numpy(), M)
+    assert np.array_equal(vd.cpu().numpy(), V)
+    st = opt.state[pt]
+    ptv = pt.detach().numpy()
+    frac = float((ptv != P).mean())
+    assert frac < 1e-3, frac
+    assert np.abs(ptv - P).max() <= 4 * np.spacing(np.abs(P).max())
+    assert float((st["exp_avg"].numpy() != M).mean()) < 1e-3 and float((st["exp_avg_sq"].numpy() != V).mean()) < 1e-3

@@ -223,6 +223,9 @@ def _global_worker(rank, world, port, q):
         r = [fused.run_epoch(data, 32, True, ConstBeta(0.2), 0.3) for _ in range(3)]
         # shuffled sharded validation: the order comes from the shared seed, so both ranks deal the same batches
         r.append(fused.run_epoch(data, 32, True, ConstBeta(0.2), 0.3, train=False))
+        # with a caller's generator (seeded differently per rank) the order is rank 0's draw, broadcast
+        gen = torch.Generator().manual_seed(100 + rank)
+        r.append(fused.run_epoch(data, 32, True, ConstBeta(0.2), 0.3, train=False, generator=gen))
         torch.cuda.synchronize()
         q.put((rank, r, fused.flat.cpu().numpy(), int(fused.step_dev.item())))
         dist.barrier()
@@ -251,6 +254,7 @@ def test_dp_global_sharding_epochs(hip_device):
     assert (fa == fb).all()
     assert ra[2]["total_loss"] < ra[0]["total_loss"]
     assert all(abs(v) < float("inf") for v in ra[3].values())
+    assert all(abs(v) < float("inf") for v in ra[4].values())
 
 
 def test_dp_two_ranks_one_gpu(hip_device):

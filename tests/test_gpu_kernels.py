@@ -241,6 +241,38 @@ def test_decoder_bf16_d768(ops, hip_device, nb, N, D):
     _check_decoder(ops, hip_device, "bf16", nb, N, D)
 
 
+@pytest.mark.parametrize("nb,N", [(97, 3001), (700, 50_001), (4096, 3000), (4096, 200_000), (1000, 40_000)])
+def test_decoder_bf16_d768_v6_tasks(ops, hip_device, nb, N):
+    """The d = 768 bf16 sweep above 64 users (k_dec6_bf16: 96 users per E tile, hvae_decoder6.hip) against
+    float64 on the bf16-rounded operands, over its work assignment: a partial user block (97), 8 user blocks x 32
+    splits (700), 43 user blocks with the two excess tasks cut into 128 pieces each -- at 3000 items most of the
+    pieces are empty, at 200,000 every piece runs 40 tiles (4096) -- and 11 user blocks with 8 excess tasks (1000).
+    The fused train form (merge + sparse terms) equals decoder_fwd + decoder_bwd on the same inputs."""
+    D = 768
+    g = torch.Generator(device=hip_device).manual_seed(nb + N)
+    E = torch.randn(N, D, device=hip_device, generator=g)
+    E /= E.norm(dim=1, keepdim=True)
+    U = torch.randn(nb, D, device=hip_device, generator=g) * (4.0 / D ** 0.5)
+    Ek = ops.decoder_image(E)
+    enorm = ops.row_norm_max(Ek)
+    lse, O = ops.decoder_fwd(U, Ek, enorm)
+    Ur, Er = U.bfloat16().double(), Ek.bf16.double()
+    S = Ur @ Er.t()
+    lse_ref = torch.logsumexp(S, 1)
+    O_ref = torch.softmax(S, 1) @ Er
+    assert torch.isfinite(lse).all() and torch.isfinite(O).all()
+    assert (lse.double() - lse_ref).abs().max() < 2e-3 * max(1.0, lse_ref.abs().max().item())
+    assert _maxrel(O, O_ref) < 1e-2
+    lse2, _ = ops.decoder_fwd(U, Ek, enorm, with_o=False)
+    assert torch.allclose(lse2, lse, rtol=0, atol=1e-5)
+    X = synth_csr(nb, N, lam=5.0, seed=nb)
+    xd = ops.csr_from_scipy(X, hip_device)
+    lse_t, O_t, rr, dU = ops.decoder_train(xd, U, Ek, enorm, E, 1.0 / nb, want_o=True)
+    assert torch.equal(lse_t, lse) and torch.equal(O_t, O)
+    rr_b, dU_b = ops.decoder_bwd(xd, U, E, lse, O, 1.0 / nb)
+    assert torch.equal(rr, rr_b) and torch.equal(dU, dU_b)
+
+
 def _check_decoder(ops, hip_device, dtype, nb, N, D):
     E = torch.as_tensor(synth_embeddings(N, D, seed=N))
     g = torch.Generator().manual_seed(nb)

@@ -175,13 +175,18 @@ def test_graph_replay_is_bitwise_eager(hip_device):
     assert a2["total_loss"] < a1["total_loss"]  # it learns
 
 
-@pytest.mark.parametrize("wd,plan_side", [(0.0, False), (0.01, False), (0.01, True)])
-def test_lazy_adam_is_bitwise_dense(hip_device, wd, plan_side, monkeypatch):
+@pytest.mark.parametrize("lazy_read", [True, False])
+@pytest.mark.parametrize("wd,plan_side", [(0.0, False), (0.01, False), (0.01, True), (0.0, True)])
+def test_lazy_adam_is_bitwise_dense(hip_device, wd, plan_side, lazy_read, monkeypatch):
     """Exact lazy Adam (rows outside a batch replay their g = 0 steps when next read) leaves parameters and
-    moments bitwise equal to torch's every-row update, over graph-replayed epochs with a short tail batch.
+    moments bitwise equal to the every-row update, over graph-replayed epochs with a short tail batch.
     plan_side: the W1-gradient plan on its own stream and the catch-up from the CSR entries
-    (hvae_adam_lazy_catchup_csr), the large-batch configuration, forced at B = 32."""
+    (hvae_adam_lazy_catchup_csr), the large-batch configuration, forced at B = 32 -- with wd = 0 its p-only
+    replays (bits 24-29 of last_step) and the per-row slicing of small batches, with wd != 0 the full-store
+    branch. lazy_read=False: the small-batch forward's CSR catch-up launch instead of the row-parallel encoder
+    reading W1t through lazy Adam in registers (HVAE_ENC_LAZY_READ=0)."""
     monkeypatch.setenv("HVAE_PLAN_SIDE_MIN_BATCH", "1" if plan_side else "1000000")
+    monkeypatch.setenv("HVAE_ENC_LAZY_READ", "1" if lazy_read else "0")
     from hvae.executor import ConstBeta, FusedTrainer
     from src.ml.model import HybridVAE
     X = synth_csr(290, 700, seed=13)
