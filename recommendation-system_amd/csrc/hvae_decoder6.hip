@@ -114,17 +114,20 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // LDS-DMA piece i (0..11) of this wave's rows of a tile: M0 = lbase + 8192 (i >> 1) + 1024 (i & 1), source
-// soff + vlane + 128 i; the first of a group waits out the readfirstlane of its SGPR operands (s_nop 4)
+// soff + 128 i + vlane; the first of a group waits out the readfirstlane of its SGPR operands (s_nop 4). Both
+// come in computed: an s_add inside the asm would write SCC behind the compiler's back (a loop branch on SCC then
+// ran the sweep's loop far past its end), and the instruction's offset field moves the LDS destination too (the
+// LDS address is M0 + inst_offset + 16 lane), so the piece's source offset goes in soffset
 template <int i>
 __device__ __forceinline__ void dma_piece(uint32_t soff, uint32_t lbase, int vlane, __amdgpu_buffer_rsrc_t rsrc) {
+  const uint32_t m0 = lbase + (uint32_t)((i >> 1) * 8192 + (i & 1) * 1024);
+  const uint32_t so = soff + (uint32_t)(128 * i);
   if constexpr (i == 0)
-    asm volatile("s_nop 4\n\ts_add_u32 m0, %0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen offset:%5 lds"
-                 :: "s"(lbase), "v"(vlane), "s"(rsrc), "s"(soff), "i"((i >> 1) * 8192 + (i & 1) * 1024),
-                    "i"(128 * i) : "memory");
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(m0), "v"(vlane), "s"(rsrc), "s"(so) : "memory");
   else
-    asm volatile("s_add_u32 m0, %0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen offset:%5 lds"
-                 :: "s"(lbase), "v"(vlane), "s"(rsrc), "s"(soff), "i"((i >> 1) * 8192 + (i & 1) * 1024),
-                    "i"(128 * i) : "memory");
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(m0), "v"(vlane), "s"(rsrc), "s"(so) : "memory");
 }
 
 template <bool WITH_O>

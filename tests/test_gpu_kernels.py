@@ -265,6 +265,23 @@ def test_decoder_bf16_d768_v6_tasks(ops, hip_device, nb, N):
     assert _maxrel(O, O_ref) < 1e-2
     lse2, _ = ops.decoder_fwd(U, Ek, enorm, with_o=False)
     assert torch.allclose(lse2, lse, rtol=0, atol=1e-5)
+    # no user may be flagged: a flagged user is recomputed exactly by the finalize, so a sweep that flags every
+    # user still returns the right lse and O (slowly). The workspace begins with the sweep's flag words (one per
+    # partial row); poisoned with 0xFF, rows the sweep never writes stay -1, and 1 marks a flagged row
+    from hvae._lib import check, lib, ptr, stream_of
+    dt, _, Eh = ops._dec_operand(Ek)
+    need = int(lib().hvae_decoder_workspace(dt, nb, N, D))
+    ws = torch.full((need,), 0xFF, dtype=torch.uint8, device=hip_device)
+    lse3, O3 = torch.empty_like(lse), torch.empty_like(O)
+    check(lib().hvae_decoder_fwd(dt, ptr(U), U.stride(0), ptr(Eh), ptr(enorm), nb, N, D, ptr(lse3), ptr(O3), ptr(ws),
+                                 ws.numel(), stream_of(U)), "hvae_decoder_fwd")
+    ntiles, nub = -(-N // 32), -(-nb // 96)
+    S = max(1, min(-(-256 // nub), max(1, ntiles // 8)))
+    S = -(-ntiles // -(-ntiles // S))
+    slots = nub * S if nub * S <= 256 else 256 + (nub * S - 256) * (256 // (nub * S - 256))
+    flags = ws[:slots * 96 * 4].view(torch.int32)
+    assert int((flags == 1).sum()) == 0 and int((flags == 0).sum()) >= nb
+    assert torch.equal(lse3, lse) and torch.equal(O3, O)
     X = synth_csr(nb, N, lam=5.0, seed=nb)
     xd = ops.csr_from_scipy(X, hip_device)
     lse_t, O_t, rr, dU = ops.decoder_train(xd, U, Ek, enorm, E, 1.0 / nb, want_o=True)
