@@ -71,6 +71,38 @@ constexpr float kMinL = 8.75651e-27f;
 #ifndef DEC6_G2A
 #define DEC6_G2A 12  // GEMM2 d-blocks run beside GEMM1 (the rest beside the softmax)
 #endif
+// Timing-ablation builds only (outputs invalid by construction; scripts/build_variant_src.sh), a bit mask of what
+// the sweep loop leaves out: 1 the LDS-DMA pieces (and their waits), 2 the two barriers, 4 the softmax (exp2, sums,
+// P packing), 8 GEMM1's A operand reads, 16 GEMM2's E^T reads, 32 GEMM1's MFMAs, 64 GEMM2's MFMAs, 128 the waits
+// for the pieces (issued, never waited), 256 the partial / P exchange through LDS
+// LDS-DMA placement: the last DEC6_DMAP of a tile's 12 pieces go one per phase-2 step (beside GEMM2 and the
+// softmax, where a piece costs less issue time than among phase 1's operand reads); the others spread evenly
+// over phase 1's 12 steps
+#ifndef DEC6_DMAP
+#define DEC6_DMAP 0
+#endif
+constexpr int kDmaP2 = DEC6_DMAP, kDmaP1 = 12 - DEC6_DMAP;
+static_assert(kDmaP2 >= 0 && kDmaP2 <= 12, "DEC6_DMAP");
+template <int ks>
+constexpr int p1_piece() {  // the phase-1 piece issued at step ks, or -1
+  constexpr int p = kDmaP1 == 0 ? 0 : (ks * kDmaP1 + 11) / 12;
+  return (kDmaP1 > 0 && p < kDmaP1 && p * 12 / kDmaP1 == ks) ? p : -1;
+}
+#ifndef DEC6_ABL
+#define DEC6_ABL 0
+#endif
+constexpr int kAbl = DEC6_ABL;
+// Timing build only (scripts/probe_dec6_phases.py): each wave adds s_memtime deltas of the sweep loop's phases
+// (wait for [L], phase 1, put + [B1], phase 2), its tile count and its kernel time into dec6_tm
+#ifndef DEC6_TIMING
+#define DEC6_TIMING 0
+#endif
+#if DEC6_TIMING
+__device__ unsigned long long dec6_tm[1024 * 8];
+#define DEC6_T(...) __VA_ARGS__
+#else
+#define DEC6_T(...)
+#endif
 
 __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   const bf16x2 v = {(__bf16)lo, (__bf16)hi};
@@ -196,6 +228,7 @@ __global__ void __launch_bounds__(256, 1) k_dec6_bf16(Dec6Args a) {
   };
 
   f32x4 O[WITH_O ? NDB : 1][3];
+  DEC6_T(unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}; const unsigned long long tk0 = __builtin_amdgcn_s_memtime();)
   for (int task = 0; task < 2; ++task) {
     // ------------------------------------------------------------------------- the block's task ---
     int u, t_beg, t_end, slot;
@@ -361,15 +394,18 @@ __global__ void __launch_bounds__(256, 1) k_dec6_bf16(Dec6Args a) {
     int c0 = 0;
     for (int t = t_beg; t < t_end; ++t) {
       const int c1 = c0 == 2 ? 0 : c0 + 1, c2 = c1 == 2 ? 0 : c1 + 1;
-      wait_vmcnt<0>();
-      barrier();  // [L] tile t + 1 landed, the partner's P(t) in my region, GEMM2(t - 1) done with slot c2
+      DEC6_T(const unsigned long long tm0 = __builtin_amdgcn_s_memtime();)
+      if constexpr (!(kAbl & (1 | 128))) wait_vmcnt<0>();
+      if constexpr (!(kAbl & 2)) barrier();  // [L] tile t + 1 landed, the partner's P(t) in my region, GEMM2(t - 1) done
+                                              // with slot c2
       bf16x8 pb[3];  // P(t)^T: k slots 0..3 my items, 4..7 the partner's
 #pragma unroll
       for (int ub = 0; ub < 3; ++ub) {
-        const uint2 pq = *reinterpret_cast<const uint2*>(xw + ub * 512 + lane * 8);
+        const uint2 pq = (kAbl & 256) ? pn[ub] : *reinterpret_cast<const uint2*>(xw + ub * 512 + lane * 8);
         pb[ub] = __builtin_bit_cast(bf16x8, make_uint4(pn[ub].x, pn[ub].y, pq.x, pq.y));
       }
       asm volatile("s_nop 1" : "+v"(pb[0]), "+v"(pb[1]), "+v"(pb[2]));  // VALU write -> asm MFMA B read
+      DEC6_T(const unsigned long long tm1 = __builtin_amdgcn_s_memtime();)
       const unsigned char* b0 = lds + c0 * TB;  // tile t
       const unsigned char* b1 = lds + c1 * TB;  // tile t + 1
       const uint32_t soff2 = tile_soff(t + 2), lb2 = slot_base(c2);
@@ -381,40 +417,85 @@ __global__ void __launch_bounds__(256, 1) k_dec6_bf16(Dec6Args a) {
       __builtin_amdgcn_sched_barrier(0);
       static_for<0, KS>([&](auto kc) {
         constexpr int ks = decltype(kc)::value;
+        // each operand register is refilled right after the MFMAs that read it have issued, so every LDS read has
+        // the other two MFMA triples (96 cycles) to land in
+        if constexpr (!(kAbl & 32)) {
 #pragma unroll
-        for (int ub = 0; ub < 3; ++ub) sO[ub] = mfma(x0, uf[ub][ks], sO[ub]);
+          for (int ub = 0; ub < 3; ++ub) sO[ub] = mfma(x0, uf[ub][ks], sO[ub]);
+        } else {
 #pragma unroll
-        for (int ub = 0; ub < 3; ++ub) sP[ub] = mfma(x1, uf[ub][ks], sP[ub]);
-        __builtin_amdgcn_sched_barrier(0);  // the operand registers are free once the MFMAs have issued
-        if constexpr (ks + 1 < KS) { x0 = rdA(b1, aOwn, ks + 1); x1 = rdA(b1, aPrt, ks + 1); }
-        if constexpr (WITH_O) {
-          mfma_o<(ks * 3 + 0 < kOInAgpr)>(O[ks][0], y, pb[0]);
-          mfma_o<(ks * 3 + 1 < kOInAgpr)>(O[ks][1], y, pb[1]);
-          mfma_o<(ks * 3 + 2 < kOInAgpr)>(O[ks][2], y, pb[2]);
-          __builtin_amdgcn_sched_barrier(0);
-          y = rdT(b0, ks + 1);
+          for (int ub = 0; ub < 3; ++ub) sO[ub][0] += (float)x0[ub] * (float)uf[ub][ks][0];
         }
-        dma_piece<ks>(soff2, lb2, vlane, rsrc);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (ks + 1 < KS && !(kAbl & 8)) x0 = rdA(b1, aOwn, ks + 1);
+        if constexpr (!(kAbl & 32)) {
+#pragma unroll
+          for (int ub = 0; ub < 3; ++ub) sP[ub] = mfma(x1, uf[ub][ks], sP[ub]);
+        } else {
+#pragma unroll
+          for (int ub = 0; ub < 3; ++ub) sP[ub][0] += (float)x1[ub];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (ks + 1 < KS && !(kAbl & 8)) x1 = rdA(b1, aPrt, ks + 1);
+        if constexpr (WITH_O) {
+          if constexpr (!(kAbl & 64)) {
+            mfma_o<(ks * 3 + 0 < kOInAgpr)>(O[ks][0], y, pb[0]);
+            mfma_o<(ks * 3 + 1 < kOInAgpr)>(O[ks][1], y, pb[1]);
+            mfma_o<(ks * 3 + 2 < kOInAgpr)>(O[ks][2], y, pb[2]);
+          } else {
+            O[ks][0][0] += (float)y[0] * (float)pb[0][0];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (!(kAbl & 16)) y = rdT(b0, ks + 1);
+        }
+        if constexpr (!(kAbl & 1) && p1_piece<ks>() >= 0) dma_piece<p1_piece<ks>()>(soff2, lb2, vlane, rsrc);
         __builtin_amdgcn_sched_barrier(0);
       });
-      put_partial();
-      barrier();  // [B1] partials of tile t + 1
-      // phase 2: the partner's partial in, softmax of tile t + 1, P(t + 1) out | GEMM2(t) d-blocks 12 .. 23
+      DEC6_T(const unsigned long long tm2 = __builtin_amdgcn_s_memtime();)
+      if constexpr (!(kAbl & 256)) put_partial();
+      if constexpr (!(kAbl & 2)) barrier();  // [B1] partials of tile t + 1
+      DEC6_T(const unsigned long long tm3 = __builtin_amdgcn_s_memtime();)
+      // phase 2: the partner's partial in, softmax of tile t + 1, P(t + 1) out | GEMM2(t) d-blocks 12 .. 23. GEMM1's
+      // operand registers are dead here, so E^T is read two d-blocks ahead (y: even blocks, y2: odd) and each read
+      // has two MFMA triples to land; the partner's partial is consumed one step after the barrier, and the 12
+      // exponentials run 2, 1, 1, ... over steps 1 .. 11
       f32x4 xq[3];
 #pragma unroll
-      for (int ub = 0; ub < 3; ++ub) xq[ub] = *reinterpret_cast<const f32x4*>(xp + ub * 1024 + lane * 16);
+      for (int ub = 0; ub < 3; ++ub)
+        xq[ub] = (kAbl & 256) ? sP[ub] : *reinterpret_cast<const f32x4*>(xp + ub * 1024 + lane * 16);
+      bf16x8 y2 = y;
+      if constexpr (!(kAbl & 16)) y2 = rdT(b0, KS + 1);
       __builtin_amdgcn_sched_barrier(0);
       uint2 pq[3];
-      static_for<KS, NDB>([&](auto dc) {
-        constexpr int db = decltype(dc)::value, j = db - KS, ub = j >> 2, r = j & 3;
-        if constexpr (WITH_O) {
-          mfma_o<(db * 3 + 0 < kOInAgpr)>(O[db][0], y, pb[0]);
-          mfma_o<(db * 3 + 1 < kOInAgpr)>(O[db][1], y, pb[1]);
-          mfma_o<(db * 3 + 2 < kOInAgpr)>(O[db][2], y, pb[2]);
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (db + 1 < NDB) y = rdT(b0, db + 1);
+      auto soft = [&](auto ec) {  // exponential e = 4 ub + r; the block's P piece packed and stored after its 4th
+        constexpr int e = decltype(ec)::value, ub = e >> 2, r = e & 3;
+        if constexpr (!(kAbl & 4)) {
+          sO[ub][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sO[ub][r], kLog2e, -mL[ub]));
+          lsum[ub] += sO[ub][r];
         }
-        if constexpr (j == 0) {
+        if constexpr (r == 3) {
+          pq[ub] = (kAbl & 4) ? make_uint2(__float_as_uint(sO[ub][0]), __float_as_uint(sO[ub][1]))
+                              : make_uint2(pack_bf16x2(sO[ub][0], sO[ub][1]), pack_bf16x2(sO[ub][2], sO[ub][3]));
+          if constexpr (!(kAbl & 256))
+            *reinterpret_cast<uint2*>(xp + ub * 512 + lane * 8) = pq[ub];  // over the partner's partial (read above)
+        }
+        (void)ub; (void)r;
+      };
+      static_for<KS, NDB>([&](auto dc) {
+        constexpr int db = decltype(dc)::value, j = db - KS;
+        if constexpr (WITH_O) {
+          bf16x8& yc = (db & 1) ? y2 : y;
+          if constexpr (!(kAbl & 64)) {
+            mfma_o<(db * 3 + 0 < kOInAgpr)>(O[db][0], yc, pb[0]);
+            mfma_o<(db * 3 + 1 < kOInAgpr)>(O[db][1], yc, pb[1]);
+            mfma_o<(db * 3 + 2 < kOInAgpr)>(O[db][2], yc, pb[2]);
+          } else {
+            O[db][0][0] += (float)yc[0] * (float)pb[0][0];
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (db + 2 < NDB && !(kAbl & 16)) yc = rdT(b0, db + 2);
+        }
+        if constexpr (j == 1) {
 #pragma unroll
           for (int u2 = 0; u2 < 3; ++u2) sO[u2] += xq[u2];
           mask_tail(t + 1);
@@ -422,20 +503,22 @@ __global__ void __launch_bounds__(256, 1) k_dec6_bf16(Dec6Args a) {
 #pragma unroll
             for (int u2 = 0; u2 < 3; ++u2) sO[u2] = f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
           }
+          soft(std::integral_constant<int, 0>{});
+          soft(std::integral_constant<int, 1>{});
         }
-        // one exponential per step: element r of user block ub; the block's P piece packed and stored after its 4th
-        sO[ub][r] = __builtin_amdgcn_exp2f(__builtin_fmaf(sO[ub][r], kLog2e, -mL[ub]));
-        lsum[ub] += sO[ub][r];
-        if constexpr (r == 3) {
-          pq[ub] = make_uint2(pack_bf16x2(sO[ub][0], sO[ub][1]), pack_bf16x2(sO[ub][2], sO[ub][3]));
-          *reinterpret_cast<uint2*>(xp + ub * 512 + lane * 8) = pq[ub];  // over the partner's partial (read above)
+        if constexpr (j >= 2) soft(std::integral_constant<int, j>{});
+        if constexpr (!(kAbl & 1) && j < kDmaP2) dma_piece<kDmaP1 + j>(soff2, lb2, vlane, rsrc);
+        if constexpr ((kAbl & 4) && j == 11) {
+#pragma unroll
+          for (int u2 = 0; u2 < 3; ++u2) lsum[u2] += 1.f;  // l >= 1: no user flagged
         }
-        (void)ub; (void)r;
         __builtin_amdgcn_sched_barrier(0);
       });
 #pragma unroll
       for (int ub = 0; ub < 3; ++ub) pn[ub] = pq[ub];
       c0 = c1;
+      DEC6_T(const unsigned long long tm4 = __builtin_amdgcn_s_memtime(); tacc[0] += tm1 - tm0; tacc[1] += tm2 - tm1;
+             tacc[2] += tm3 - tm2; tacc[3] += tm4 - tm3; tacc[4] += 1;)
     }
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");  // the last asm MFMAs' results settle
@@ -461,7 +544,7 @@ __global__ void __launch_bounds__(256, 1) k_dec6_bf16(Dec6Args a) {
       if (h == 0 && kg == 0) {
         a.m[row] = mvl[w * GU + 16 * ub + c16];
         a.l[row] = l;
-        a.flag[row] = !(l >= kMinL);
+        a.flag[row] = kAbl ? 0 : !(l >= kMinL);  // ablation builds: never the exact fixup (outputs invalid anyway)
       }
       if constexpr (WITH_O) {
         float* orow = a.O + row * D + 384 * h + 4 * kg;
@@ -472,9 +555,22 @@ __global__ void __launch_bounds__(256, 1) k_dec6_bf16(Dec6Args a) {
     }
     barrier();  // [E2] the exchange words are read before a next task's prologue rewrites them
   }
+#if DEC6_TIMING
+  tacc[5] = __builtin_amdgcn_s_memtime() - tk0;
+  if (lane == 0 && blockIdx.x < 256)
+    for (int i = 0; i < 6; ++i) dec6_tm[(blockIdx.x * 4 + w) * 8 + i] = tacc[i];
+#endif
 }
 
 }  // namespace dec6
+
+#if DEC6_TIMING
+extern "C" int hvae_dec6_timing_fetch(unsigned long long* out) {  // [1024 waves][8], timing builds only
+  HVAE_HIP(hipDeviceSynchronize());
+  HVAE_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(dec6::dec6_tm), sizeof(dec6::dec6_tm)));
+  return HVAE_OK;
+}
+#endif
 
 bool dec6_plan(int64_t nb, int64_t N, Dec6Plan& p) {
   p = Dec6Plan{};

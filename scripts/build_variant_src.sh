@@ -9,6 +9,7 @@ mkdir -p ../build_var
 HIPCC=/opt/rocm/bin/hipcc
 extra=""
 [ "$stem" = "hvae_decoder5" ] && extra="-mllvm -amdgpu-mfma-vgpr-form"
+[ "$stem" = "hvae_decoder6" ] && extra="-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize"
 $HIPCC --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I../include -munsafe-fp-atomics $extra "$@" \
   -c csrc/$stem.hip -o ../build_var/${stem}_$name.o
 objs=$(ls build/*.o | grep -v "/$stem.o")
