@@ -38,8 +38,8 @@
 #include <algorithm>
 #include <array>
 
-#include "hvae_common.h"
-#include "hvae_dec6.h"
+#include "../hvae_common.h"
+#include "../hvae_dec6.h"
 
 namespace hvae {
 namespace dec6 {

@@ -1139,6 +1139,7 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   float lse_b;
   float o[4] = {0.f, 0.f, 0.f, 0.f};
   int nsp = a.splits;
+#if HVAE_AB  // version 6's slot rows (A/B library only)
   const int v6u = a.v6_upb ? (int)(b / a.v6_upb) : 0;
   const int64_t v6j = a.v6_upb ? b % a.v6_upb : 0;
   if (a.v6_upb) nsp = dec6_nslots(a.v6_nub, a.v6_S, a.v6_main, a.v6_P, v6u);
@@ -1146,6 +1147,9 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     return a.v6_upb ? (int64_t)dec6_slot_of(a.v6_nub, a.v6_S, a.v6_main, a.v6_P, v6u, s) * a.v6_upb + v6j
                     : (int64_t)s * a.nb + b;
   };
+#else
+  auto prow = [&](int s) -> int64_t { return (int64_t)s * a.nb + b; };  // partial row of user b's s-th split
+#endif
   if (a.splits > 1 || a.v6_upb) {
     float M = -INFINITY;
     int fl = 0;
@@ -1515,8 +1519,11 @@ static DecPlan dec_plan(int dtype, int64_t nb, int64_t N, int64_t D) {
   p.v3 = p.v2 && v3_supported(D);
   p.v4 = (p.v3 && v4_supported(D)) || (p.v2 && v4_384(D, nb));
   p.v5 = p.v4 && v5_supported(D);  // same users per block (64), splits and partial layout as version 4
-  // version 6 (hvae_decoder6.hip) above 64 users: 96 users per E tile; HVAE_DEC_V6=0 (A/B) runs version 5
-  p.v6 = p.v5 && D == 768 && env_int("HVAE_DEC_V6", 1) != 0 && dec6_plan(nb, N, p.p6);
+#if HVAE_AB  // HVAE_DEC_V6=1: version 6 (ab/hvae_decoder6.hip, 96 users per E tile) above 64 users
+  p.v6 = p.v5 && D == 768 && env_int("HVAE_DEC_V6", 0) != 0 && dec6_plan(nb, N, p.p6);
+#else
+  p.v6 = 0;
+#endif
   p.ds = p.v2 && (D > 384 || nb <= 64) ? 2 : 1;
   if (p.v2 && D <= 384 && (dec_forced_ds() == 1 || dec_forced_ds() == 2)) p.ds = dec_forced_ds();
   p.nw = p.v2 && p.ds == 2 && nb > 64 && D <= 384 ? 8 : 4;
@@ -1805,8 +1812,9 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
   }
   const bool bf = dtype != HVAE_F32;  // fixed-offset sweeps (bf16, fp8): flags, bf16 E for the exact fixup
   const bool want_o = O || dU;
-  if (p.v6 && ws_bytes < dec6_ws_bytes(p.p6, nb, D)) p.v6 = 0;
   FinArgs a{};
+#if HVAE_AB
+  if (p.v6 && ws_bytes < dec6_ws_bytes(p.p6, nb, D)) p.v6 = 0;
   if (p.v6) {  // version 6: slot-row partials, merged per user by the finalize's slot map
     const Dec6Plan& q = p.p6;
     const size_t rows = (size_t)q.slots * kDec6Users;
@@ -1830,6 +1838,7 @@ static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, co
     return decoder_finalize(a, U, ldu, E, E32, x, nb, N, D, scale, lse, recon_rows, dU, kl_rows, beta, beta_dev,
                             loss3, accum3, q.X > 0 || q.S > 8, st);
   }
+#endif
   char* w = (char*)ws;
   DecOut o{};
   o.flag = (int*)w;

@@ -1,4 +1,4 @@
-"""LDS bank-conflict model of the version-6 bf16 sweep (hvae_decoder6.hip, k_dec6_bf16, d = 768) and the
+"""LDS bank-conflict model of the version-6 bf16 sweep (csrc/ab/hvae_decoder6.hip, k_dec6_bf16, d = 768) and the
 search that picked its row map and chunk swizzle.
 
 The tile image is version 2's (8-row x 32-column sub-tiles of 512 B per 128-column segment), with a chunk XOR
@@ -88,7 +88,7 @@ def search():
     return best[1], best[2], best[3]
 
 
-# the kernel's choice (DEC6_BASES / DEC6_SWZ in hvae_decoder6.hip); test_fp8_layout_cpu.py asserts it is conflict-free
+# the kernel's choice (DEC6_BASES / DEC6_SWZ in csrc/ab/hvae_decoder6.hip); test_fp8_layout_cpu.py asserts it is conflict-free
 KERNEL_BASES = (0, 4, 8, 12)
 KERNEL_SWZ = 0x40
 

@@ -2,6 +2,8 @@
 shape NBxN given, and report the partial slot rows that come back unwritten or flagged (a flagged user is
 recomputed exactly by the finalize, so a sweep that flags users gives right answers slowly), and lse against
 float64 for the unflagged users."""
+import os
+os.environ.setdefault("HVAE_DEC_V6", "1")  # version 6 is an A/B-library sweep (HVAE_LIB=build_var/libhvae_ab.so or a variant)
 import sys, time
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]

@@ -1,5 +1,7 @@
-"""Time the d = 768 bf16 sweep (product library: version 6 above 64 users) over growing item counts, one line
+"""Time the d = 768 bf16 sweep (A/B library or a variant build, HVAE_DEC_V6=1: version 6 above 64 users) over growing item counts, one line
 per call, so that a slow or stuck shape shows where it starts."""
+import os
+os.environ.setdefault("HVAE_DEC_V6", "1")  # version 6 is an A/B-library sweep (HVAE_LIB=build_var/libhvae_ab.so or a variant)
 import sys, time
 from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]

@@ -4,6 +4,8 @@ phase 1 (GEMM1 | GEMM2 first half | DMA), at put + [B1], and in phase 2 (GEMM2 s
 
     HVAE_LIB=build_var/libhvae_d6tm.so python scripts/probe_dec6_phases.py [--nb 4096] [--N 1000000]
 """
+import os
+os.environ.setdefault("HVAE_DEC_V6", "1")  # version 6 is an A/B-library sweep (HVAE_LIB=build_var/libhvae_ab.so or a variant)
 import argparse
 import ctypes as C
 import json

@@ -1,9 +1,10 @@
 """Checks of the A/B variant kernels (not collected by default: no test_ prefix).
 
 The product libhvae.so runs one sweep per (dtype, d) and ignores the environment. The retired variants -- bf16
-versions 2, 3 and 4 at d = 768 beside version 5, the fp8 sweep with version 4's structure (k_dec4_f8) and the
-D-split ring beside the fp8 version 5 (k_dec5_f8) -- build only with -DHVAE_AB=1 (`make -C recommendation-system_amd lib-ab` ->
-build_var/libhvae_ab.so), where HVAE_DEC_* select them at plan time. tests/test_gpu_ab_variant.py runs this file
+versions 2, 3 and 4 at d = 768 beside version 5, version 6 (96 users per E tile), the d = 384 version 5
+(k_dec5w_bf16), the fp8 sweep with version 4's structure (k_dec4_f8) and the D-split ring beside the fp8 version 5
+(k_dec5_f8) -- live in recommendation-system_amd/csrc/ab/ and build only with -DHVAE_AB=1
+(`make -C recommendation-system_amd lib-ab` -> build_var/libhvae_ab.so), where HVAE_DEC_* select them at plan time. tests/test_gpu_ab_variant.py runs this file
 in a subprocess with HVAE_LIB pointing at that build, so the variants keep their parity checks without being
 shipped.
 """
@@ -161,3 +162,55 @@ def test_rowgrad_sorted_plan_equals_atomic_plan(ops, dev, nb, N, lam, hot, monke
         assert torch.equal(x, y)
     assert a[9] == 0 and a[10] == 0
     np.testing.assert_array_equal(a[2].cpu().numpy(), np.unique(X.indices))
+
+
+@pytest.mark.parametrize("nb,N", [(97, 3001), (700, 50_001), (4096, 3000), (4096, 200_000), (1000, 40_000)])
+def test_decoder_bf16_d768_v6_tasks(ops, dev, nb, N, monkeypatch):
+    """The d = 768 bf16 sweep above 64 users (k_dec6_bf16: 96 users per E tile, csrc/ab/hvae_decoder6.hip) against
+    float64 on the bf16-rounded operands, over its work assignment: a partial user block (97), 8 user blocks x 32
+    splits (700), 43 user blocks with the two excess tasks cut into 128 pieces each -- at 3000 items most of the
+    pieces are empty, at 200,000 every piece runs 40 tiles (4096) -- and 11 user blocks with 8 excess tasks (1000).
+    The fused train form (merge + sparse terms) equals decoder_fwd + decoder_bwd on the same inputs. Version 6
+    tied with version 5 at the Syn-10M shard, so it runs only here (HVAE_DEC_V6=1)."""
+    monkeypatch.setenv("HVAE_DEC_V6", "1")
+    D = 768
+    g = torch.Generator(device=dev).manual_seed(nb + N)
+    E = torch.randn(N, D, device=dev, generator=g)
+    E /= E.norm(dim=1, keepdim=True)
+    U = torch.randn(nb, D, device=dev, generator=g) * (4.0 / D ** 0.5)
+    Ek = ops.decoder_image(E)
+    enorm = ops.row_norm_max(Ek)
+    lse, O = ops.decoder_fwd(U, Ek, enorm)
+    Ur, Er = U.bfloat16().double(), Ek.bf16.double()
+    S = Ur @ Er.t()
+    lse_ref = torch.logsumexp(S, 1)
+    O_ref = torch.softmax(S, 1) @ Er
+    assert torch.isfinite(lse).all() and torch.isfinite(O).all()
+    assert (lse.double() - lse_ref).abs().max() < 2e-3 * max(1.0, lse_ref.abs().max().item())
+    assert _maxrel(O, O_ref) < 1e-2
+    lse2, _ = ops.decoder_fwd(U, Ek, enorm, with_o=False)
+    assert torch.allclose(lse2, lse, rtol=0, atol=1e-5)
+    # no user may be flagged: a flagged user is recomputed exactly by the finalize, so a sweep that flags every
+    # user still returns the right lse and O (slowly). The workspace begins with the sweep's flag words (one per
+    # partial row); poisoned with 0xFF, rows the sweep never writes stay -1, and 1 marks a flagged row
+    from hvae._lib import check, lib, ptr, stream_of
+    dt, _, Eh = ops._dec_operand(Ek)
+    need = int(lib().hvae_decoder_workspace(dt, nb, N, D))
+    assert int(lib().hvae_decoder_users_per_tile(dt, nb, N, D)) == 96  # the plan took version 6
+    ws = torch.full((need,), 0xFF, dtype=torch.uint8, device=dev)
+    lse3, O3 = torch.empty_like(lse), torch.empty_like(O)
+    check(lib().hvae_decoder_fwd(dt, ptr(U), U.stride(0), ptr(Eh), ptr(enorm), nb, N, D, ptr(lse3), ptr(O3), ptr(ws),
+                                 ws.numel(), stream_of(U)), "hvae_decoder_fwd")
+    ntiles, nub = -(-N // 32), -(-nb // 96)
+    S = max(1, min(-(-256 // nub), max(1, ntiles // 8)))
+    S = -(-ntiles // -(-ntiles // S))
+    slots = nub * S if nub * S <= 256 else 256 + (nub * S - 256) * (256 // (nub * S - 256))
+    flags = ws[:slots * 96 * 4].view(torch.int32)
+    assert int((flags == 1).sum()) == 0 and int((flags == 0).sum()) >= nb
+    assert torch.equal(lse3, lse) and torch.equal(O3, O)
+    X = synth_csr(nb, N, lam=5.0, seed=nb)
+    xd = ops.csr_from_scipy(X, dev)
+    lse_t, O_t, rr, dU = ops.decoder_train(xd, U, Ek, enorm, E, 1.0 / nb, want_o=True)
+    assert torch.equal(lse_t, lse) and torch.equal(O_t, O)
+    rr_b, dU_b = ops.decoder_bwd(xd, U, E, lse, O, 1.0 / nb)
+    assert torch.equal(rr, rr_b) and torch.equal(dU, dU_b)

@@ -241,55 +241,6 @@ def test_decoder_bf16_d768(ops, hip_device, nb, N, D):
     _check_decoder(ops, hip_device, "bf16", nb, N, D)
 
 
-@pytest.mark.parametrize("nb,N", [(97, 3001), (700, 50_001), (4096, 3000), (4096, 200_000), (1000, 40_000)])
-def test_decoder_bf16_d768_v6_tasks(ops, hip_device, nb, N):
-    """The d = 768 bf16 sweep above 64 users (k_dec6_bf16: 96 users per E tile, hvae_decoder6.hip) against
-    float64 on the bf16-rounded operands, over its work assignment: a partial user block (97), 8 user blocks x 32
-    splits (700), 43 user blocks with the two excess tasks cut into 128 pieces each -- at 3000 items most of the
-    pieces are empty, at 200,000 every piece runs 40 tiles (4096) -- and 11 user blocks with 8 excess tasks (1000).
-    The fused train form (merge + sparse terms) equals decoder_fwd + decoder_bwd on the same inputs."""
-    D = 768
-    g = torch.Generator(device=hip_device).manual_seed(nb + N)
-    E = torch.randn(N, D, device=hip_device, generator=g)
-    E /= E.norm(dim=1, keepdim=True)
-    U = torch.randn(nb, D, device=hip_device, generator=g) * (4.0 / D ** 0.5)
-    Ek = ops.decoder_image(E)
-    enorm = ops.row_norm_max(Ek)
-    lse, O = ops.decoder_fwd(U, Ek, enorm)
-    Ur, Er = U.bfloat16().double(), Ek.bf16.double()
-    S = Ur @ Er.t()
-    lse_ref = torch.logsumexp(S, 1)
-    O_ref = torch.softmax(S, 1) @ Er
-    assert torch.isfinite(lse).all() and torch.isfinite(O).all()
-    assert (lse.double() - lse_ref).abs().max() < 2e-3 * max(1.0, lse_ref.abs().max().item())
-    assert _maxrel(O, O_ref) < 1e-2
-    lse2, _ = ops.decoder_fwd(U, Ek, enorm, with_o=False)
-    assert torch.allclose(lse2, lse, rtol=0, atol=1e-5)
-    # no user may be flagged: a flagged user is recomputed exactly by the finalize, so a sweep that flags every
-    # user still returns the right lse and O (slowly). The workspace begins with the sweep's flag words (one per
-    # partial row); poisoned with 0xFF, rows the sweep never writes stay -1, and 1 marks a flagged row
-    from hvae._lib import check, lib, ptr, stream_of
-    dt, _, Eh = ops._dec_operand(Ek)
-    need = int(lib().hvae_decoder_workspace(dt, nb, N, D))
-    ws = torch.full((need,), 0xFF, dtype=torch.uint8, device=hip_device)
-    lse3, O3 = torch.empty_like(lse), torch.empty_like(O)
-    check(lib().hvae_decoder_fwd(dt, ptr(U), U.stride(0), ptr(Eh), ptr(enorm), nb, N, D, ptr(lse3), ptr(O3), ptr(ws),
-                                 ws.numel(), stream_of(U)), "hvae_decoder_fwd")
-    ntiles, nub = -(-N // 32), -(-nb // 96)
-    S = max(1, min(-(-256 // nub), max(1, ntiles // 8)))
-    S = -(-ntiles // -(-ntiles // S))
-    slots = nub * S if nub * S <= 256 else 256 + (nub * S - 256) * (256 // (nub * S - 256))
-    flags = ws[:slots * 96 * 4].view(torch.int32)
-    assert int((flags == 1).sum()) == 0 and int((flags == 0).sum()) >= nb
-    assert torch.equal(lse3, lse) and torch.equal(O3, O)
-    X = synth_csr(nb, N, lam=5.0, seed=nb)
-    xd = ops.csr_from_scipy(X, hip_device)
-    lse_t, O_t, rr, dU = ops.decoder_train(xd, U, Ek, enorm, E, 1.0 / nb, want_o=True)
-    assert torch.equal(lse_t, lse) and torch.equal(O_t, O)
-    rr_b, dU_b = ops.decoder_bwd(xd, U, E, lse, O, 1.0 / nb)
-    assert torch.equal(rr, rr_b) and torch.equal(dU, dU_b)
-
-
 def _check_decoder(ops, hip_device, dtype, nb, N, D):
     E = torch.as_tensor(synth_embeddings(N, D, seed=N))
     g = torch.Generator().manual_seed(nb)
@@ -454,7 +405,10 @@ def test_clip_and_adam(ops, hip_device):
 
 
 def test_adam_flat_equals_split(ops, hip_device):
-    """hvae_adam_flat (one launch over [W1t | pad | dense]) == hvae_adam_rows + hvae_adam_dense, bitwise."""
+    """hvae_adam_flat (one launch over [W1t | pad | dense]) == hvae_adam_rows + hvae_adam_dense: bitwise over W1t
+    and the pad; over the dense tail within a few ulp, since hvae_adam_dense (the eager drop-in step) follows torch's
+    CPU arithmetic (correctly rounded sqrt and division, hvae_adam.h adam_elem_exact) while the fused trainer's flat
+    launch keeps unfused products and the hardware square root and reciprocal (adam_elem)."""
     from hvae._lib import lib, ptr, stream_of
     from hvae import _lib
     g = torch.Generator().manual_seed(9)
@@ -474,7 +428,9 @@ def test_adam_flat_equals_split(ops, hip_device):
     p2, m2, v2 = flat.clone(), m.clone(), v.clone()
     _lib.check(lib().hvae_adam_flat(C.byref(cfg), ptr(p2), ptr(m2), ptr(v2), rg.ref, N, H, ptr(gd), off, nd,
                                     stream_of(p2)), "adam_flat")
-    assert torch.equal(p1, p2) and torch.equal(m1, m2) and torch.equal(v1, v2)
+    assert torch.equal(p1[:off], p2[:off]) and torch.equal(m1[:off], m2[:off]) and torch.equal(v1[:off], v2[:off])
+    for a, b in ((p1, p2), (m1, m2), (v1, v2)):  # exact (fma-contracted, correctly rounded) vs fast: ~1 ulp
+        assert torch.allclose(a[off:], b[off:], rtol=1e-6, atol=1e-7)
 
 
 def test_clip_step_counters(ops, hip_device):
