@@ -92,6 +92,32 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 #ifndef DEC5_BFREE
 #define DEC5_BFREE 0  // A/B: branch-free LDS-DMA issue in the loop
 #endif
+// Exponential offload (A/B builds): DEC5_EXPPOLY of the 4 item pairs per user half and tile take a packed-f32
+// polynomial exp2 (exp2_pk) instead of two v_exp_f32
+#ifndef DEC5_EXPPOLY
+#define DEC5_EXPPOLY 0
+#endif
+#ifndef DEC5_EXPPOLY8  // the same for the fp8 producers' 8 pairs per lane and tile
+#define DEC5_EXPPOLY8 0
+#endif
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2v __attribute__((ext_vector_type(2)));
+// 2^x for a pair on the packed f32 VALU (v_pk_add_f32 / v_pk_fma_f32): Cody-Waite split x = n + f, n = rint(x)
+// by the 1.5 * 2^23 shift, f in [-1/2, 1/2], 2^f by a degree-4 polynomial (relative error 4e-5, far below the
+// bf16 rounding of P), 2^n added into the exponent field; x below -126 clamps (2^-126, not 0)
+__device__ __forceinline__ f32x2 exp2_pk(f32x2 x) {
+  const f32x2 lo = {-126.f, -126.f}, sh = {12582912.f, 12582912.f};
+  x = __builtin_elementwise_max(x, lo);
+  const f32x2 t = x + sh;
+  const f32x2 f = x - (t - sh);
+  f32x2 p = {0.0096181291f, 0.0096181291f};
+  p = __builtin_elementwise_fma(p, f, f32x2{0.0555041087f, 0.0555041087f});
+  p = __builtin_elementwise_fma(p, f, f32x2{0.2402265070f, 0.2402265070f});
+  p = __builtin_elementwise_fma(p, f, f32x2{0.6931471806f, 0.6931471806f});
+  p = __builtin_elementwise_fma(p, f, f32x2{1.f, 1.f});
+  const i32x2v e = (__builtin_bit_cast(i32x2v, t) - 0x4B400000) << 23;
+  return __builtin_bit_cast(f32x2, __builtin_bit_cast(i32x2v, p) + e);
+}
 #ifndef DEC5_P32
 #define DEC5_P32 1  // producers of 32 users over one item half (GEMM1 reads each tile twice, not four times);
                     // 0 (A/B): producers of 16 users over both halves

@@ -198,6 +198,17 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
         float pv[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
+          if (uh * 2 + (r >> 1) < DEC5_EXPPOLY) {  // A/B: the pair (r, r + 1) on the packed polynomial
+            if ((r & 1) == 0) {
+              const f32x2 x = {__builtin_fmaf(s_nx[uh][r], kLog2e, -mL[uh]), __builtin_fmaf(s_nx[uh][r + 1], kLog2e, -mL[uh])};
+              const f32x2 y = exp2_pk(x);
+              pv[r] = y[0];
+              pv[r + 1] = y[1];
+              lsum[uh] += pv[r];
+              lsum[uh] += pv[r + 1];
+            }
+            continue;
+          }
           pv[r] = __builtin_amdgcn_exp2f(__builtin_fmaf(s_nx[uh][r], kLog2e, -mL[uh]));
           lsum[uh] += pv[r];
         }
@@ -757,6 +768,17 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
         float qv[4];
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
+          if (j4 * 2 + (b >> 1) < DEC5_EXPPOLY8) {  // A/B: the pair (b, b + 1) on the packed polynomial
+            if ((b & 1) == 0) {
+              const f32x2 y = exp2_pk(f32x2{__builtin_fmaf(sv[4 * j4 + b], kLog2e, -cE),
+                                            __builtin_fmaf(sv[4 * j4 + b + 1], kLog2e, -cE)});
+              qv[b] = y[0];
+              qv[b + 1] = y[1];
+              qsum += qv[b];
+              qsum += qv[b + 1];
+            }
+            continue;
+          }
           qv[b] = __builtin_amdgcn_exp2f(__builtin_fmaf(sv[4 * j4 + b], kLog2e, -cE));
           qsum += qv[b];
         }
