@@ -47,6 +47,16 @@ struct Probe {
 static Probe g_probe;
 static std::mutex g_probe_mu;
 
+// Head start for an armed launch: one wave that spins ~200 us on the constant 100-MHz clock (a bounded loop)
+// before the start event. A hipEvent recorded on a stream the device has drained is stamped before the host has
+// enqueued the kernel after it, so on a host-bound (eager) step the pair would time the host's gap too (the fp8
+// Syn-10M line's 428-us "adam_catchup" against 115 us in its kernel trace); with the hold in front, the kernel
+// is queued behind the start event by the time the event executes.
+__global__ void k_probe_hold(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
 void probe_mark(const char* name, hipStream_t st, bool begin) {
   if (g_probe.cap == 0) return;  // fast path: nothing armed
   std::lock_guard<std::mutex> lk(g_probe_mu);
@@ -55,6 +65,8 @@ void probe_mark(const char* name, hipStream_t st, bool begin) {
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
   if (begin) {
     if (g_probe.n >= g_probe.cap) return;
+    k_probe_hold<<<1, 64, 0, st>>>(20000);  // 200 us at 100 MHz
+    if (hipGetLastError() != hipSuccess) return;
     if (hipEventRecord(g_probe.ev[2 * g_probe.n], st) == hipSuccess) g_probe.open = true;
   } else if (g_probe.open) {
     if (hipEventRecord(g_probe.ev[2 * g_probe.n + 1], st) == hipSuccess) ++g_probe.n;
