@@ -1067,10 +1067,10 @@ class FusedTrainer:
             if int(sizes[0]) != n or int(-sizes[1]) != n:
                 raise ValueError("data-parallel shards of unequal sizes: give every rank the whole dataset "
                                  "(DeviceData.dp_global) or equal shards")
-            if shuffle:
-                mine = users[_sampler_order(n, generator, self.device).cpu().numpy()]
-            else:
-                mine = users
+            # the rank's own shard in the sampler's order, gathered on the device (a host round trip of the
+            # order and the users cost ~10-45 ms per epoch at 1.25 M users: scripts/bench_dp_emul.py)
+            order = _sampler_order(n, generator, self.device) if shuffle else None
+            mine = data.users[order.to(self.device)] if order is not None else data.users
             n_full, t = divmod(n, B)
             counts = [t] * W
         self.dp_epoch += 1
@@ -1078,7 +1078,10 @@ class FusedTrainer:
             counts = [0] * W
         if max_batches is not None:
             n_full, counts = min(n_full, max_batches), [0] * W
-        data.perm[:len(mine)].copy_(torch.as_tensor(np.asarray(mine, dtype=np.int32)).to(self.device))
+        if isinstance(mine, torch.Tensor):
+            data.perm[:len(mine)].copy_(mine)
+        else:
+            data.perm[:len(mine)].copy_(torch.as_tensor(np.asarray(mine, dtype=np.int32)).to(self.device))
         self.accum_train.zero_()
         self.boff.zero_()
         n_steps = n_full + (1 if sum(counts) else 0)

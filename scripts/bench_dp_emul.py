@@ -1,6 +1,6 @@
 """One rank's data-parallel step at W ranks, emulated on ONE GPU.
 
-    python scripts/bench_dp_emul.py [--world 8] [--steps 20] [--warmup 6] [--workload syn10m]
+    python scripts/bench_dp_emul.py [--world 8] [--steps 20] [--warmup 6] [--workload syn10m] [--precision bf16|fp8]
 
 The step of rank 0 of a W-rank job is the single-GPU step over its own batch of B users plus the work the
 exchange adds: the union batch's row-gradient plan (beside the forward), its apply over the gathered da, the
@@ -31,6 +31,49 @@ import torch  # noqa: E402
 from bench import WORKLOADS, make_data  # noqa: E402
 
 
+MARKS = []  # (tag, host time, device event) while ARMED
+ARMED = [False]
+
+
+def mark(tag):
+    """A step-phase boundary: the host clock and a hipEvent on the current stream (every phase of a rank's step
+    is enqueued on it in order: the three graphs and the exchanges between them)."""
+    if ARMED[0]:
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        MARKS.append((tag, time.perf_counter(), e))
+
+
+def phase_report(marks):
+    """Median per-step phase times from the marks of the timed run: device (event to event) and host (enqueue
+    clock), plus what lies outside the steps (the epoch's host setup and its closing sync)."""
+    steps, cur = [], None
+    for tag, ht, ev in marks:
+        if tag == "s":
+            cur = {"s": (ht, ev)}
+            steps.append(cur)
+        elif cur is not None:
+            cur[tag] = (ht, ev)
+    full = [st for st in steps if "e" in st]
+    if len(full) < 3:
+        return {}
+    order = [t for t in ("s", "csr0", "csr1", "g0", "g1", "e") if t in full[0]]
+    names = {("s", "csr0"): "pre_graph", ("csr0", "csr1"): "csr_exchange", ("csr1", "g0"): "main_graph",
+             ("g0", "g1"): "grad_exchange", ("g1", "e"): "update_graph", ("s", "e"): "step_graphs"}
+    out = {"device_ms": {}, "host_ms": {}}
+    body = full[1:-1]  # steady state: drop the first and the last step of the run
+    for a, b in zip(order, order[1:]):
+        nm = names.get((a, b), f"{a}-{b}")
+        out["device_ms"][nm] = round(float(np.median([st[a][1].elapsed_time(st[b][1]) for st in body])), 4)
+        out["host_ms"][nm] = round(float(np.median([(st[b][0] - st[a][0]) * 1e3 for st in body])), 4)
+    nxt = list(zip(full, full[1:]))[1:]
+    out["device_ms"]["step_to_step"] = round(float(np.median([a["s"][1].elapsed_time(b["s"][1]) for a, b in nxt])), 4)
+    out["host_ms"]["step_to_step"] = round(float(np.median([(b["s"][0] - a["s"][0]) * 1e3 for a, b in nxt])), 4)
+    out["steps_marked"] = len(full)
+    out["run_span_ms"] = round((full[-1]["e"][0] - full[0]["s"][0]) * 1e3, 3)
+    return out
+
+
 def make_emul_exchange(world, device, n_items, H, n_small, packets_fn):
     """A DPExchange whose rank-0 collectives are served from pre-packed packets of W - 1 synthetic ranks."""
     from hvae import dist as D
@@ -50,11 +93,14 @@ def make_emul_exchange(world, device, n_items, H, n_small, packets_fn):
             return np.asarray(values, dtype=np.float64)  # every emulated rank reports the same bookkeeping
 
         def communicate_csr(self):
+            mark("csr0")
             pk = packets_fn(self.B, self.cap, self.L)  # [W - 1, batches, L] on the device
             self.recv_csr[0].copy_(self.send[self.ns:])
             self.recv_csr[1:].copy_(pk[:, self.step_i % pk.shape[1], self.ns:])
+            mark("csr1")
 
         def communicate_grads(self):
+            mark("g0")
             self.recv_g[0].copy_(self.send_g)
             self.recv_g[1:].copy_(self.send_g.expand(self.world - 1, -1))
             B = self.B
@@ -64,6 +110,7 @@ def make_emul_exchange(world, device, n_items, H, n_small, packets_fn):
                 self.da_other = 1e-4 * torch.randn((self.world - 1) * B, self.H, generator=g, device=self.device)
             self.recv_da[B:].copy_(self.da_other)
             self.step_i += 1
+            mark("g1")
 
     return EmulExchange()
 
@@ -75,6 +122,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--workload", default="syn10m", choices=sorted(WORKLOADS))
     ap.add_argument("--other-batches", type=int, default=8, help="distinct batches per emulated rank (cycled)")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp8"])
     args = ap.parse_args()
     w = dict(WORKLOADS[args.workload])
     dev = torch.device("cuda", 0)
@@ -92,7 +140,17 @@ def main():
         torch.manual_seed(0)
         model = HybridVAE(w["items"], E, latent_dim=w["latent"], hidden_dims=w["hidden"], dropout=w["dropout"],
                           beta=w["beta"]).to(dev)
-        fused = FusedTrainer(model, dev, lr=w["lr"], precision="bf16", seed=1234, use_graphs=True)
+        fused = FusedTrainer(model, dev, lr=w["lr"], precision=args.precision, seed=1234,
+                               use_graphs=True)
+        replay0 = fused._replay
+
+        def replay_marked(*a, **k):  # step boundaries for phase_report
+            mark("s")
+            n = replay0(*a, **k)
+            mark("e")
+            return n
+
+        fused._replay = replay_marked
         data = fused.device_data(X, users)
         info = {}
         if W > 1:
@@ -145,10 +203,16 @@ def main():
 
         run(args.warmup)
         torch.cuda.synchronize()
+        MARKS.clear()
+        ARMED[0] = True
         t0 = time.perf_counter()
         run(args.steps)
         torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        ARMED[0] = False
+        info["phases"] = phase_report(MARKS)
+        if info["phases"]:
+            info["phases"]["outside_steps_ms_per_step"] = round((el * 1e3 - info["phases"]["run_span_ms"]) / args.steps, 4)
         if fused.dp is not None:
             fused.dp.check()
             info["union_unique_rows_last_step"] = int(fused.dp.merged.n_unique.item())
@@ -156,7 +220,8 @@ def main():
             L = fused.dp.L
             info["allgather_recv_bytes_per_step"] = int((W - 1) * (4 * (L - fused.layout.n_small) + 4 * fused.layout.n_small
                                                                  + 4 * B * H))
-        out = {"probe": "dp_emul", "workload": args.workload, "world": W, "B": B, "steps": args.steps,
+        out = {"probe": "dp_emul", "workload": args.workload, "precision": args.precision, "world": W, "B": B,
+               "steps": args.steps,
                "ms_per_step": round(el / args.steps * 1e3, 4), **info}
         print(json.dumps(out), flush=True)
         del fused, model, data
