@@ -530,6 +530,17 @@ int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, const float
                     int64_t R, int64_t K, int32_t* idx, float* val, int32_t* flag, void* ws,
                     size_t ws_bytes, void* stream);
 
+/* The 99-negative protocol's negatives, host only, draw for draw numpy's: per test row r, the items
+ * neither in row users[r] of the training CSR (row_ptr / col_idx) nor tests[r], ascending ("available",
+ * src/ml/evaluate.py:159-165); all of them when fewer than n_neg (counts[r] = that number, no draw), else
+ * np.random.choice(available, n_neg, replace=False) (:166-170) = available[permutation(len)[:n_neg]] of the
+ * legacy RandomState, counts[r] = n_neg. mt_key [624] / mt_pos: numpy's MT19937 state
+ * (np.random.get_state()[1:3]), advanced in place as the per-row choices in row order would leave it.
+ * out [n_rows, n_neg]. */
+int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const int64_t* row_ptr, const int32_t* col_idx,
+                          int64_t n_items, const int32_t* users, const int32_t* tests, int64_t n_rows,
+                          int32_t n_neg, int32_t* out, int32_t* counts);
+
 /* ---------------------------------------------------- data artifacts (host) -- */
 /* A host CSR plus the file's users, allocated by hvae_read_interactions and
  * released by hvae_host_csr_free. */

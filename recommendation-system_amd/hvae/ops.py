@@ -501,3 +501,29 @@ def topk_fused(U: torch.Tensor, E_img: "DecoderImage", E32: torch.Tensor, e32_ma
         idx.index_copy_(0, bad, i2)
         val.index_copy_(0, bad, v2)
     return (idx, val, flag) if with_flags else (idx, val)
+
+
+def negatives_legacy(indptr, indices, n_items: int, users, tests, n_neg: int):
+    """The 99-negative protocol's negatives for test rows (users[r], tests[r]) over a training CSR
+    (indptr / indices), drawn by libhvae from numpy's global legacy RandomState exactly as the reference's
+    per-row np.random.choice(available, n_neg, replace=False) would (src/ml/evaluate.py:159-170), which
+    leaves the global state where those calls would have (hvae_negatives_legacy). Returns a list of int64
+    arrays, one per row (shorter where fewer than n_neg items are available)."""
+    import numpy as np
+    indptr = np.ascontiguousarray(indptr, dtype=np.int64)
+    indices = np.ascontiguousarray(indices, dtype=np.int32)
+    users = np.ascontiguousarray(users, dtype=np.int32)
+    tests = np.ascontiguousarray(tests, dtype=np.int32)
+    R = len(users)
+    st = np.random.get_state(legacy=True)
+    if st[0] != "MT19937":
+        raise RuntimeError(f"negatives_legacy: numpy global bit generator {st[0]}, not MT19937")
+    key = np.array(st[1], dtype=np.uint32, copy=True)
+    pos = np.array([st[2]], dtype=np.int32)
+    out = np.empty((R, n_neg), dtype=np.int32)
+    counts = np.empty(R, dtype=np.int32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    check(lib().hvae_negatives_legacy(p(key), p(pos), p(indptr), p(indices), int(n_items), p(users), p(tests), R,
+                                      int(n_neg), p(out), p(counts)), "hvae_negatives_legacy")
+    np.random.set_state((st[0], key, int(pos[0]), st[3], st[4]))
+    return [out[r, :counts[r]].astype(np.int64) for r in range(R)]

@@ -8,7 +8,8 @@ scores per row (99-negative protocol; hvae_score_candidates + hvae_rank_first)
 or the full fp32 score matrix + exact top-K with seen items masked
 (full-ranking protocol; hvae_gemm_f32 + hvae_topk). Negatives are drawn with
 np.random.choice(available, n, replace=False) exactly as the reference does
-(:159-170), so the protocol's sampling distribution is unchanged.
+(:159-170) -- draw for draw from numpy's global stream, by a native sampler over all rows at once
+(hvae_negatives_legacy) -- so the negatives are the reference's.
 """
 from __future__ import annotations
 
@@ -181,13 +182,20 @@ class RecommendationEvaluator:
         return {k: {n: float(v[0]) for n, v in m[k].items()} for k in k_values}
 
     def _sample_negatives(self, user_idx: int, test_item_idx: int, n_negatives: int) -> np.ndarray:
-        """The reference's sampler (evaluate.py:159-170), unchanged."""
-        seen = set(self.interaction_matrix[user_idx].indices)
-        mask = np.ones(self.n_items, dtype=bool)
-        mask[list(seen)] = False
-        mask[test_item_idx] = False
-        available = np.where(mask)[0]
-        return available if len(available) < n_negatives else np.random.choice(available, n_negatives, replace=False)
+        """The reference's sampler (evaluate.py:159-170): one row of _sample_negatives_rows."""
+        return self._sample_negatives_rows([user_idx], [test_item_idx], n_negatives)[0]
+
+    def _sample_negatives_rows(self, users, tests, n_negatives: int) -> list[np.ndarray]:
+        """The reference's per-row np.random.choice(available, n, replace=False) over all rows in one native
+        call (hvae_negatives_legacy): the same draws from numpy's global stream, in row order, which it leaves
+        where the per-row calls would."""
+        im = self.interaction_matrix
+        if getattr(self, "_neg_csr", None) is None or self._neg_csr[0] is not im:
+            im = im.tocsr()
+            self._neg_csr = (self.interaction_matrix, np.ascontiguousarray(im.indptr, dtype=np.int64),
+                             np.ascontiguousarray(im.indices, dtype=np.int32))
+        _, indptr, indices = self._neg_csr
+        return ops.negatives_legacy(indptr, indices, self.n_items, users, tests, n_negatives)
 
     def _ranks(self, users: np.ndarray, tests: np.ndarray, negatives: list[np.ndarray]) -> np.ndarray:
         """0-based rank of the test item among [test] + negatives, per row (batched on the device)."""
@@ -229,14 +237,13 @@ class RecommendationEvaluator:
         logger.info(f"Evaluating with negative sampling ({n_negatives} negatives)...")
         if self.group is not None:  # every rank draws every row's negatives from the same stream
             np.random.seed(broadcast_seed(self.group, self.device))
-        users, tests, negs = [], [], []
+        users, tests = [], []
         for user_id, item_id in zip(test_df["user_id"].tolist(), test_df["asin"].tolist()):
             if user_id not in self.user_to_idx or item_id not in self.item_to_idx:
                 continue
-            u, t = self.user_to_idx[user_id], self.item_to_idx[item_id]
-            users.append(u)
-            tests.append(t)
-            negs.append(self._sample_negatives(u, t, n_negatives))
+            users.append(self.user_to_idx[user_id])
+            tests.append(self.item_to_idx[item_id])
+        negs = self._sample_negatives_rows(users, tests, n_negatives)
         all_metrics = {k: {"recall": [], "ndcg": [], "hit_ratio": []} for k in k_values}
         sl = self._shard(len(users))
         if len(users[sl]):

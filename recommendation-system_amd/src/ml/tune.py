@@ -94,14 +94,13 @@ def evaluate_config_on_val(model, train_matrix: csr_matrix, val_df: pd.DataFrame
     """
     k_values = k_values or [10]
     ev = RecommendationEvaluator(model, train_matrix, user_to_idx, item_to_idx, device)
-    users, tests, negs = [], [], []
+    users, tests = [], []
     for user_id, item_id in zip(val_df["user_id"].tolist(), val_df["asin"].tolist()):
         if user_id not in user_to_idx or item_id not in item_to_idx:
             continue
-        u, t = user_to_idx[user_id], item_to_idx[item_id]
-        users.append(u)
-        tests.append(t)
-        negs.append(ev._sample_negatives(u, t, n_negatives))
+        users.append(user_to_idx[user_id])
+        tests.append(item_to_idx[item_id])
+    negs = ev._sample_negatives_rows(users, tests, n_negatives)
     if not users:
         return {f"{m}@{k}": 0.0 for k in k_values for m in ("recall", "ndcg", "hit_ratio")}
     rank = ev._ranks(np.array(users), np.array(tests), negs)

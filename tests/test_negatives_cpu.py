@@ -1,0 +1,66 @@
+"""The native 99-negative sampler (hvae_negatives_legacy, host only) against numpy itself: the reference's
+per-row draw (src/ml/evaluate.py:159-170, restated below as the reference writes it) from the same global
+seed must give the same negatives row for row, and leave numpy's global stream where the per-row calls leave
+it. Runs on the CPU (the function does no device work)."""
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "recommendation-system_amd"))
+
+
+def _reference_negatives(X, users, tests, n_neg):
+    out = []
+    for u, t in zip(users, tests):
+        seen = set(X[u].indices)
+        mask = np.ones(X.shape[1], dtype=bool)
+        mask[list(seen)] = False
+        mask[t] = False
+        available = np.where(mask)[0]
+        out.append(available if len(available) < n_neg else np.random.choice(available, n_neg, replace=False))
+    return out
+
+
+@pytest.mark.parametrize("n_users,n_items,density,seed", [(40, 500, 0.05, 1), (30, 120, 0.3, 2), (25, 101, 0.0, 3),
+                                                          (20, 2000, 0.01, 4), (12, 60, 0.5, 5),
+                                                          (90, 300_000, 0.00002, 6)])
+def test_negatives_match_numpy(n_users, n_items, density, seed):
+    """Row for row against the reference's draw; the last case spans three of the sampler's row chunks
+    (2^25 / 300,000 = 111 rows each), so its pipelined passes hand the stream across chunk boundaries."""
+    from hvae import ops
+    rng = np.random.default_rng(seed)
+    X = sp.random(n_users, n_items, density=density, format="csr", random_state=seed)
+    X.data[:] = 1.0
+    R = 3 * n_users
+    users = rng.integers(0, n_users, R)
+    tests = rng.integers(0, n_items, R)
+    np.random.seed(1000 + seed)
+    ref = _reference_negatives(X, users, tests, 99)
+    after_ref = np.random.random(5)
+    np.random.seed(1000 + seed)
+    got = ops.negatives_legacy(X.indptr, X.indices, n_items, users, tests, 99)
+    after_got = np.random.random(5)
+    assert len(got) == len(ref)
+    for r, (a, b) in enumerate(zip(got, ref)):
+        assert np.array_equal(a, b), f"row {r}: {a[:8]} vs {b[:8]}"
+    assert np.array_equal(after_got, after_ref)  # the global stream continues where the reference leaves it
+
+
+def test_negatives_row_with_duplicate_and_test_in_seen():
+    """A training row holding the test item itself, duplicate entries and an empty row."""
+    from hvae import ops
+    indptr = np.array([0, 4, 4, 6], dtype=np.int64)
+    indices = np.array([3, 3, 7, 150, 0, 1], dtype=np.int32)
+    X = sp.csr_matrix((np.ones(6, np.float32), indices, indptr), shape=(3, 200))
+    users = np.array([0, 1, 2, 0], dtype=np.int32)
+    tests = np.array([7, 199, 0, 3], dtype=np.int32)
+    np.random.seed(7)
+    ref = _reference_negatives(X, users, tests, 99)
+    np.random.seed(7)
+    got = ops.negatives_legacy(indptr, indices, 200, users, tests, 99)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
