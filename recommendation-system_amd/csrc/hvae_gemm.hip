@@ -642,6 +642,223 @@ __device__ __forceinline__ void gemm_fast_block(const GemmP& g, unsigned bx, uns
 template <int BM, int BN>
 constexpr int fast_smem_f4() { return 2 * (FImg<BM>::F4 + FImg<BN>::F4); }
 
+// ------------------------------------------------------------- LDS-DMA path ---
+// The whole-tile case of both kernels above (M % BM == N % BN == 0, k ranges multiples of 32, 16-B aligned
+// operands, ld % 4 == 0 -- every GEMM of the train step at B = 4096), with the operands copied from global
+// memory straight into LDS by buffer_load_dwordx4 ... lds (no register staging, no ds_write), a ring of DNS
+// 32-deep k stages, one barrier per stage. Registers drop to the accumulators and fragments, so blocks of
+// three or four per CU overlap each other's waits (the register-staged kernel ran one wave per SIMD at
+// K = 768: MFMA busy 27 %, profiles/r04_pmc_sq_gemm_syn10m_summary.txt). Per operand and stage the tile is
+// R x 32 floats = R / 8 one-KiB pieces, issued by the block's waves in turn. LDS images:
+//   k-contiguous source ([r][k]: A, or B^T under TB) -- the fast path's image [8 k-chunks][R slots][4 k]:
+//     piece lane i fills slot e = 64 p + i of chunk e / R from row slot^-1(e % R) (the XOR slot map is its own
+//     inverse), so the swizzle costs nothing; fragments as the fast path, one ds_read_b128 per 4 MFMAs;
+//   r-contiguous source ([k][r]: A^T under TA, or B): [32 k][R] floats with the 16-B chunk index XORed by
+//     4 ((k >> 2) & 1), so the k = 16 j + 4 q + s rows a ds_read_b32 lane group reads (q = 0, 1 | 2, 3) land
+//     on disjoint bank halves; one ds_read_b32 per MFMA.
+// The k order (MFMA s of 16-k group j sums k = 16 j + 4 q + s over the lane groups q) and the accumulator
+// layout are the fast path's, so gemm_finish (epilogues, split-K) is shared.
+#ifndef GEMM_DNS
+#define GEMM_DNS 3
+#endif
+constexpr int DNS = GEMM_DNS;
+template <int R>
+struct DImg {
+  static constexpr int BYTES = R * FBK * 4;  // one operand, one stage (either layout)
+  static constexpr int PIECES = BYTES / 1024;
+  static_assert(PIECES % 4 == 0, "pieces per operand and stage: a multiple of the block's 4 waves");
+};
+
+template <int i>
+__device__ __forceinline__ void gemm_dma_piece(uint32_t m0, int voff, __amdgpu_buffer_rsrc_t rsrc, uint32_t soff) {
+  // M0 and soffset come in computed (an s_add in the asm would write SCC behind the compiler's back; the
+  // instruction's offset field would move the LDS destination too); the first piece of a group waits out the
+  // readfirstlane of its SGPR operands
+  if constexpr (i == 0)
+    asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(m0), "v"(voff), "s"(rsrc), "s"(soff) : "memory");
+  else
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :: "s"(m0), "v"(voff), "s"(rsrc), "s"(soff) : "memory");
+}
+
+template <int n>
+__device__ __forceinline__ void gemm_wait_vmcnt() {
+  static_assert(n >= 0 && n < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((n & 15) | (7 << 4) | (15 << 8) | ((n >> 4) << 14));
+}
+
+// lane offsets of this wave's pieces of one operand (bytes from the tile's first element at stage 0)
+template <bool KC, int R>
+__device__ __forceinline__ void dma_lane_offsets(int64_t ld, int (&voff)[DImg<R>::PIECES / 4]) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int u = 0; u < DImg<R>::PIECES / 4; ++u) {
+    const int p = w + 4 * u;
+    const int e = 64 * p + lane;  // float4 slot of the image
+    if (KC) {
+      const int c = e / R, sl = e % R;
+      const int r = FImg<R>::slot(sl);  // the slot map is an involution
+      voff[u] = (int)((int64_t)r * ld * 4 + 16 * c);
+    } else {
+      const int k = e / (R / 4), d = e % (R / 4);
+      const int c = d ^ (4 * ((k >> 2) & 1));
+      voff[u] = (int)((int64_t)k * ld * 4 + 16 * c);
+    }
+  }
+}
+
+template <bool TA, bool TB, int BM, int BN>
+__device__ __forceinline__ void gemm_dma_block(const GemmP& g, unsigned bx, unsigned by, unsigned bz,
+                                               unsigned char* __restrict__ smem) {
+  constexpr int IM = BM / 32, JN = BN / 32;
+  constexpr bool AKC = !TA, BKC = TB;  // k-contiguous sources
+  constexpr int SA = DImg<BM>::BYTES, SB = DImg<BN>::BYTES, STAGE = SA + SB;
+  constexpr int PA = DImg<BM>::PIECES / 4, PB = DImg<BN>::PIECES / 4;  // pieces per wave and stage
+  constexpr int P = PA + PB;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int64_t m0 = (int64_t)by * BM, n0 = (int64_t)bx * BN;
+  const int64_t kb = (int64_t)bz * g.kps;
+  const int nst = (int)((min(g.K, kb + g.kps) - kb) / FBK);
+  const int wm = (w >> 1) * (BM / 2), wn = (w & 1) * (BN / 2);
+  const int q = lane >> 4, c16 = lane & 15;
+  const bool do_rowsum = g.ep.opa_rowsum != nullptr && bx == 0;
+  float rowsum = 0.f;
+
+  // buffer resources over each operand's whole extent (byte offsets stay below 2^31: checked on the host)
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.A), (short)0, 0x7fffffff,
+                                                                      0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.B), (short)0, 0x7fffffff,
+                                                                      0x00020000);
+  int va[PA], vb[PB];
+  dma_lane_offsets<AKC, BM>(g.lda, va);
+  dma_lane_offsets<BKC, BN>(g.ldb, vb);
+  // the tile's origin (stage 0) and the per-stage step, in bytes
+  const int64_t a0 = AKC ? (m0 * g.lda + kb) * 4 : (kb * g.lda + m0) * 4;
+  const int64_t b0 = BKC ? (n0 * g.ldb + kb) * 4 : (kb * g.ldb + n0) * 4;
+  const int64_t ast = AKC ? FBK * 4 : (int64_t)FBK * g.lda * 4;
+  const int64_t bst = BKC ? FBK * 4 : (int64_t)FBK * g.ldb * 4;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)smem;
+
+  auto issue = [&](int st) {
+    const int slot = st % DNS;
+    const uint32_t la = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + slot * STAGE + w * 1024));
+    const uint32_t lb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(lds0 + slot * STAGE + SA + w * 1024));
+    const uint32_t sa = (uint32_t)__builtin_amdgcn_readfirstlane((int)(a0 + st * ast));
+    const uint32_t sb = (uint32_t)__builtin_amdgcn_readfirstlane((int)(b0 + st * bst));
+    gemm_dma_piece<0>(la, va[0], ra, sa);
+#pragma unroll
+    for (int u = 1; u < PA; ++u) gemm_dma_piece<1>(la + 4096u * u, va[u], ra, sa);
+#pragma unroll
+    for (int u = 0; u < PB; ++u) gemm_dma_piece<1>(lb + 4096u * u, vb[u], rb, sb);
+  };
+
+  f32x4 acc[IM][JN];
+#pragma unroll
+  for (int i = 0; i < IM; ++i)
+#pragma unroll
+    for (int j = 0; j < JN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int slot) {
+    const unsigned char* ia = smem + slot * STAGE;
+    const unsigned char* ib = ia + SA;
+    const float4* a4 = reinterpret_cast<const float4*>(ia);
+    const float4* b4 = reinterpret_cast<const float4*>(ib);
+    const float* a1 = reinterpret_cast<const float*>(ia);
+    const float* b1 = reinterpret_cast<const float*>(ib);
+    if (do_rowsum && t < BM) {  // sum_k op(A)[m, k] of this stage, m = m0 + t
+      if (AKC) {
+#pragma unroll
+        for (int c = 0; c < FBK / 4; ++c) {
+          const float4 x = a4[c * BM + FImg<BM>::slot(t)];
+          rowsum += x.x;
+          rowsum += x.y;
+          rowsum += x.z;
+          rowsum += x.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < FBK; ++k) rowsum += a1[k * BM + 4 * ((t >> 2) ^ (4 * ((k >> 2) & 1))) + (t & 3)];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < FBK / 16; ++j) {
+      float4 af[IM], bfr[JN];
+#pragma unroll
+      for (int i = 0; i < IM; ++i) {
+        const int x = wm + c16 + 16 * i;
+        if (AKC) {
+          af[i] = a4[(4 * j + q) * BM + FImg<BM>::slot(x)];
+        } else {
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) {
+            const int k = 16 * j + 4 * q + s2;
+            (&af[i].x)[s2] = a1[k * BM + 4 * ((x >> 2) ^ (4 * ((k >> 2) & 1))) + (x & 3)];
+          }
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < JN; ++n) {
+        const int x = wn + c16 + 16 * n;
+        if (BKC) {
+          bfr[n] = b4[(4 * j + q) * BN + FImg<BN>::slot(x)];
+        } else {
+#pragma unroll
+          for (int s2 = 0; s2 < 4; ++s2) {
+            const int k = 16 * j + 4 * q + s2;
+            (&bfr[n].x)[s2] = b1[k * BN + 4 * ((x >> 2) ^ (4 * ((k >> 2) & 1))) + (x & 3)];
+          }
+        }
+      }
+#pragma unroll
+      for (int s2 = 0; s2 < 4; ++s2)
+#pragma unroll
+        for (int i = 0; i < IM; ++i)
+#pragma unroll
+          for (int n = 0; n < JN; ++n)
+            acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x4f32((&af[i].x)[s2], (&bfr[n].x)[s2], acc[i][n], 0, 0, 0);
+    }
+  };
+
+  // ring: stages 0 .. DNS - 2 in flight before the loop; stage st + DNS - 1 is issued into the slot that
+  // compute(st - 1) freed, right after the barrier that proves every wave is past it
+#pragma unroll
+  for (int u = 0; u < DNS - 1; ++u)
+    if (u < nst) issue(u);
+  for (int st = 0; st < nst; ++st) {
+    if (st + DNS - 2 < nst) gemm_wait_vmcnt<P * (DNS - 2)>();  // this wave's pieces of stage st have landed
+    else gemm_wait_vmcnt<0>();
+    __syncthreads();
+    if (st + DNS - 1 < nst) issue(st + DNS - 1);
+    compute(st % DNS);
+  }
+  gemm_finish<BM, BN>(g, acc, bx, by, bz, do_rowsum, rowsum);
+}
+
+template <int BM, int BN>
+constexpr int dma_smem_bytes() { return DNS * (DImg<BM>::BYTES + DImg<BN>::BYTES); }
+
+template <bool TA, bool TB, int BM, int BN>
+__global__ void __launch_bounds__(256) k_gemm_dma(GemmP g) {
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[dma_smem_bytes<BM, BN>()];
+  gemm_dma_block<TA, TB, BM, BN>(g, blockIdx.x, blockIdx.y, blockIdx.z, smem);
+}
+
+// a layer's backward pair (dW = dY^T X split-K, dX = dY W) both on the LDS-DMA path, in one launch
+template <int BM0, int BM1>
+__global__ void __launch_bounds__(256) k_gemm_dma_pair(GemmP g0, GemmP g1) {
+  constexpr int S0 = dma_smem_bytes<BM0, BM0>(), S1 = dma_smem_bytes<BM1, BM1>();
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[S0 > S1 ? S0 : S1];
+  const unsigned nb0 = g0.gx * g0.gy * g0.gz;
+  unsigned b = blockIdx.x;
+  if (b < nb0) {
+    gemm_dma_block<true, false, BM0, BM0>(g0, b % g0.gx, (b / g0.gx) % g0.gy, b / (g0.gx * g0.gy), smem);
+  } else {
+    b -= nb0;
+    gemm_dma_block<false, false, BM1, BM1>(g1, b % g1.gx, (b / g1.gx) % g1.gy, b / (g1.gx * g1.gy), smem);
+  }
+}
+
 template <bool TA, bool TB, int BM, int BN>
 __global__ void __launch_bounds__(256) k_gemm_fast(GemmP g) {
   __shared__ float4 smem[fast_smem_f4<BM, BN>()];
@@ -824,6 +1041,26 @@ static FastPlan fast_plan(bool ta, bool tb, int64_t M, int64_t N, int64_t K, con
   return f;
 }
 
+// ---- LDS-DMA path plan: the tile (64 or 32) when the problem is whole tiles of it, 0 otherwise. A/B knobs
+// (read at every call): HVAE_GEMM_DMA=0 keeps the register-staged / fast kernels, HVAE_GEMM_DMA_TILE=32|64.
+static int dma_tile(bool ta, bool tb, const GemmP& g) {
+  if (const char* e = ab_getenv("HVAE_GEMM_DMA"))
+    if (std::atoi(e) == 0) return 0;
+  const int64_t M = g.M, N = g.N, K = g.K;
+  if (K == 0 || K % FBK || g.kps % FBK || ((uintptr_t)g.A) % 16 || ((uintptr_t)g.B) % 16 || g.lda % 4 || g.ldb % 4)
+    return 0;
+  const int64_t ea = (ta ? K * g.lda : M * g.lda) * 4, eb = (tb ? N * g.ldb : K * g.ldb) * 4;
+  if (ea >= ((int64_t)1 << 31) || eb >= ((int64_t)1 << 31)) return 0;  // 32-bit buffer offsets
+  int bt = (M % 64 == 0 && N % 64 == 0 && (M / 64) * (N / 64) * (int64_t)g.gz >= 256) ? 64 : 32;
+  if (const char* e = ab_getenv("HVAE_GEMM_DMA_TILE")) bt = std::atoi(e) == 64 ? 64 : 32;
+  if (M % bt || N % bt) return 0;
+  if (g.slab && (M / bt) * (N / bt) > (int64_t)kTicketSlice) return 0;
+  // the weight gradients in 32-square tiles (768 x 128, 256 x 512 over K = 4096) stay on the fast path: 20.5 /
+  // 21.3 us there against 23.0 / 26.9 here (profiles/r05_gemm_dma_trace_ab.jsonl)
+  if (ta && !tb && bt == 32 && !ab_getenv("HVAE_GEMM_DMA_TILE")) return 0;
+  return bt;
+}
+
 static int colsum_parts(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(M, 64), 64)); }
 
 }  // namespace hvae
@@ -929,6 +1166,21 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
                           bt, &f))
     return rc;
   hipStream_t st = as_stream(stream);
+  if (const int dt = dma_tile(trans_a, trans_b, g)) {
+    g.gx = (unsigned)(N / dt);
+    g.gy = (unsigned)(M / dt);
+    dim3 grid(g.gx, g.gy, g.gz);
+    ProbeScope probe("gemm", st);
+#define HVAE_DMA_CALL(TA_, TB_) \
+  (dt == 64 ? (k_gemm_dma<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(g)) : (k_gemm_dma<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(g)))
+    if (!trans_a && !trans_b) HVAE_DMA_CALL(false, false);
+    else if (!trans_a && trans_b) HVAE_DMA_CALL(false, true);
+    else if (trans_a && !trans_b) HVAE_DMA_CALL(true, false);
+    else HVAE_DMA_CALL(true, true);
+#undef HVAE_DMA_CALL
+    HVAE_LAUNCH_CHECK("k_gemm_dma");
+    return HVAE_OK;
+  }
   dim3 grid(g.gx, g.gy, g.gz);
   ProbeScope probe("gemm", st);
   if (f.bm) {  // trans_a && !trans_b (or, under HVAE_GEMM_FAST_SHORT, !trans_a)
@@ -987,6 +1239,21 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
                           x->epi, x->ws, x->ws_bytes, g1, bt1, &f1))
     return rc;
   hipStream_t st = as_stream(stream);
+  {
+    const int d0 = dma_tile(true, false, g0), d1 = dma_tile(false, false, g1);
+    if (d0 && d1 && !(g0.slab && g1.slab)) {  // both on the LDS-DMA path, one launch
+      g0.gx = (unsigned)(g0.N / d0); g0.gy = (unsigned)(g0.M / d0);
+      g1.gx = (unsigned)(g1.N / d1); g1.gy = (unsigned)(g1.M / d1);
+      const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
+      ProbeScope probe("gemm", st);
+      if (d0 == 64 && d1 == 64) k_gemm_dma_pair<64, 64><<<nblk, 256, 0, st>>>(g0, g1);
+      else if (d0 == 64) k_gemm_dma_pair<64, 32><<<nblk, 256, 0, st>>>(g0, g1);
+      else if (d1 == 64) k_gemm_dma_pair<32, 64><<<nblk, 256, 0, st>>>(g0, g1);
+      else k_gemm_dma_pair<32, 32><<<nblk, 256, 0, st>>>(g0, g1);
+      HVAE_LAUNCH_CHECK("k_gemm_dma_pair");
+      return HVAE_OK;
+    }
+  }
   if (f0.bm || f1.bm) {
     if (!f0.bm || f1.bm || (g0.slab && g1.slab)) {  // not (fast dW, register-staged dX): two launches
       if (int rc = gemm_desc(w, stream)) return rc;

@@ -32,7 +32,9 @@ def _maxrel(a, b):
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (7, 13, 5), (64, 64, 64), (130, 67, 300), (37, 384, 4096),
                                    (384, 384, 4096), (4096, 128, 512),
                                    # weight-gradient fast path (trans_a, K >= 1024): 32- and 64-square tiles
-                                   (768, 768, 4096), (256, 64, 2048)])
+                                   (768, 768, 4096), (256, 64, 2048),
+                                   # whole 64-tiles (the LDS-DMA path's 64 x 64 instance)
+                                   (4096, 768, 256)])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 def test_gemm_f32(ops, hip_device, M, N, K, ta, tb):
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
@@ -47,10 +49,11 @@ def test_gemm_f32(ops, hip_device, M, N, K, ta, tb):
     assert _maxrel(out, ref) < 2e-5 * max(1.0, math.sqrt(K) / 8)
 
 
-def test_gemm_epilogues(ops, hip_device):
+@pytest.mark.parametrize("M,N,K", [(50, 70, 33), (128, 96, 64)])
+def test_gemm_epilogues(ops, hip_device, M, N, K):
+    """The fused epilogues on a ragged shape (register-staged kernel) and a whole-tile one (LDS-DMA path)."""
     from hvae import _lib
     g = torch.Generator().manual_seed(3)
-    M, N, K = 50, 70, 33
     A, W, bias = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)
     mult = ((torch.rand(M, N, generator=g) >= 0.3).float() / 0.7)
     Ad, Wd, bd, md = (t.to(hip_device) for t in (A, W, bias, mult))
@@ -61,7 +64,7 @@ def test_gemm_epilogues(ops, hip_device):
     assert _maxrel(pre, ref_pre) < 1e-5
     assert _maxrel(out, R.gelu(ref_pre) * mult) < 1e-5
     # backward epilogue: c * mult * gelu'(pre)
-    G, W2 = torch.randn(M, 40, generator=g), torch.randn(40, N, generator=g)
+    G, W2 = torch.randn(M, 64, generator=g), torch.randn(64, N, generator=g)
     epi2 = ops.epilogue(_lib.EPI_GELU_DROP_BWD, pre_in=pre, p_drop=0.3, drop_mult=md, train=True)
     out2 = ops.gemm(G.to(hip_device), W2.to(hip_device), epi=epi2)
     x = ref_pre.clone().requires_grad_(True)
