@@ -659,7 +659,9 @@ constexpr int fast_smem_f4() { return 2 * (FImg<BM>::F4 + FImg<BN>::F4); }
 // The k order (MFMA s of 16-k group j sums k = 16 j + 4 q + s over the lane groups q) and the accumulator
 // layout are the fast path's, so gemm_finish (epilogues, split-K) is shared.
 #ifndef GEMM_DNS
-#define GEMM_DNS 3
+#define GEMM_DNS 2  // ring depth: 2 stages (32 KiB a 64 x 64 block, five blocks per CU) against 3 / 4 at the
+                    // Syn-10M shapes: 269 / 276 / 292 us summed (profiles/r05_gemm_dma_tuning.txt) -- more blocks
+                    // per CU hide the fill better than a deeper ring in fewer blocks
 #endif
 constexpr int DNS = GEMM_DNS;
 template <int R>
@@ -1030,7 +1032,9 @@ static FastPlan fast_plan(bool ta, bool tb, int64_t M, int64_t N, int64_t K, con
   if (M % bt || N % bt) return f;
   const int64_t tiles = (M / bt) * (N / bt);
   int64_t s = 1;
-  if (K > 1024) s = std::max<int64_t>(1, std::min<int64_t>((512 + tiles - 1) / tiles, K / 256));
+  // ~512 blocks in 32-square tiles; in 64-square ones (768 x 768 at the Syn-10M shard) ~1024, which the
+  // LDS-DMA path's five blocks per CU can hold: 768x768x4096 65.9 us with 8 splits against 69.4 with 4
+  if (K > 1024) s = std::max<int64_t>(1, std::min<int64_t>(((bt == 64 ? 1024 : 512) + tiles - 1) / tiles, K / 256));
   if (const char* t = ab_getenv("HVAE_GEMM_FAST_SPLITS")) s = std::max(1, std::atoi(t));
   s = std::min<int64_t>(s, 64);
   if (s > 1 && tiles > (int64_t)kTicketSlice) s = 1;
@@ -1041,9 +1045,11 @@ static FastPlan fast_plan(bool ta, bool tb, int64_t M, int64_t N, int64_t K, con
   return f;
 }
 
-// ---- LDS-DMA path plan: the tile (64 or 32) when the problem is whole tiles of it, 0 otherwise. A/B knobs
-// (read at every call): HVAE_GEMM_DMA=0 keeps the register-staged / fast kernels, HVAE_GEMM_DMA_TILE=32|64.
-static int dma_tile(bool ta, bool tb, const GemmP& g) {
+// ---- LDS-DMA path plan: the tile when the problem is whole tiles of it, 0 otherwise: 64 (64 x 64), 32 (32 x 32)
+// or kTile6432 (64 x 32, single launches only). A/B knobs (read at every call): HVAE_GEMM_DMA=0 keeps the
+// register-staged / fast kernels, HVAE_GEMM_DMA_TILE=32|64|6432 forces a tile.
+constexpr int kTile6432 = 6432;
+static int dma_tile(bool ta, bool tb, const GemmP& g, bool pair = false) {
   if (const char* e = ab_getenv("HVAE_GEMM_DMA"))
     if (std::atoi(e) == 0) return 0;
   const int64_t M = g.M, N = g.N, K = g.K;
@@ -1051,10 +1057,18 @@ static int dma_tile(bool ta, bool tb, const GemmP& g) {
     return 0;
   const int64_t ea = (ta ? K * g.lda : M * g.lda) * 4, eb = (tb ? N * g.ldb : K * g.ldb) * 4;
   if (ea >= ((int64_t)1 << 31) || eb >= ((int64_t)1 << 31)) return 0;  // 32-bit buffer offsets
-  int bt = (M % 64 == 0 && N % 64 == 0 && (M / 64) * (N / 64) * (int64_t)g.gz >= 256) ? 64 : 32;
-  if (const char* e = ab_getenv("HVAE_GEMM_DMA_TILE")) bt = std::atoi(e) == 64 ? 64 : 32;
-  if (M % bt || N % bt) return 0;
-  if (g.slab && (M / bt) * (N / bt) > (int64_t)kTicketSlice) return 0;
+  // 64 x 64 from two blocks per CU; 64 x 32 where that doubles one block per CU to two; else 64 x 64 at one
+  // block per CU; else 32 x 32
+  const int64_t t64 = (M % 64 == 0 && N % 64 == 0) ? (M / 64) * (N / 64) * (int64_t)g.gz : 0;
+  const int64_t t6432 = (M % 64 == 0 && N % 32 == 0) ? (M / 64) * (N / 32) * (int64_t)g.gz : 0;
+  int bt = t64 >= 512 ? 64 : (!pair && !ta && t6432 >= 512) ? kTile6432 : t64 >= 256 ? 64 : 32;
+  if (const char* e = ab_getenv("HVAE_GEMM_DMA_TILE")) {
+    const int v = std::atoi(e);
+    bt = v == 64 ? 64 : (v == kTile6432 && !pair) ? kTile6432 : 32;
+  }
+  const int bm = bt == kTile6432 ? 64 : bt, bn = bt == kTile6432 ? 32 : bt;
+  if (M % bm || N % bn) return 0;
+  if (g.slab && (M / bm) * (N / bn) > (int64_t)kTicketSlice) return 0;
   // the weight gradients in 32-square tiles (768 x 128, 256 x 512 over K = 4096) stay on the fast path: 20.5 /
   // 21.3 us there against 23.0 / 26.9 here (profiles/r05_gemm_dma_trace_ab.jsonl)
   if (ta && !tb && bt == 32 && !ab_getenv("HVAE_GEMM_DMA_TILE")) return 0;
@@ -1167,12 +1181,15 @@ extern "C" int hvae_gemm_f32(int trans_a, int trans_b, int64_t M, int64_t N, int
     return rc;
   hipStream_t st = as_stream(stream);
   if (const int dt = dma_tile(trans_a, trans_b, g)) {
-    g.gx = (unsigned)(N / dt);
-    g.gy = (unsigned)(M / dt);
+    const int bm = dt == kTile6432 ? 64 : dt, bn = dt == kTile6432 ? 32 : dt;
+    g.gx = (unsigned)(N / bn);
+    g.gy = (unsigned)(M / bm);
     dim3 grid(g.gx, g.gy, g.gz);
     ProbeScope probe("gemm", st);
-#define HVAE_DMA_CALL(TA_, TB_) \
-  (dt == 64 ? (k_gemm_dma<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(g)) : (k_gemm_dma<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(g)))
+#define HVAE_DMA_CALL(TA_, TB_)                                                       \
+  (dt == 64 ? (k_gemm_dma<TA_, TB_, 64, 64><<<grid, 256, 0, st>>>(g))                \
+   : dt == kTile6432 ? (k_gemm_dma<TA_, TB_, 64, 32><<<grid, 256, 0, st>>>(g))       \
+                     : (k_gemm_dma<TA_, TB_, 32, 32><<<grid, 256, 0, st>>>(g)))
     if (!trans_a && !trans_b) HVAE_DMA_CALL(false, false);
     else if (!trans_a && trans_b) HVAE_DMA_CALL(false, true);
     else if (trans_a && !trans_b) HVAE_DMA_CALL(true, false);
@@ -1240,8 +1257,14 @@ extern "C" int hvae_gemm_f32_pair(const hvae_gemm_desc* w, const hvae_gemm_desc*
     return rc;
   hipStream_t st = as_stream(stream);
   {
-    const int d0 = dma_tile(true, false, g0), d1 = dma_tile(false, false, g1);
-    if (d0 && d1 && !(g0.slab && g1.slab)) {  // both on the LDS-DMA path, one launch
+    const int d0 = dma_tile(true, false, g0, true), d1 = dma_tile(false, false, g1, true);
+    if ((d0 != 0) != (d1 != 0) || (d0 && d1 && g0.slab && g1.slab)) {
+      // one half on the LDS-DMA path, the other not: two launches, so that each half runs the kernel its own
+      // hvae_gemm_f32 call would (the pair stays bitwise the two launches)
+      if (int rc = gemm_desc(w, stream)) return rc;
+      return gemm_desc(x, stream);
+    }
+    if (d0 && d1) {  // both on the LDS-DMA path, one launch
       g0.gx = (unsigned)(g0.N / d0); g0.gy = (unsigned)(g0.M / d0);
       g1.gx = (unsigned)(g1.N / d1); g1.gy = (unsigned)(g1.M / d1);
       const unsigned nblk = g0.gx * g0.gy * g0.gz + g1.gx * g1.gy * g1.gz;
