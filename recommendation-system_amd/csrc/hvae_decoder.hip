@@ -1108,10 +1108,17 @@ constexpr int kFinEB = 16;  // CSR entries per batch of the finalize's sparse-te
 
 // GRP: the merge of many split partials (> 8) by split groups (memory-level parallelism at small
 // batches); otherwise one thread per column walks the splits in order (fewer registers, more blocks
-// per CU at large batches)
-template <bool GRP>
+// per CU at large batches). V4 (every row operand 16-B aligned, as the host checks): thread t owns the four
+// columns 4 t .. 4 t + 3 and moves them as one 16-B load / store (the scalar form's thread owns t + 256 k and
+// issues four times the load instructions for the same bytes: 2.2-3.1 TB/s, profiles/pmc_syn1m.json)
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void f4_fma(float4& acc, float w, const float4& v) {
+  acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+}
+template <bool GRP, bool V4>
 __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   __shared__ float wsh[kMaxSplits];
+  __shared__ __attribute__((aligned(16))) float obuf[V4 ? 1024 : 4];  // exact fixup's columns -> V4 layout
   __shared__ __attribute__((aligned(16))) float opart[GRP ? 8 * 1024 : 4];  // per-split-group O sums
   __shared__ float red[4];
   __shared__ float pbuf[256];
@@ -1174,7 +1181,22 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     L = block_sum<256>(L, red);  // its barriers also publish wsh and any_flag
     lse_b = M + logf(L);
     const float inv = 1.0f / L;
-    if (a.pO && !GRP) {
+    if (V4 && a.pO && !GRP) {  // sum_s w_s O_s in split order, 8 splits' 16-B loads in flight
+      const bool act = 4 * tid < D;
+      float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      int s0 = 0;
+      for (; s0 + 8 <= nsp; s0 += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = act ? ld4(a.pO + prow(s0 + j) * D + 4 * tid) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f4_fma(acc4, wsh[s0 + j], v[j]);
+      }
+      for (; s0 < nsp; ++s0)
+        if (act) f4_fma(acc4, wsh[s0], ld4(a.pO + prow(s0) * D + 4 * tid));
+      o[0] = acc4.x * inv; o[1] = acc4.y * inv; o[2] = acc4.z * inv; o[3] = acc4.w * inv;
+    }
+    if (!V4 && a.pO && !GRP) {
       // sum_s w_s O_s in split order; loads batched 8 splits x 4 columns deep so that
       // they are in flight together (a one-at-a-time chain is HBM-latency bound)
       const int nk = (int)min<int64_t>(4, (D - tid + 255) / 256);
@@ -1242,36 +1264,71 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
         if (q < nq) reinterpret_cast<float4*>(opart + sg * 1024)[q] = acc4[i];
       }
       __syncthreads();
+      if constexpr (V4) {
+        if (4 * tid < D) {
+          float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int64_t d = tid + 256 * k;
-        float t = 0.f;
-        if (d < D) {
-#pragma unroll
-          for (int g = 0; g < SG; ++g) t += opart[g * 1024 + d];
+          for (int g = 0; g < SG; ++g) {
+            const float4 v = reinterpret_cast<const float4*>(opart + g * 1024)[tid];
+            t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+          }
+          o[0] = t.x * inv; o[1] = t.y * inv; o[2] = t.z * inv; o[3] = t.w * inv;
         }
-        o[k] = t * inv;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t d = tid + 256 * k;
+          float t = 0.f;
+          if (d < D) {
+#pragma unroll
+            for (int g = 0; g < SG; ++g) t += opart[g * 1024 + d];
+          }
+          o[k] = t * inv;
+        }
       }
     }
   } else {
     if (a.flag && a.flag[b]) any_flag = 1;
     lse_b = a.lse_in[b];
     if (a.O_in) {
+      if constexpr (V4) {
+        if (4 * tid < D) {
+          const float4 v = ld4(a.O_in + b * D + 4 * tid);
+          o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+        }
+      } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int64_t d = tid + 256 * k;
-        if (d < D) o[k] = a.O_in[b * D + d];
+        for (int k = 0; k < 4; ++k) {
+          const int64_t d = tid + 256 * k;
+          if (d < D) o[k] = a.O_in[b * D + d];
+        }
       }
     }
     __syncthreads();
   }
-  if (any_flag) lse_b = exact_user(b, a.U, a.ldu, a.Ebf, a.N, D, o, red, pbuf);  // rare, block-uniform
+  if (any_flag) {  // rare, block-uniform
+    lse_b = exact_user(b, a.U, a.ldu, a.Ebf, a.N, D, o, red, pbuf);  // columns tid + 256 k
+    if constexpr (V4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (tid + 256 * k < D) obuf[tid + 256 * k] = o[k];
+      __syncthreads();
+      if (4 * tid < D) {
+        const float4 v = reinterpret_cast<const float4*>(obuf)[tid];
+        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
+      }
+    }
+  }
   if (tid == 0) a.lse_out[b] = lse_b;
   if (a.O_out) {
+    if constexpr (V4) {
+      if (4 * tid < D) *reinterpret_cast<float4*>(a.O_out + b * D + 4 * tid) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t d = tid + 256 * k;
-      if (d < D) a.O_out[b * D + d] = o[k];
+      for (int k = 0; k < 4; ++k) {
+        const int64_t d = tid + 256 * k;
+        if (d < D) a.O_out[b * D + d] = o[k];
+      }
     }
   }
   if (!a.row_ptr) return;
@@ -1289,13 +1346,23 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
       }
     }
     float ev[kFinEB][4];
+    if constexpr (V4) {
+      const bool act = 4 * tid < D;
 #pragma unroll
-    for (int u = 0; u < kFinEB; ++u)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int64_t d = tid + 256 * k;
-        ev[u][k] = (e0 + u < sp_end && d < D) ? a.E32[(int64_t)sp_j[u] * D + d] : 0.f;
+      for (int u = 0; u < kFinEB; ++u) {
+        const float4 v = (e0 + u < sp_end && act) ? ld4(a.E32 + (int64_t)sp_j[u] * D + 4 * tid)
+                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        ev[u][0] = v.x; ev[u][1] = v.y; ev[u][2] = v.z; ev[u][3] = v.w;
       }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kFinEB; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int64_t d = tid + 256 * k;
+          ev[u][k] = (e0 + u < sp_end && d < D) ? a.E32[(int64_t)sp_j[u] * D + d] : 0.f;
+        }
+    }
 #pragma unroll
     for (int u = 0; u < kFinEB; ++u) {
       if (e0 + u >= sp_end) break;
@@ -1305,10 +1372,17 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     }
   }
   float dot = 0.f;
+  if constexpr (V4) {
+    if (4 * tid < D) {
+      const float4 uu = ld4(a.U + b * a.ldu + 4 * tid);
+      dot = uu.x * acc[0] + uu.y * acc[1] + uu.z * acc[2] + uu.w * acc[3];
+    }
+  } else {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int64_t d = tid + 256 * k;
-    if (d < D) dot += a.U[b * a.ldu + d] * acc[k];
+    for (int k = 0; k < 4; ++k) {
+      const int64_t d = tid + 256 * k;
+      if (d < D) dot += a.U[b * a.ldu + d] * acc[k];
+    }
   }
   dot = block_sum<256>(dot, red);
   if (a.recon_rows && tid == 0) {
@@ -1316,10 +1390,17 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     else a.recon_rows[b] = n * lse_b - dot;
   }
   if (a.dU) {
+    if constexpr (V4) {
+      if (4 * tid < D)
+        *reinterpret_cast<float4*>(a.dU + b * D + 4 * tid) =
+            make_float4(a.scale * (n * o[0] - acc[0]), a.scale * (n * o[1] - acc[1]), a.scale * (n * o[2] - acc[2]),
+                        a.scale * (n * o[3] - acc[3]));
+    } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t d = tid + 256 * k;
-      if (d < D) a.dU[b * D + d] = a.scale * (n * o[k] - acc[k]);
+      for (int k = 0; k < 4; ++k) {
+        const int64_t d = tid + 256 * k;
+        if (d < D) a.dU[b * D + d] = a.scale * (n * o[k] - acc[k]);
+      }
     }
   }
   if (a.loss3 && last_block_arrives(a.ticket, gridDim.x))
@@ -1783,6 +1864,12 @@ static int decoder_finalize(FinArgs& a, const float* U, int64_t ldu, const void*
                             float* recon_rows, float* dU, const float* kl_rows, float beta, const float* beta_dev,
                             float* loss3, double* accum3, bool grouped, hipStream_t st);
 
+// the finalize's 16-B column form: every row operand it reads or writes starts 16-B aligned
+static bool fin_v4(const FinArgs& a) {
+  auto al = [](const void* p) { return ((uintptr_t)p % 16) == 0; };
+  return a.D % 4 == 0 && a.ldu % 4 == 0 && al(a.U) && al(a.pO) && al(a.O_in) && al(a.O_out) && al(a.E32) && al(a.dU);
+}
+
 // flash sweep + finalize; csr / recon_rows / dU optional
 static int decoder_run(int dtype, const float* U, int64_t ldu, const void* E, const float* e_maxnorm,
                        const float* E32, const hvae_csr_batch* x, int64_t nb, int64_t N, int64_t D, float scale,
@@ -1895,8 +1982,14 @@ static int decoder_finalize(FinArgs& a, const float* U, int64_t ldu, const void*
     if (!(a.ticket = ticket_slice())) return HVAE_ERR_HIP;
   }
   ProbeScope probe("decoder_finalize", st);
-  if (grouped) k_dec_finalize<true><<<(unsigned)nb, 256, 0, st>>>(a);
-  else k_dec_finalize<false><<<(unsigned)nb, 256, 0, st>>>(a);
+  const bool v4 = fin_v4(a);
+  if (grouped) {
+    if (v4) k_dec_finalize<true, true><<<(unsigned)nb, 256, 0, st>>>(a);
+    else k_dec_finalize<true, false><<<(unsigned)nb, 256, 0, st>>>(a);
+  } else {
+    if (v4) k_dec_finalize<false, true><<<(unsigned)nb, 256, 0, st>>>(a);
+    else k_dec_finalize<false, false><<<(unsigned)nb, 256, 0, st>>>(a);
+  }
   HVAE_LAUNCH_CHECK("k_dec_finalize");
   return HVAE_OK;
 }
@@ -1937,7 +2030,8 @@ extern "C" int hvae_decoder_bwd(const hvae_csr_batch* x, const float* U, int64_t
   a.lse_out = const_cast<float*>(lse);  // rewritten with the same value
   a.recon_rows = recon_rows;
   a.dU = dU;
-  k_dec_finalize<false><<<(unsigned)x->nb, 256, 0, as_stream(stream)>>>(a);
+  if (fin_v4(a)) k_dec_finalize<false, true><<<(unsigned)x->nb, 256, 0, as_stream(stream)>>>(a);
+  else k_dec_finalize<false, false><<<(unsigned)x->nb, 256, 0, as_stream(stream)>>>(a);
   HVAE_LAUNCH_CHECK("k_dec_finalize");
   return HVAE_OK;
 }
