@@ -1104,6 +1104,9 @@ struct FinArgs {
   int v6_upb, v6_nub, v6_S, v6_main, v6_P;
 };
 
+#ifndef FIN_EB_V4
+#define FIN_EB_V4 8  // 16-B form: 8 entries x 16 B in flight per thread (59 VGPRs, 7 waves per SIMD) beat 16 (99, 4): Syn-1M shape 33.5 -> 27.9 us, Syn-10M 45.5 -> 39.8 (profiles/r05_finalize_eb_ab.jsonl)
+#endif
 constexpr int kFinEB = 16;  // CSR entries per batch of the finalize's sparse-term loads
 
 // GRP: the merge of many split partials (> 8) by split groups (memory-level parallelism at small
@@ -1117,6 +1120,7 @@ __device__ __forceinline__ void f4_fma(float4& acc, float w, const float4& v) {
 }
 template <bool GRP, bool V4>
 __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
+  constexpr int EB = V4 ? FIN_EB_V4 : kFinEB;  // CSR entries per batch of the sparse-term loads
   __shared__ float wsh[kMaxSplits];
   __shared__ __attribute__((aligned(16))) float obuf[V4 ? 1024 : 4];  // exact fixup's columns -> V4 layout
   __shared__ __attribute__((aligned(16))) float opart[GRP ? 8 * 1024 : 4];  // per-split-group O sums
@@ -1126,17 +1130,17 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   const int64_t b = blockIdx.x;
   const int tid = threadIdx.x;
   const int64_t D = a.D;
-  // the batch row's CSR entries: located and the first kFinEB fetched now, under the merge's loads
+  // the batch row's CSR entries: located and the first EB fetched now, under the merge's loads
   int64_t sp_beg = 0, sp_end = 0;
-  int sp_j[kFinEB];
-  float sp_x[kFinEB];
+  int sp_j[EB];
+  float sp_x[EB];
   if (a.row_ptr) {
     const int64_t r = batch_row(a.rows, a.rows_offset, b);
     sp_beg = a.row_ptr[r];
     sp_end = a.row_ptr[r + 1];
   }
 #pragma unroll
-  for (int u = 0; u < kFinEB; ++u) {
+  for (int u = 0; u < EB; ++u) {
     const int64_t e = sp_beg + u;
     sp_j[u] = e < sp_end ? a.col_idx[e] : 0;
     sp_x[u] = e < sp_end ? a.vals[e] : 0.f;
@@ -1336,27 +1340,27 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   // E loads in flight together (the first chunk's indices were fetched before the merge)
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float n = 0.f;
-  for (int64_t e0 = sp_beg; e0 < sp_end; e0 += kFinEB) {
+  for (int64_t e0 = sp_beg; e0 < sp_end; e0 += EB) {
     if (e0 != sp_beg) {
 #pragma unroll
-      for (int u = 0; u < kFinEB; ++u) {
+      for (int u = 0; u < EB; ++u) {
         const int64_t e = e0 + u;
         sp_j[u] = e < sp_end ? a.col_idx[e] : 0;
         sp_x[u] = e < sp_end ? a.vals[e] : 0.f;
       }
     }
-    float ev[kFinEB][4];
+    float ev[EB][4];
     if constexpr (V4) {
       const bool act = 4 * tid < D;
 #pragma unroll
-      for (int u = 0; u < kFinEB; ++u) {
+      for (int u = 0; u < EB; ++u) {
         const float4 v = (e0 + u < sp_end && act) ? ld4(a.E32 + (int64_t)sp_j[u] * D + 4 * tid)
                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
         ev[u][0] = v.x; ev[u][1] = v.y; ev[u][2] = v.z; ev[u][3] = v.w;
       }
     } else {
 #pragma unroll
-      for (int u = 0; u < kFinEB; ++u)
+      for (int u = 0; u < EB; ++u)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int64_t d = tid + 256 * k;
@@ -1364,7 +1368,7 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
         }
     }
 #pragma unroll
-    for (int u = 0; u < kFinEB; ++u) {
+    for (int u = 0; u < EB; ++u) {
       if (e0 + u >= sp_end) break;
       n += sp_x[u];
 #pragma unroll
