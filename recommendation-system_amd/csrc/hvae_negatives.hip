@@ -14,7 +14,6 @@
 // gets it back advanced exactly as the per-row choices would have left it, so the negatives -- and every
 // later draw of the process -- are the reference's. tests/test_negatives_cpu.py checks both against numpy.
 #include <algorithm>
-#include <atomic>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -27,6 +26,8 @@ constexpr int kMtN = 624, kMtM = 397;
 
 struct Mt19937 {
   uint32_t key[kMtN];  // numpy's state words (untempered)
+  uint32_t out[kMtN];  // the block's tempered outputs
+  int pos;
 
   void gen() {  // the next block of 624 (numpy's mt19937_gen)
     constexpr uint32_t kA = 0x9908b0dfu, kUp = 0x80000000u, kLo = 0x7fffffffu;
@@ -41,79 +42,25 @@ struct Mt19937 {
     }
     const uint32_t y = (key[kMtN - 1] & kUp) | (key[0] & kLo);
     key[kMtN - 1] = key[kMtM - 1] ^ (y >> 1) ^ ((0u - (y & 1u)) & kA);
-  }
-};
-
-// The MT19937 stream as blocks of 624 tempered words, produced ahead by a thread of their own: generating and
-// tempering a block is ~half the draw pass's cost and needs nothing from it. A ring of kRing blocks (block i in
-// slot i % kRing, its untempered key beside its outputs, so the state at any position can be handed back); the
-// producer never runs more than kRing - 1 blocks ahead of the block the draws are reading.
-class MtStream {
- public:
-  static constexpr int kRing = 32;
-  const uint32_t* out;  // the current block's tempered words
-  int pos;              // next word of the current block
-  MtStream(const uint32_t* key, int p) : ring_(kRing) {
-    std::memcpy(ring_[0].key, key, sizeof(ring_[0].key));
-    temper(ring_[0]);
-    produced_.store(1, std::memory_order_release);
-    out = ring_[0].out;
-    pos = p;
-    th_ = std::thread([this] { produce(); });
-  }
-  ~MtStream() {
-    stop_.store(true, std::memory_order_release);
-    th_.join();
-  }
-  void next_block() {
-    ++blk_;
-    cur_.store(blk_, std::memory_order_release);  // blocks before blk_ are free
-    for (int spins = 0; produced_.load(std::memory_order_acquire) <= blk_; ++spins)
-      if (spins > 64) std::this_thread::yield();
-    out = ring_[blk_ % kRing].out;
     pos = 0;
   }
-  void state(uint32_t* key, int32_t* p) const {  // numpy's (key, pos) at the current position
-    std::memcpy(key, ring_[blk_ % kRing].key, sizeof(ring_[0].key));
-    *p = pos;
-  }
-
- private:
-  struct Block {
-    uint32_t key[kMtN];
-    uint32_t out[kMtN];
-  };
-  static void temper(Block& b) {
-    for (int i = 0; i < kMtN; ++i) {
-      uint32_t y = b.key[i];
+  void temper_from(int p0) {  // numpy's mt19937_next32 tempering, a block at a time (vectorised)
+    for (int i = p0; i < kMtN; ++i) {
+      uint32_t y = key[i];
       y ^= y >> 11;
       y ^= (y << 7) & 0x9d2c5680u;
       y ^= (y << 15) & 0xefc60000u;
       y ^= y >> 18;
-      b.out[i] = y;
+      out[i] = y;
     }
   }
-  void produce() {
-    Mt19937 g;
-    for (int64_t i = 1;; ++i) {
-      for (int spins = 0; i >= cur_.load(std::memory_order_acquire) + kRing; ++spins) {
-        if (stop_.load(std::memory_order_acquire)) return;
-        if (spins > 64) std::this_thread::yield();
-      }
-      if (stop_.load(std::memory_order_acquire)) return;
-      std::memcpy(g.key, ring_[(i - 1) % kRing].key, sizeof(g.key));
-      g.gen();
-      Block& d = ring_[i % kRing];
-      std::memcpy(d.key, g.key, sizeof(d.key));
-      temper(d);
-      produced_.store(i + 1, std::memory_order_release);
+  inline uint32_t next() {
+    if (__builtin_expect(pos == kMtN, 0)) {
+      gen();
+      temper_from(0);
     }
+    return out[pos++];
   }
-  std::vector<Block> ring_;
-  int64_t blk_ = 0;
-  std::atomic<int64_t> produced_{0}, cur_{0};
-  std::atomic<bool> stop_{false};
-  std::thread th_;
 };
 
 }  // namespace
@@ -126,13 +73,16 @@ namespace {
 // which a branch mispredicts at ~8 ns an element). The mask is fixed between powers of two, and a run of
 // words that cannot take i below the next power is processed without a bound check, so the loop-carried chain
 // is one compare and one subtract per word.
-void draw_row(MtStream& mt, int32_t A, int32_t* js) {
+void draw_row(Mt19937& mt, int32_t A, int32_t* js) {
   int32_t i = A - 1, k = 0;
   while (i >= 1) {
     const uint32_t m = 0xffffffffu >> __builtin_clz((uint32_t)i);
     const int32_t lo = (int32_t)(m >> 1);  // i keeps this mask while i > lo
     while (i > lo) {
-      if (mt.pos == kMtN) mt.next_block();
+      if (mt.pos == kMtN) {
+        mt.gen();
+        mt.temper_from(0);
+      }
       const int p0 = mt.pos;
       const int n = std::min(kMtN - p0, i - lo);
       const uint32_t* w = mt.out + p0;
@@ -215,7 +165,10 @@ extern "C" int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const in
     for (int64_t k = row_ptr[users[r]]; k < row_ptr[users[r] + 1]; ++k)
       HVAE_REQUIRE(col_idx[k] >= 0 && col_idx[k] < n_items, "hvae_negatives_legacy: item outside [0, n_items)");
   }
-  MtStream mt(mt_key, *mt_pos);
+  Mt19937 mt;
+  std::memcpy(mt.key, mt_key, sizeof(mt.key));
+  mt.pos = *mt_pos;
+  mt.temper_from(0);
   const int kWorkers = (int)std::max(1u, std::min(4u, std::thread::hardware_concurrency()));
   // chunk rows: about 32 M draw slots per chunk buffer (two buffers in flight)
   const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(256, ((int64_t)1 << 25) / n_items));
@@ -260,6 +213,7 @@ extern "C" int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const in
     pending = std::thread(finish, c0, nr, jsb[ci].data(), Ab[ci].data());
   }
   if (pending.joinable()) pending.join();
-  mt.state(mt_key, mt_pos);
+  std::memcpy(mt_key, mt.key, sizeof(mt.key));
+  *mt_pos = mt.pos;
   return HVAE_OK;
 }
