@@ -1,7 +1,7 @@
 # Round-5 final evidence, part B: FETCH_SIZE / WRITE_SIZE PMC passes (separate runs, one counter each) of the five
+# bench workloads on the final tree (stamped locally by scripts/pmc_to_traffic.py), then the other bench lines.
 # (the bench lines at the default --probe-steps 50: the probe brackets eager steps, and a run_epoch call's first
 # steps carry a heavier catch-up, so 5 probe steps read the fp8 adam_catchup at 430-470 us against 118 in the trace)
-# bench workloads on the final tree (stamped locally by scripts/pmc_to_traffic.py), then the other bench lines.
 set -e
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${OUT:-r05_final}
