@@ -27,11 +27,14 @@ def _reference_negatives(X, users, tests, n_neg):
 
 @pytest.mark.parametrize("n_users,n_items,density,seed", [(40, 500, 0.05, 1), (30, 120, 0.3, 2), (25, 101, 0.0, 3),
                                                           (20, 2000, 0.01, 4), (12, 60, 0.5, 5),
-                                                          (90, 300_000, 0.00002, 6)])
-def test_negatives_match_numpy(n_users, n_items, density, seed):
-    """Row for row against the reference's draw; the last case spans three of the sampler's row chunks
-    (2^25 / 300,000 = 111 rows each), so its pipelined passes hand the stream across chunk boundaries."""
+                                                          (90, 300_000, 0.00002, 6), (100, 3000, 0.01, 7)])
+@pytest.mark.parametrize("form", ["simd", "scalar"])
+def test_negatives_match_numpy(n_users, n_items, density, seed, form, monkeypatch):
+    """Row for row against the reference's draw, in both forms of the draw loop (the AVX-512 one where the host
+    has it, and the scalar one); the last case spans two of the sampler's 256-row chunks, so its pipelined
+    passes hand the stream across a chunk boundary."""
     from hvae import ops
+    monkeypatch.setenv("HVAE_NEG_SCALAR", "1" if form == "scalar" else "0")
     rng = np.random.default_rng(seed)
     X = sp.random(n_users, n_items, density=density, format="csr", random_state=seed)
     X.data[:] = 1.0
