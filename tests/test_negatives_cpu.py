@@ -67,3 +67,38 @@ def test_negatives_row_with_duplicate_and_test_in_seen():
     got = ops.negatives_legacy(indptr, indices, 200, users, tests, 99)
     for a, b in zip(got, ref):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("workers", [1, 3])
+@pytest.mark.parametrize("form", ["simd", "scalar"])
+def test_negatives_boundary_sizes(workers, form, monkeypatch):
+    """Rows whose available count sits at the draw's edges: exactly n_neg (a full permutation is drawn), n_neg - 1
+    (no draw), 1 and 0 available items, and counts just around powers of two (the mask changes there, and the
+    32- / 16-word groups must not cross it); odd worker counts split the chunks unevenly; a mid-block stream
+    position on entry."""
+    from hvae import ops
+    monkeypatch.setenv("HVAE_NEG_SCALAR", "1" if form == "scalar" else "0")
+    monkeypatch.setenv("HVAE_NEG_WORKERS", str(workers))
+    n_items = 300
+    rows = []
+    for avail in (99, 98, 1, 0, 100, 128, 129, 127, 256, 257, 255, 33, 17, 299):
+        n_seen = n_items - 1 - avail if avail < n_items else 0  # the test item is never available
+        rows.append(np.arange(n_items - 1 - max(n_seen, 0), n_items - 1, dtype=np.int32) if n_seen > 0 else
+                    np.zeros(0, np.int32))
+    indptr = np.zeros(len(rows) + 1, np.int64)
+    indptr[1:] = np.cumsum([len(r) for r in rows])
+    indices = np.concatenate(rows).astype(np.int32)
+    X = sp.csr_matrix((np.ones(len(indices), np.float32), indices, indptr), shape=(len(rows), n_items))
+    users = np.repeat(np.arange(len(rows), dtype=np.int32), 2)
+    tests = np.full(len(users), n_items - 1, dtype=np.int32)
+    np.random.seed(11)
+    np.random.random(301)  # leave the stream mid-block
+    ref = _reference_negatives(X, users, tests, 99)
+    after_ref = np.random.random(3)
+    np.random.seed(11)
+    np.random.random(301)
+    got = ops.negatives_legacy(indptr, indices, n_items, users, tests, 99)
+    after_got = np.random.random(3)
+    for r, (a, b) in enumerate(zip(got, ref)):
+        assert np.array_equal(a, b), f"row {r}"
+    assert np.array_equal(after_got, after_ref)
