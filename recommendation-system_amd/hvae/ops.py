@@ -503,12 +503,13 @@ def topk_fused(U: torch.Tensor, E_img: "DecoderImage", E32: torch.Tensor, e32_ma
     return (idx, val, flag) if with_flags else (idx, val)
 
 
-def negatives_legacy(indptr, indices, n_items: int, users, tests, n_neg: int):
+def negatives_legacy(indptr, indices, n_items: int, users, tests, n_neg: int, arrays: bool = False):
     """The 99-negative protocol's negatives for test rows (users[r], tests[r]) over a training CSR
     (indptr / indices), drawn by libhvae from numpy's global legacy RandomState exactly as the reference's
     per-row np.random.choice(available, n_neg, replace=False) would (src/ml/evaluate.py:159-170), which
     leaves the global state where those calls would have (hvae_negatives_legacy). Returns a list of int64
-    arrays, one per row (shorter where fewer than n_neg items are available)."""
+    arrays, one per row (shorter where fewer than n_neg items are available); with arrays=True the int32
+    [rows, n_neg] block and the per-row counts instead (entries past a row's count are undefined)."""
     import numpy as np
     indptr = np.ascontiguousarray(indptr, dtype=np.int64)
     indices = np.ascontiguousarray(indices, dtype=np.int32)
@@ -526,4 +527,6 @@ def negatives_legacy(indptr, indices, n_items: int, users, tests, n_neg: int):
     check(lib().hvae_negatives_legacy(p(key), p(pos), p(indptr), p(indices), int(n_items), p(users), p(tests), R,
                                       int(n_neg), p(out), p(counts)), "hvae_negatives_legacy")
     np.random.set_state((st[0], key, int(pos[0]), st[3], st[4]))
+    if arrays:
+        return out, counts
     return [out[r, :counts[r]].astype(np.int64) for r in range(R)]

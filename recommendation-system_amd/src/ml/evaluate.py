@@ -185,30 +185,54 @@ class RecommendationEvaluator:
         """The reference's sampler (evaluate.py:159-170): one row of _sample_negatives_rows."""
         return self._sample_negatives_rows([user_idx], [test_item_idx], n_negatives)[0]
 
-    def _sample_negatives_rows(self, users, tests, n_negatives: int) -> list[np.ndarray]:
+    def _sample_negatives_rows(self, users, tests, n_negatives: int, arrays: bool = False):
         """The reference's per-row np.random.choice(available, n, replace=False) over all rows in one native
         call (hvae_negatives_legacy): the same draws from numpy's global stream, in row order, which it leaves
-        where the per-row calls would."""
+        where the per-row calls would. A list of per-row arrays, or with arrays=True (negatives [R, n], counts [R])
+        for _ranks."""
         im = self.interaction_matrix
         if getattr(self, "_neg_csr", None) is None or self._neg_csr[0] is not im:
             im = im.tocsr()
             self._neg_csr = (self.interaction_matrix, np.ascontiguousarray(im.indptr, dtype=np.int64),
                              np.ascontiguousarray(im.indices, dtype=np.int32))
         _, indptr, indices = self._neg_csr
-        return ops.negatives_legacy(indptr, indices, self.n_items, users, tests, n_negatives)
+        return ops.negatives_legacy(indptr, indices, self.n_items, users, tests, n_negatives, arrays=arrays)
 
-    def _ranks(self, users: np.ndarray, tests: np.ndarray, negatives: list[np.ndarray]) -> np.ndarray:
-        """0-based rank of the test item among [test] + negatives, per row (batched on the device)."""
-        C = 1 + max((len(n) for n in negatives), default=0)
-        R = len(users)
+    @staticmethod
+    def _candidates(tests: np.ndarray, negatives):
+        """[test] + negatives per row as one int32 matrix (cand [R, C], pad [R]: rows padded with their test item
+        past their count, cnt [R]). negatives: a list of per-row arrays, or the (negatives [R, n], counts [R])
+        block of _sample_negatives_rows(arrays=True), which needs no per-row loop."""
+        R = len(tests)
+        if isinstance(negatives, tuple):
+            neg, cnt = negatives
+            cnt = np.asarray(cnt, np.int64)
+            C = 1 + (int(cnt.max()) if R else 0)
+            cand = np.empty((R, C), np.int32)
+            cand[:, 0] = tests
+            cand[:, 1:] = neg[:, :C - 1]
+            pad = cnt < C - 1
+            if pad.any():  # fewer available items than requested: pad with the test item (never outranks)
+                fill = np.arange(1, C)[None, :] > cnt[:, None]
+                cand[:, 1:] = np.where(fill, np.asarray(tests, np.int32)[:, None], cand[:, 1:])
+            return cand, pad, cnt
+        cnt = np.array([len(n) for n in negatives], np.int64)
+        C = 1 + (int(cnt.max()) if R else 0)
         cand = np.empty((R, C), np.int32)
         pad = np.zeros(R, bool)
         for r, (t, n) in enumerate(zip(tests, negatives)):
             cand[r, 0] = t
             cand[r, 1:1 + len(n)] = n
-            if len(n) < C - 1:  # fewer available items than requested: pad with the test item (never outranks)
+            if len(n) < C - 1:
                 cand[r, 1 + len(n):] = t
                 pad[r] = True
+        return cand, pad, cnt
+
+    def _ranks(self, users: np.ndarray, tests: np.ndarray, negatives) -> np.ndarray:
+        """0-based rank of the test item among [test] + negatives, per row (batched on the device); negatives as
+        _candidates takes them."""
+        R = len(users)
+        cand, pad, cnt = self._candidates(tests, negatives)
         out = np.empty(R, np.int64)
         with torch.no_grad():
             for s in range(0, R, self.batch_size):
@@ -219,7 +243,7 @@ class RecommendationEvaluator:
                 if pad[s:e].any():
                     scn = sc.cpu().numpy()
                     for r in np.nonzero(pad[s:e])[0]:
-                        n = len(negatives[s + r])
+                        n = int(cnt[s + r])
                         row = scn[r, : 1 + n]
                         out[s + r] = int((row[1:] > row[0]).sum() + (row[1:] == row[0]).sum())
                     rk = ops.rank_first(sc).cpu().numpy()
@@ -243,11 +267,11 @@ class RecommendationEvaluator:
                 continue
             users.append(self.user_to_idx[user_id])
             tests.append(self.item_to_idx[item_id])
-        negs = self._sample_negatives_rows(users, tests, n_negatives)
+        negs = self._sample_negatives_rows(users, tests, n_negatives, arrays=True)
         all_metrics = {k: {"recall": [], "ndcg": [], "hit_ratio": []} for k in k_values}
         sl = self._shard(len(users))
         if len(users[sl]):
-            rank = self._ranks(np.array(users[sl]), np.array(tests[sl]), negs[sl])
+            rank = self._ranks(np.array(users[sl]), np.array(tests[sl]), (negs[0][sl], negs[1][sl]))
             m = metrics_from_rank(rank, k_values)
             for k in k_values:
                 for name in ("recall", "ndcg", "hit_ratio"):

@@ -100,7 +100,7 @@ def evaluate_config_on_val(model, train_matrix: csr_matrix, val_df: pd.DataFrame
             continue
         users.append(user_to_idx[user_id])
         tests.append(item_to_idx[item_id])
-    negs = ev._sample_negatives_rows(users, tests, n_negatives)
+    negs = ev._sample_negatives_rows(users, tests, n_negatives, arrays=True)
     if not users:
         return {f"{m}@{k}": 0.0 for k in k_values for m in ("recall", "ndcg", "hit_ratio")}
     rank = ev._ranks(np.array(users), np.array(tests), negs)

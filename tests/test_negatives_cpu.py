@@ -102,3 +102,27 @@ def test_negatives_boundary_sizes(workers, form, monkeypatch):
     for r, (a, b) in enumerate(zip(got, ref)):
         assert np.array_equal(a, b), f"row {r}"
     assert np.array_equal(after_got, after_ref)
+
+
+def test_candidate_block_equals_per_row_lists():
+    """The evaluator's candidate matrix from the sampler's (negatives, counts) block equals the one built row by
+    row from the per-row lists (short rows padded with the test item) -- the block form the dataset protocol
+    and the tuner use, the list form the single-user path uses."""
+    from hvae import ops
+    from src.ml.evaluate import RecommendationEvaluator
+    rng = np.random.default_rng(5)
+    X = sp.random(40, 150, density=0.3, format="lil", random_state=5)
+    X[3, :] = 1.0  # every item seen: no item available, so the row is all padding
+    X = X.tocsr()
+    users = rng.integers(0, 40, 60).astype(np.int32)
+    users[:3] = 3
+    tests = rng.integers(0, 150, 60).astype(np.int32)
+    np.random.seed(3)
+    lists = ops.negatives_legacy(X.indptr, X.indices, 150, users, tests, 99)
+    np.random.seed(3)
+    block = ops.negatives_legacy(X.indptr, X.indices, 150, users, tests, 99, arrays=True)
+    assert any(len(n) < 99 for n in lists)
+    a = RecommendationEvaluator._candidates(tests, lists)
+    b = RecommendationEvaluator._candidates(tests, block)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
