@@ -267,63 +267,17 @@ class RecommendationEvaluator:
                 continue
             users.append(self.user_to_idx[user_id])
             tests.append(self.item_to_idx[item_id])
+        negs = self._sample_negatives_rows(users, tests, n_negatives, arrays=True)
         all_metrics = {k: {"recall": [], "ndcg": [], "hit_ratio": []} for k in k_values}
         sl = self._shard(len(users))
         if len(users[sl]):
-            rank = self._ranks_pipelined(np.array(users, np.int32), np.array(tests, np.int32), n_negatives, sl)
+            rank = self._ranks(np.array(users[sl]), np.array(tests[sl]), (negs[0][sl], negs[1][sl]))
             m = metrics_from_rank(rank, k_values)
             for k in k_values:
                 for name in ("recall", "ndcg", "hit_ratio"):
                     all_metrics[k][name] = list(m[k][name])
         logger.info(f"Evaluated {len(users)} users")
         return _aggregate_metrics(all_metrics, k_values, self.group, self.device)
-
-    NEG_CHUNK = 1024  # rows per sampler call in the pipelined dataset protocol
-
-    def _ranks_pipelined(self, users: np.ndarray, tests: np.ndarray, n_negatives: int, sl: slice) -> np.ndarray:
-        """_ranks of rows users[sl] with every row's negatives drawn in row order: a thread draws chunk c + 1
-        (hvae_negatives_legacy runs without the GIL) while this one ranks chunk c on the device. The chunks' calls
-        continue numpy's one global stream, so the negatives -- and the stream left behind -- are those of a
-        single call over all rows; nothing else draws from numpy meanwhile."""
-        import queue
-        import threading
-        R = len(users)
-        C = self.NEG_CHUNK
-        if R <= C:
-            negs = self._sample_negatives_rows(users, tests, n_negatives, arrays=True)
-            return self._ranks(users[sl], tests[sl], (negs[0][sl], negs[1][sl]))
-        q: queue.Queue = queue.Queue(maxsize=2)
-
-        def draw():
-            try:
-                for c0 in range(0, R, C):
-                    q.put((c0, self._sample_negatives_rows(users[c0:c0 + C], tests[c0:c0 + C], n_negatives,
-                                                           arrays=True)))
-            except BaseException as e:  # handed to the consumer, which raises it
-                q.put(e)
-
-        th = threading.Thread(target=draw, name="hvae-negatives", daemon=True)
-        th.start()
-        start, step = sl.start or 0, sl.step or 1
-        out = []
-        try:
-            for _ in range(0, R, C):
-                item = q.get()
-                if isinstance(item, BaseException):
-                    raise item
-                c0, (neg, cnt) = item
-                idx = np.arange(c0, c0 + len(cnt))
-                mine = (idx >= start) & ((idx - start) % step == 0)  # this rank's rows of the chunk
-                if mine.any():
-                    out.append(self._ranks(users[idx[mine]], tests[idx[mine]], (neg[mine], cnt[mine])))
-        finally:  # a failed ranking leaves the thread blocked on a full queue: drain it so that it can finish
-            while th.is_alive():
-                try:
-                    q.get(timeout=0.05)
-                except queue.Empty:
-                    pass
-            th.join()
-        return np.concatenate(out) if out else np.empty(0, np.int64)
 
     def _shard(self, n: int) -> slice:
         """This rank's rows of a dataset protocol (all rows without a process group)."""

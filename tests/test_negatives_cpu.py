@@ -126,41 +126,3 @@ def test_candidate_block_equals_per_row_lists():
     b = RecommendationEvaluator._candidates(tests, block)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
-
-
-def test_pipelined_ranks_cover_the_shard_in_order(monkeypatch):
-    """The dataset protocol's pipelined ranking (a thread draws chunk c + 1 while chunk c is ranked) hands _ranks
-    the shard's rows in row order with the negatives of one call over all rows, and leaves numpy's stream where
-    that call does; _ranks itself is stubbed (it scores on the device) to return the rows' own negatives."""
-    from hvae import ops
-    from src.ml.evaluate import RecommendationEvaluator
-    rng = np.random.default_rng(9)
-    X = sp.random(50, 400, density=0.05, format="csr", random_state=9)
-    users = rng.integers(0, 50, 700).astype(np.int32)
-    tests = rng.integers(0, 400, 700).astype(np.int32)
-    np.random.seed(21)
-    neg_all, cnt_all = ops.negatives_legacy(X.indptr, X.indices, 400, users, tests, 99, arrays=True)
-    after_ref = np.random.random(3)
-    ev = RecommendationEvaluator.__new__(RecommendationEvaluator)
-    ev.interaction_matrix, ev.n_items = X, 400
-    ev.NEG_CHUNK = 128
-    seen = []
-
-    def fake_ranks(u, t, negatives):
-        neg, cnt = negatives
-        seen.append((u.copy(), t.copy(), neg[:, :99].copy(), cnt.copy()))
-        return np.zeros(len(u), np.int64)
-
-    monkeypatch.setattr(ev, "_ranks", fake_ranks)
-    for sl in (slice(0, 700), slice(1, 700, 3)):
-        seen.clear()
-        np.random.seed(21)
-        r = ev._ranks_pipelined(users, tests, 99, sl)
-        after = np.random.random(3)
-        assert np.array_equal(after, after_ref)
-        u = np.concatenate([x[0] for x in seen])
-        n = np.concatenate([x[2] for x in seen])
-        c = np.concatenate([x[3] for x in seen])
-        assert len(r) == len(u) and np.array_equal(u, users[sl]) and np.array_equal(c, cnt_all[sl])
-        full = c == 99
-        assert np.array_equal(n[full], neg_all[sl][full])
