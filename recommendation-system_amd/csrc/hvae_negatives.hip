@@ -211,12 +211,13 @@ HVAE_AVX512 void draw_row_avx512(Mt19937& mt, int32_t A, int32_t* js) {
 
 // The swaps replayed backwards for the n_neg leading positions only (rows are independent here). The value
 // that ends at position q < n_neg is the one at src[q] before the swaps, found by undoing them from the last
-// (i = 1) to the first (i = A - 1); at[] maps a position to the tracked q sitting there (-1: none; int8, so
-// the map stays in L1), back to all -1 on return.
-void replay_row(int32_t A, int32_t n_neg, const int32_t* js, int8_t* at, int32_t* src) {
+// (i = 1) to the first (i = A - 1); at[] maps a position to the tracked q sitting there (-1: none; int8 up to
+// 127 tracked positions, so the map stays in L1, int16 past that), back to all -1 on return.
+template <typename At>
+void replay_row(int32_t A, int32_t n_neg, const int32_t* js, At* at, int32_t* src) {
   for (int32_t q = 0; q < n_neg; ++q) {
     src[q] = q;
-    at[q] = (int8_t)q;
+    at[q] = (At)q;
   }
   for (int32_t i = 1; i < A; ++i) {
     const int32_t j = js[A - 1 - i];
@@ -224,8 +225,8 @@ void replay_row(int32_t A, int32_t n_neg, const int32_t* js, int8_t* at, int32_t
     if (__builtin_expect((a & b) >= 0, 0) && j != i) {  // either position tracked
       if (a >= 0) src[a] = j;
       if (b >= 0) src[b] = i;
-      at[i] = (int8_t)b;
-      at[j] = (int8_t)a;
+      at[i] = (At)b;
+      at[j] = (At)a;
     }
   }
   for (int32_t q = 0; q < n_neg; ++q) at[src[q]] = -1;
@@ -279,8 +280,8 @@ extern "C" int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const in
                                      const int32_t* tests, int64_t n_rows, int32_t n_neg, int32_t* out,
                                      int32_t* counts) {
   HVAE_REQUIRE(mt_key && mt_pos && row_ptr && n_items > 0 && n_items < (int64_t)1 << 31 && n_rows >= 0 &&
-                   n_neg >= 0 && n_neg <= 127 && (n_rows == 0 || (users && tests && out && counts)),
-               "hvae_negatives_legacy: bad args (n_neg <= 127)");
+                   n_neg >= 0 && n_neg <= 32767 && (n_rows == 0 || (users && tests && out && counts)),
+               "hvae_negatives_legacy: bad args (n_neg <= 32767)");
   HVAE_REQUIRE(*mt_pos >= 0 && *mt_pos <= kMtN, "hvae_negatives_legacy: MT19937 position outside [0, 624]");
   for (int64_t r = 0; r < n_rows; ++r) {
     HVAE_REQUIRE(users[r] >= 0 && tests[r] >= 0 && tests[r] < n_items,
@@ -310,7 +311,9 @@ extern "C" int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const in
     auto work = [&](int wk) {
       std::vector<uint8_t> ex((size_t)n_items, 0);
       std::vector<int32_t> avail((size_t)n_items), js((size_t)n_items + 16), src((size_t)n_neg + 1);
-      std::vector<int8_t> at((size_t)n_items, -1);
+      const bool narrow = n_neg <= 127;
+      std::vector<int8_t> at8(narrow ? (size_t)n_items : 0, -1);
+      std::vector<int16_t> at16(narrow ? 0 : (size_t)n_items, -1);
       Mt19937 g;
       for (int64_t rr = wk; rr < nr; rr += kWorkers) {
         const int64_t r = c0 + rr;
@@ -330,7 +333,10 @@ extern "C" int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const in
           mt_temper_all(g);
           draw_row_scalar<true>(g, A, js.data());
         }
-        replay_row(A, n_neg, js.data(), at.data(), src.data());
+        if (narrow)
+          replay_row(A, n_neg, js.data(), at8.data(), src.data());
+        else
+          replay_row(A, n_neg, js.data(), at16.data(), src.data());
         for (int32_t q = 0; q < n_neg; ++q) o[q] = avail[src[q]];
         counts[r] = n_neg;
       }

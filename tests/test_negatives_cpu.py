@@ -126,3 +126,22 @@ def test_candidate_block_equals_per_row_lists():
     b = RecommendationEvaluator._candidates(tests, block)
     for x, y in zip(a, b):
         assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("n_neg", [128, 200, 1000])
+def test_negatives_beyond_127(n_neg):
+    """`--n-negatives` above 127 (the wide tracked-slot map), including more than some rows have available."""
+    from hvae import ops
+    rng = np.random.default_rng(n_neg)
+    X = sp.random(30, 1500, density=0.2, format="csr", random_state=n_neg)
+    users = rng.integers(0, 30, 40)
+    tests = rng.integers(0, 1500, 40)
+    np.random.seed(n_neg)
+    ref = _reference_negatives(X, users, tests, n_neg)
+    after_ref = np.random.random(3)
+    np.random.seed(n_neg)
+    got = ops.negatives_legacy(X.indptr, X.indices, 1500, users, tests, n_neg)
+    after_got = np.random.random(3)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+    assert np.array_equal(after_got, after_ref)
