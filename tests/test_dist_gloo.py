@@ -98,7 +98,10 @@ def _worker(rank, world, port, q, B, sizes):
         ex.pack(g_small, None, 0, None, 0.0)
     ex.communicate()
     merged = ex.unpack_merge(g_small)
-    q.put((rank, mine, g_small.clone(), merged.dense.clone()))
+    # numpy, not tensors: a tensor crosses the queue as a file descriptor the exiting worker may close before the
+    # parent receives it (ConnectionResetError in the parent's rebuild)
+    q.put((rank, tuple(x.numpy().copy() if torch.is_tensor(x) else x for x in mine), g_small.numpy().copy(),
+           merged.dense.numpy().copy()))
     dist.destroy_process_group()
 
 
@@ -120,6 +123,7 @@ def test_dp_exchange_gloo_world2(B, sizes):
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda t: t[0])
+    res = [(r, tuple(torch.as_tensor(x) if i in (0, 4) else x for i, x in enumerate(m)), torch.as_tensor(sm), torch.as_tensor(w)) for r, m, sm, w in res]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
