@@ -313,6 +313,11 @@ def main():
             done += k
 
     run(args.warmup)
+    # the wall time is never taken from probed steps: an armed probe puts a 200-us hold kernel in front of every
+    # bracketed launch (csrc/hvae_abi.hip, probe_mark), so the library is disarmed here and armed only after the
+    # timed region, for the separate probe pass below
+    from hvae._lib import check as _check, lib as _lib
+    _check(_lib().hvae_probe_arm(None, 0), "probe_disarm")
     if group is not None:
         torch.distributed.barrier()
     torch.cuda.synchronize()

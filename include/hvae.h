@@ -534,12 +534,13 @@ int hvae_topk_fused(const float* U, int64_t ldu, const void* E_bf16, const float
  * neither in row users[r] of the training CSR (row_ptr / col_idx) nor tests[r], ascending ("available",
  * src/ml/evaluate.py:159-165); all of them when fewer than n_neg (counts[r] = that number, no draw), else
  * np.random.choice(available, n_neg, replace=False) (:166-170) = available[permutation(len)[:n_neg]] of the
- * legacy RandomState, counts[r] = n_neg. mt_key [624] / mt_pos: numpy's MT19937 state
+ * legacy RandomState, counts[r] = n_neg. n_users = the CSR's row count (row_ptr has n_users + 1 entries): every
+ * users[r] must lie in [0, n_users). mt_key [624] / mt_pos: numpy's MT19937 state
  * (np.random.get_state()[1:3]), advanced in place as the per-row choices in row order would leave it.
  * out [n_rows, n_neg], n_neg <= 32767. Threads: the caller's plus up to 8 workers (HVAE_NEG_WORKERS overrides the count);
  * AVX-512 where the host has it (HVAE_NEG_SCALAR=1 forces the scalar form; the results are identical). */
-int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const int64_t* row_ptr, const int32_t* col_idx,
-                          int64_t n_items, const int32_t* users, const int32_t* tests, int64_t n_rows,
+int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const int64_t* row_ptr, int64_t n_users,
+                          const int32_t* col_idx, int64_t n_items, const int32_t* users, const int32_t* tests, int64_t n_rows,
                           int32_t n_neg, int32_t* out, int32_t* counts);
 
 /* ---------------------------------------------------- data artifacts (host) -- */

@@ -65,6 +65,9 @@ void probe_mark(const char* name, hipStream_t st, bool begin) {
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
   if (begin) {
     if (g_probe.n >= g_probe.cap) return;
+    // a pending launch error of the caller's is left for the caller's own check (hipGetLastError below would
+    // clear it): no hold, no bracket
+    if (hipPeekAtLastError() != hipSuccess) return;
     k_probe_hold<<<1, 64, 0, st>>>(20000);  // 200 us at 100 MHz
     if (hipGetLastError() != hipSuccess) return;
     if (hipEventRecord(g_probe.ev[2 * g_probe.n], st) == hipSuccess) g_probe.open = true;

@@ -36,6 +36,25 @@
 namespace hvae {
 namespace dec5 {
 
+// Timing build only (DEC5_TIMING=1, scripts/probe_dec5_phases.py; outputs unchanged): each wave of k_dec5_bf16 adds
+// s_memtime deltas of its loop's phases -- producer: [vmcnt wait | barrier | GEMM1 with its DMA pieces | tail mask,
+// exponentials, P out]; consumer: [vmcnt wait | barrier | P read, GEMM2 with its DMA pieces | -] -- its tile
+// count, its kernel cycles, the s_memrealtime span of the same interval (in-kernel clock) and its role into dec5_tm
+#ifndef DEC5_TIMING
+#define DEC5_TIMING 0
+#endif
+#if DEC5_TIMING
+__device__ unsigned long long dec5_tm[2048 * 8];
+#define DEC5_T(...) __VA_ARGS__
+#else
+#define DEC5_T(...)
+#endif
+// DEC5_GLDS=1 (A/B): the LDS-DMA pieces as global_load_lds_dwordx4 (64-bit SGPR base + the lane's VGPR offset, no
+// buffer descriptor) instead of buffer_load_dwordx4 ... lds. Rows past N of the last tile then read the image's
+// next bytes (the tile-transposed copy: finite bf16) instead of the descriptor's zeros; their P is 0 (tail mask)
+#ifndef DEC5_GLDS
+#define DEC5_GLDS 0
+#endif
 
 template <bool WITH_O>
 __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, int64_t ldu,
@@ -57,6 +76,15 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int role = w >> 2, q = w & 3;
   const int ug = q & 1, dh = q >> 1;
+  DEC5_T(unsigned long long tacc[4] = {0, 0, 0, 0}, ntl = 0;
+         const unsigned long long tk0 = __builtin_amdgcn_s_memtime(), rk0 = __builtin_amdgcn_s_memrealtime();
+         auto tm_store = [&] {
+           if (lane == 0 && blockIdx.x < 256) {
+             unsigned long long* o = dec5_tm + (blockIdx.x * 8 + w) * 8;
+             o[0] = tacc[0]; o[1] = tacc[1]; o[2] = tacc[2]; o[3] = tacc[3]; o[4] = ntl;
+             o[5] = __builtin_amdgcn_s_memtime() - tk0; o[6] = __builtin_amdgcn_s_memrealtime() - rk0; o[7] = role;
+           }
+         };)
   // block -> (user block, split): by default split = b % splits, so with 4 splits each XCD (b % 8) streams one
   // split; DEC5_XMIX (A/B) deals each XCD's blocks over all splits (b / 8 picks the split) when the grid allows
   int split, ublk;
@@ -98,12 +126,22 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     const int p = q * PW + i;
     const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
     const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
+#if DEC5_GLDS
+    const unsigned char* src = reinterpret_cast<const unsigned char*>(E) + so;  // wave-uniform: an SGPR pair
+    if (fresh)
+      asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" DEC5_POL
+                   :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(src) : "memory");
+    else
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2" DEC5_POL
+                   :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(src) : "memory");
+#else
     if (fresh)
       asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen" DEC5_POL " lds"
                    :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
     else
       asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen" DEC5_POL " lds"
                    :: "s"(lb + (uint32_t)(i * 1024)), "v"(vo), "s"(rsrc), "s"(so) : "memory");
+#endif
   };
   auto tile_soff = [&](int64_t t) {
     return (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * (int64_t)(kTI * D * 2)));
@@ -249,17 +287,23 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     for (int64_t t = t_beg; t < t_end; ++t) {
       const int li = (int)(t - t_beg);
       const int nxt = (li + 1) % NS, s_dma = (li + 2) % NS, par = li & 1;
-      wait_vmcnt<0>();
+      DEC5_T(const unsigned long long tm0 = __builtin_amdgcn_s_memtime();)
+      if (!(DEC5_ABL & (1 | 128))) wait_vmcnt<0>();
+      DEC5_T(const unsigned long long tm1 = __builtin_amdgcn_s_memtime();)
       barrier();  // [L] tile t + 1 landed, P(t) published, GEMM2(t - 1) done
+      DEC5_T(const unsigned long long tm2 = __builtin_amdgcn_s_memtime(); unsigned long long tm3 = tm2;)
       if (t + 1 < t_end) {
         const uint32_t soff_dma = tile_soff(t + 2);  // branch-free: past the split the pieces fill the free slot
         gemm1(lds + nxt * TB, s_nx, [&](int ks) {
           const int kk = ks - DEC5_PDMA_AT;
-          if (kk >= 0 && kk % DEC5_DMA_STRIDE == 0 && kk / DEC5_DMA_STRIDE < PA) issue_piece(soff_dma, s_dma, prot(kk / DEC5_DMA_STRIDE, PA), kk == 0);
+          if (!(DEC5_ABL & 1) && kk >= 0 && kk % DEC5_DMA_STRIDE == 0 && kk / DEC5_DMA_STRIDE < PA) issue_piece(soff_dma, s_dma, prot(kk / DEC5_DMA_STRIDE, PA), kk == 0);
         });
+        DEC5_T(tm3 = __builtin_amdgcn_s_memtime();)
         mask_tail(s_nx, t + 1);
         p_out(par ^ 1);
       }
+      DEC5_T(const unsigned long long tm4 = __builtin_amdgcn_s_memtime(); tacc[0] += tm1 - tm0; tacc[1] += tm2 - tm1;
+             tacc[2] += tm3 - tm2; tacc[3] += tm4 - tm3; ++ntl;)
     }
     wait_vmcnt<0>();
 #pragma unroll
@@ -281,6 +325,7 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
       }
     }
     barrier();  // [E1]
+    DEC5_T(tm_store();)
     return;
   }
   if (role == 0) {
@@ -517,8 +562,11 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
   for (int64_t t = t_beg; t < t_end; ++t) {
     const int li = (int)(t - t_beg);
     const int cur = li % NS, s_dma = (li + 2) % NS, par = li & 1;
+    DEC5_T(const unsigned long long tm0 = __builtin_amdgcn_s_memtime();)
     if constexpr (PB > 0) if (!(DEC5_ABL & (1 | 128))) wait_vmcnt<0>();
+    DEC5_T(const unsigned long long tm1 = __builtin_amdgcn_s_memtime();)
     if (!(DEC5_ABL & 2)) barrier();  // [L]
+    DEC5_T(const unsigned long long tm2 = __builtin_amdgcn_s_memtime();)
     // P(t) in GEMM2's B layout: user col, positions 8 h .. 8 h + 7 of k-steps 0 and 1
     const uint4 pf0 = *reinterpret_cast<const uint4*>(p_row(par, col) + 16 * h);
     const uint4 pf1 = *reinterpret_cast<const uint4*>(p_row(par, col) + 32 + 16 * h);
@@ -536,11 +584,14 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
         if (dma && ii >= 0 && ii % DEC5_DMA_STRIDE == 0 && ii / DEC5_DMA_STRIDE < PB) issue_piece(soff_dma, s_dma, PA + prot(ii / DEC5_DMA_STRIDE, PB), ii == 0);
 #endif
     });
+    DEC5_T(const unsigned long long tm3 = __builtin_amdgcn_s_memtime(); tacc[0] += tm1 - tm0; tacc[1] += tm2 - tm1;
+           tacc[2] += tm3 - tm2; ++ntl;)
   }
   if constexpr (PB > 0) wait_vmcnt<0>();
   if (DEC5_P32) barrier();  // [PE0]
   barrier();  // [E0]
   barrier();  // [E1] producers' (l, m) published
+  DEC5_T(tm_store();)
   if (!wave_active || t_beg >= t_end || user >= nb) return;
   const float ltot = xm[ug * 64 + col], mu = xm[ug * 64 + 32 + col];
   if (h == 0 && dh == 0) out.flag[out.direct ? user : (int64_t)split * nb + user] = !(ltot >= kMinL);
@@ -1015,3 +1066,11 @@ int dec5_launch(bool with_o, const float* U, int64_t ldu, const void* E, const f
 }
 
 }  // namespace hvae
+
+#if DEC5_TIMING
+extern "C" int hvae_dec5_timing_fetch(unsigned long long* out) {  // [2048 waves][8], timing builds only
+  HVAE_HIP(hipDeviceSynchronize());
+  HVAE_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(hvae::dec5::dec5_tm), sizeof(hvae::dec5::dec5_tm)));
+  return HVAE_OK;
+}
+#endif

@@ -675,7 +675,9 @@ template <int i>
 __device__ __forceinline__ void gemm_dma_piece(uint32_t m0, int voff, __amdgpu_buffer_rsrc_t rsrc, uint32_t soff) {
   // M0 and soffset come in computed (an s_add in the asm would write SCC behind the compiler's back; the
   // instruction's offset field would move the LDS destination too); the first piece of a group waits out the
-  // readfirstlane of its SGPR operands
+  // readfirstlane of its SGPR operands. M0 is not in the clobber list on purpose: the AMDGPU backend reserves it
+  // (never allocates it to an "s" operand, and re-initialises it before each of its own M0 uses), and it rejects
+  // reserved registers there ("clobbering them may lead to undefined behaviour", -Winline-asm)
   if constexpr (i == 0)
     asm volatile("s_nop 4\n\ts_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
                  :: "s"(m0), "v"(voff), "s"(rsrc), "s"(soff) : "memory");

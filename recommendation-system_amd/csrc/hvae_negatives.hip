@@ -276,15 +276,15 @@ bool use_avx512() {
 // kWorkers threads meanwhile finish chunk c - 1, each row independently: regenerate the row's words from its
 // snapshot (the stored draw), list the available items and replay the swaps.
 extern "C" int hvae_negatives_legacy(uint32_t* mt_key, int32_t* mt_pos, const int64_t* row_ptr,
-                                     const int32_t* col_idx, int64_t n_items, const int32_t* users,
+                                     int64_t n_users, const int32_t* col_idx, int64_t n_items, const int32_t* users,
                                      const int32_t* tests, int64_t n_rows, int32_t n_neg, int32_t* out,
                                      int32_t* counts) {
-  HVAE_REQUIRE(mt_key && mt_pos && row_ptr && n_items > 0 && n_items < (int64_t)1 << 31 && n_rows >= 0 &&
+  HVAE_REQUIRE(mt_key && mt_pos && row_ptr && n_users >= 0 && n_items > 0 && n_items < (int64_t)1 << 31 && n_rows >= 0 &&
                    n_neg >= 0 && n_neg <= 32767 && (n_rows == 0 || (users && tests && out && counts)),
                "hvae_negatives_legacy: bad args (n_neg <= 32767)");
   HVAE_REQUIRE(*mt_pos >= 0 && *mt_pos <= kMtN, "hvae_negatives_legacy: MT19937 position outside [0, 624]");
   for (int64_t r = 0; r < n_rows; ++r) {
-    HVAE_REQUIRE(users[r] >= 0 && tests[r] >= 0 && tests[r] < n_items,
+    HVAE_REQUIRE(users[r] >= 0 && users[r] < n_users && tests[r] >= 0 && tests[r] < n_items,
                  "hvae_negatives_legacy: row %lld: bad user / test item", (long long)r);
     for (int64_t k = row_ptr[users[r]]; k < row_ptr[users[r] + 1]; ++k)
       HVAE_REQUIRE(col_idx[k] >= 0 && col_idx[k] < n_items, "hvae_negatives_legacy: item outside [0, n_items)");

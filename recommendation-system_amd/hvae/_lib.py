@@ -169,7 +169,7 @@ SIGNATURES = {
     "hvae_topk_fused": (cint, [vp, i64, vp, vp, vp, i64, i64, P(CsrBatch), i64, i64, vp, vp, vp, vp, sz,
                                vp]),
     "hvae_cast_bf16": (cint, [vp, vp, i64, vp]),
-    "hvae_negatives_legacy": (cint, [vp, vp, vp, vp, i64, vp, vp, i64, C.c_int32, vp, vp]),
+    "hvae_negatives_legacy": (cint, [vp, vp, vp, i64, vp, i64, vp, vp, i64, C.c_int32, vp, vp]),
     "hvae_read_interactions": (cint, [C.c_char_p, C.c_char_p, i64, i64, C.c_char_p, i64, i64, cint,
                                       P(HostCsr)]),
     "hvae_host_csr_free": (None, [P(HostCsr)]),

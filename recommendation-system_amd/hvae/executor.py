@@ -274,6 +274,12 @@ class FusedTrainer:
         # saves (All_Beauty B = 64: 0.1815 ms/step with the plan in line, 0.1965 beside; Syn-1M B = 4096:
         # 1.545 -> 1.293 ms/step beside)
         self.plan_side_min_batch = int(os.environ.get("HVAE_PLAN_SIDE_MIN_BATCH", "512"))
+        # where the main stream joins the plan: "apply" (before the row-gradient apply, the plan overlapping the
+        # catch-up, encoder and forward GEMMs) or "fwd" (before the first forward GEMM: the plan overlaps only the
+        # catch-up and the encoder, and the forward GEMMs get every CU)
+        self.plan_join = os.environ.get("HVAE_PLAN_JOIN", "apply")
+        # when the plan forks off the main stream: "late" (after the lazy-Adam catch-up) or "early" (before it)
+        self.plan_fork = os.environ.get("HVAE_PLAN_FORK", "late")
         # batches up to MLP_ROWS_MAX_NB run the latent / projection MLP row-parallel (hvae_mlp_*_rows)
         self.mlp_rows = bool(int(os.environ.get("HVAE_MLP_ROWS", "1")))
         self._mlp_rows_cache: dict[int, bool] = {}
@@ -548,16 +554,24 @@ class FusedTrainer:
                 self.dp.merge_plan()
         elif train and self.plan_stream is not None and B >= self.plan_side_min_batch:
             # the batch's W1t rows replay their deferred steps (found from the CSR) before the forward reads
-            # them, while the row-gradient plan runs on the plan stream
+            # them, while the row-gradient plan runs on the plan stream. With HVAE_PLAN_FORK=early the plan forks
+            # before the catch-up (it reads only the batch, and the previous step's update that read the plan's
+            # buffers is behind it on the main stream), so it overlaps the catch-up too
+            ps = self.plan_stream
+            early = self.plan_fork == "early"
+            if early:
+                self._fork(main, ps)
+                check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), ps.cuda_stream),
+                      "w1_rowgrad_plan")
             if self.lazy_adam and not enc_lazy:
                 cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
                 check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
                                                     ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
                       "adam_lazy_catchup_csr")
-            ps = self.plan_stream
-            self._fork(main, ps)
-            check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), ps.cuda_stream),
-                  "w1_rowgrad_plan")
+            if not early:
+                self._fork(main, ps)
+                check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), ps.cuda_stream),
+                      "w1_rowgrad_plan")
             ev_plan = torch.cuda.Event()
             ev_plan.record(ps)
         elif train and plan_in_rows:
@@ -608,6 +622,9 @@ class FusedTrainer:
                   "ln_gelu_drop_fwd")
         Hl = H[-1]
         mu, lv = bf.heads, bf.heads[:, Lt:]
+        if ev_plan is not None and self.plan_join == "fwd" and not dp:
+            main.wait_event(ev_plan)
+            ev_plan = None
         if rows is not None:
             if plan_in_rows:
                 rows.plan_x, rows.plan_rg = C.pointer(csr), C.pointer(bf.rg.struct)
@@ -966,18 +983,20 @@ class FusedTrainer:
         n = len(users)
         if shuffle:  # one order on every rank
             if generator is not None:
-                # the caller's generator decides it, as in a single-GPU run: every rank draws (so each
-                # generator advances as the single-GPU one would) and rank 0's draw is broadcast
+                # the caller's generator decides it, as in a single-GPU run: every rank draws the permutation
+                # exactly as _sampler_order does (so each generator ends in the state a single-GPU validation
+                # leaves it in) and rank 0's permutation is broadcast (so the ranks agree even if their generators
+                # do not): the batches are the single-GPU batches
                 grp = dp.group
                 on_dev = torch.distributed.get_backend(grp) == "nccl"
-                s = torch.randint(0, 2 ** 62, (1,), generator=generator, device=generator.device)
-                s = s.to(self.device if on_dev else "cpu")
-                torch.distributed.broadcast(s, torch.distributed.get_global_rank(grp, 0), group=grp)
-                rng = np.random.default_rng([int(s.item()), 0x5EA1])
+                perm = _sampler_order(n, generator, self.device).to(torch.int64)
+                perm = perm.to(self.device if on_dev else "cpu")
+                torch.distributed.broadcast(perm, torch.distributed.get_global_rank(grp, 0), group=grp)
+                order = users[perm.cpu().numpy()]
             else:  # the shared data-parallel seed
                 rng = np.random.default_rng([self.dp_seed, 0x5EA1, self.dp_val_epoch])
                 self.dp_val_epoch += 1
-            order = users[rng.permutation(n)]
+                order = users[rng.permutation(n)]
         else:
             order = users
         n_full, tail = divmod(n, B)

@@ -524,8 +524,8 @@ def negatives_legacy(indptr, indices, n_items: int, users, tests, n_neg: int, ar
     out = np.empty((R, n_neg), dtype=np.int32)
     counts = np.empty(R, dtype=np.int32)
     p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
-    check(lib().hvae_negatives_legacy(p(key), p(pos), p(indptr), p(indices), int(n_items), p(users), p(tests), R,
-                                      int(n_neg), p(out), p(counts)), "hvae_negatives_legacy")
+    check(lib().hvae_negatives_legacy(p(key), p(pos), p(indptr), len(indptr) - 1, p(indices), int(n_items), p(users),
+                                      p(tests), R, int(n_neg), p(out), p(counts)), "hvae_negatives_legacy")
     np.random.set_state((st[0], key, int(pos[0]), st[3], st[4]))
     if arrays:
         return out, counts

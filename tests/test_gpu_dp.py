@@ -226,6 +226,11 @@ def _global_worker(rank, world, port, q):
         # with a caller's generator (seeded differently per rank) the order is rank 0's draw, broadcast
         gen = torch.Generator().manual_seed(100 + rank)
         r.append(fused.run_epoch(data, 32, True, ConstBeta(0.2), 0.3, train=False, generator=gen))
+        # ... and the caller's generator ends where a single-GPU validation leaves it
+        from hvae.executor import _sampler_order
+        ref = torch.Generator().manual_seed(100 + rank)
+        _sampler_order(417, ref, dev)
+        r.append(bool(torch.equal(gen.get_state(), ref.get_state())))
         torch.cuda.synchronize()
         q.put((rank, r, fused.flat.cpu().numpy(), int(fused.step_dev.item())))
         dist.barrier()
@@ -255,6 +260,7 @@ def test_dp_global_sharding_epochs(hip_device):
     assert ra[2]["total_loss"] < ra[0]["total_loss"]
     assert all(abs(v) < float("inf") for v in ra[3].values())
     assert all(abs(v) < float("inf") for v in ra[4].values())
+    assert ra[5] is True and rb[5] is True
 
 
 def test_dp_two_ranks_one_gpu(hip_device):

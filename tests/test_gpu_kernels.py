@@ -34,7 +34,10 @@ def _maxrel(a, b):
                                    # weight-gradient fast path (trans_a, K >= 1024): 32- and 64-square tiles
                                    (768, 768, 4096), (256, 64, 2048),
                                    # whole 64-tiles (the LDS-DMA path's 64 x 64 instance)
-                                   (4096, 768, 256)])
+                                   (4096, 768, 256),
+                                   # the LDS-DMA path's 64 x 32 tile (no trans_a, 256 64-square tiles, 512 64 x 32
+                                   # ones: the Syn-10M step's heads / dh shapes)
+                                   (4096, 256, 512)])
 @pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
 def test_gemm_f32(ops, hip_device, M, N, K, ta, tb):
     g = torch.Generator().manual_seed(M * 7 + N * 3 + K)
@@ -49,9 +52,10 @@ def test_gemm_f32(ops, hip_device, M, N, K, ta, tb):
     assert _maxrel(out, ref) < 2e-5 * max(1.0, math.sqrt(K) / 8)
 
 
-@pytest.mark.parametrize("M,N,K", [(50, 70, 33), (128, 96, 64)])
+@pytest.mark.parametrize("M,N,K", [(50, 70, 33), (128, 96, 64), (4096, 256, 512)])
 def test_gemm_epilogues(ops, hip_device, M, N, K):
-    """The fused epilogues on a ragged shape (register-staged kernel) and a whole-tile one (LDS-DMA path)."""
+    """The fused epilogues on a ragged shape (register-staged kernel) and whole-tile ones (LDS-DMA path: 32 x 32
+    at 128 x 96, the 64 x 32 tile at 4096 x 256; split-K is never planned without trans_a)."""
     from hvae import _lib
     g = torch.Generator().manual_seed(3)
     A, W, bias = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g), torch.randn(N, generator=g)

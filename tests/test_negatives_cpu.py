@@ -69,6 +69,19 @@ def test_negatives_row_with_duplicate_and_test_in_seen():
         assert np.array_equal(a, b)
 
 
+def test_negatives_user_out_of_range_raises():
+    """A user index past the CSR's rows is refused (the reference's indexing raises IndexError), and numpy's
+    global state is left untouched."""
+    from hvae import ops
+    indptr = np.array([0, 2, 3], dtype=np.int64)
+    indices = np.array([1, 4, 0], dtype=np.int32)
+    np.random.seed(3)
+    before = np.random.get_state(legacy=True)[1].copy()
+    with pytest.raises(RuntimeError, match="bad user"):
+        ops.negatives_legacy(indptr, indices, 50, np.array([0, 2], np.int32), np.array([3, 3], np.int32), 9)
+    assert np.array_equal(np.random.get_state(legacy=True)[1], before)
+
+
 @pytest.mark.parametrize("workers", [1, 3])
 @pytest.mark.parametrize("form", ["simd", "scalar"])
 def test_negatives_boundary_sizes(workers, form, monkeypatch):
