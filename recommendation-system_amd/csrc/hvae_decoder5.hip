@@ -55,6 +55,9 @@ __device__ unsigned long long dec5_tm[2048 * 8];
 #ifndef DEC5_GLDS
 #define DEC5_GLDS 0
 #endif
+#ifndef DEC5_CRSTAGE
+#define DEC5_CRSTAGE 0
+#endif
 
 template <bool WITH_O>
 __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, int64_t ldu,
@@ -556,6 +559,23 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
       wait_vmcnt<0>();
     }
   }
+#if DEC5_CRSTAGE
+  // DEC5_CRSTAGE=1 (A/B): the consumer's PB pieces of each tile through registers instead of LDS-DMA -- loaded by
+  // buffer_load_dwordx4 in GEMM2(t)'s first gaps (tile t + 2; past the split the loads re-read tile t and are not
+  // written), written by ds_write_b128 into the same image bytes before the next iteration's barrier
+  uint4 cst[PB > 0 ? PB : 1];
+  auto c_load = [&](uint32_t soff, int k) {
+    const int p = q * PW + PA + k;
+    const uint32_t so = soff + (uint32_t)(8 * ((p >> 1) & 3) * (D * 2) + 256 * (p >> 3) + 128 * (p & 1));
+    const int vo = ((p >> 1) & 1) ? vlane[1] : vlane[0];
+    cst[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, vo, (int)so, 0));
+  };
+  auto c_write = [&](int slot_i) {
+#pragma unroll
+    for (int k = 0; k < PB; ++k)
+      *reinterpret_cast<uint4*>(lds + slot_i * TB + (q * PW + PA + k) * 1024 + lane * 16) = cst[k];
+  };
+#endif
   barrier();  // [P0]
   if (DEC5_P32) barrier();  // [PX]
   barrier();  // [P1]
@@ -564,6 +584,9 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     const int cur = li % NS, s_dma = (li + 2) % NS, par = li & 1;
     DEC5_T(const unsigned long long tm0 = __builtin_amdgcn_s_memtime();)
     if constexpr (PB > 0) if (!(DEC5_ABL & (1 | 128))) wait_vmcnt<0>();
+#if DEC5_CRSTAGE
+    if (li >= 1 && t + 1 < t_end) c_write((li + 1) % NS);  // tile t + 1, loaded in the previous iteration
+#endif
     DEC5_T(const unsigned long long tm1 = __builtin_amdgcn_s_memtime();)
     if (!(DEC5_ABL & 2)) barrier();  // [L]
     DEC5_T(const unsigned long long tm2 = __builtin_amdgcn_s_memtime();)
@@ -573,9 +596,15 @@ __global__ void __launch_bounds__(512) k_dec5_bf16(const float* __restrict__ U, 
     // DEC5_BFREE (A/B): issue the pieces of tile t + 2 unconditionally (past the split they fill the free slot)
     const bool dma = !(DEC5_ABL & 1) && (DEC5_BFREE || t + 2 < t_end);
     const uint32_t soff_dma = tile_soff(dma ? t + 2 : t);
+#if DEC5_CRSTAGE
+    const uint32_t soff_ld = tile_soff(t + 2 < t_end ? t + 2 : t);
+#endif
     gemm2(lds + cur * TB, pf0, pf1, [&](int i) {
       const int ii = i - DEC5_CDMA_AT;
-#if DEC5_DMA_BURST
+#if DEC5_CRSTAGE
+      if constexpr (PB > 0)
+        if (ii >= 0 && ii < PB) c_load(soff_ld, ii);
+#elif DEC5_DMA_BURST
       if constexpr (PB > 0)
         if (dma && ii == 0)
           for (int k = 0; k < PB; ++k) issue_piece(soff_dma, s_dma, PA + k, k == 0);
@@ -670,6 +699,9 @@ __device__ __forceinline__ int pack4(float a, float b, float c, float d) {
 // 2: all 12 pieces of the (ug, hq) pair on the producer that way, none on the consumer
 #ifndef DEC5F8_RSTAGE
 #define DEC5F8_RSTAGE 0
+#endif
+#ifndef DEC5F8_CRSTAGE
+#define DEC5F8_CRSTAGE 0
 #endif
 
 template <bool WITH_O>
@@ -964,6 +996,20 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
       wait_vmcnt<0>();
     }
   }
+#if DEC5F8_CRSTAGE
+  // DEC5F8_CRSTAGE=1 (A/B; bf16: DEC5_CRSTAGE): the consumer's PB pieces through registers -- buffer_load_dwordx4 in
+  // GEMM2(t)'s first gaps (tile t + 2), ds_write_b128 into the same image bytes before the next barrier
+  uint4 cst[PB > 0 ? PB : 1];
+  auto c_load = [&](uint32_t soff, int k) {
+    cst[k] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
+                                           rsrc, voff, (int)(soff + (uint32_t)((q * PW + PA + k) * 1024)), 0));
+  };
+  auto c_write = [&](int slot_i) {
+#pragma unroll
+    for (int k = 0; k < PB; ++k)
+      *reinterpret_cast<uint4*>(lds + slot_i * TB8 + (q * PW + PA + k) * 1024 + lane * 16) = cst[k];
+  };
+#endif
   barrier();  // [P0]
   barrier();  // [PX]
   barrier();  // [P1]
@@ -972,6 +1018,9 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
     const int li = t - t_beg;
     const int cur = li % NS, s_dma = (li + 2) % NS, par = li & 1;
     if constexpr (PB > 0) if (!(DEC5F8_ABL & (1 | 128))) wait_vmcnt<0>();
+#if DEC5F8_CRSTAGE
+    if (li >= 1 && t + 1 < t_end) c_write((li + 1) % NS);  // tile t + 1, loaded in the previous iteration
+#endif
     if (!(DEC5F8_ABL & 2)) barrier();  // [L]
     // P(t): k-block 0 = item half 0 (elements 0..15), k-block 1 = half 1; lane half h supplies k-block h's scale
     const int4 y0 = reinterpret_cast<const int4*>(p_slot(par, pq0))[lane];
@@ -983,8 +1032,13 @@ __global__ void __launch_bounds__(512) k_dec5_f8(const float* __restrict__ U, in
     const int sbp = 127 + eh;
     const uint32_t soff_dma = tile_soff(t + 2);  // branch-free, as the producers'
     gemm2(lds + cur * TB8, pf, sbp, [&](int db) {
+#if DEC5F8_CRSTAGE
+      if constexpr (PB > 0)
+        if (db < PB) c_load(soff_dma, db);
+#else
       if constexpr (PB > 0)
         if (!(DEC5F8_ABL & 1) && db < PB) issue_piece(soff_dma, s_dma, PA + db, db == 0);
+#endif
     });
   }
   if constexpr (PB > 0) wait_vmcnt<0>();

@@ -278,8 +278,10 @@ class FusedTrainer:
         # catch-up, encoder and forward GEMMs) or "fwd" (before the first forward GEMM: the plan overlaps only the
         # catch-up and the encoder, and the forward GEMMs get every CU)
         self.plan_join = os.environ.get("HVAE_PLAN_JOIN", "apply")
-        # when the plan forks off the main stream: "late" (after the lazy-Adam catch-up) or "early" (before it)
-        self.plan_fork = os.environ.get("HVAE_PLAN_FORK", "late")
+        # when the plan forks off the main stream: "early" (before the lazy-Adam catch-up, so it overlaps the
+        # catch-up too) or "late" (after it). Syn-1M 1.197 -> 1.189 ms per step, Syn-10M 11.35-11.38 -> 11.35-11.37
+        # (profiles/r06_step_ab.jsonl); steps per graph replay 8 instead of 1 at B = 4096 changed nothing there
+        self.plan_fork = os.environ.get("HVAE_PLAN_FORK", "early")
         # batches up to MLP_ROWS_MAX_NB run the latent / projection MLP row-parallel (hvae_mlp_*_rows)
         self.mlp_rows = bool(int(os.environ.get("HVAE_MLP_ROWS", "1")))
         self._mlp_rows_cache: dict[int, bool] = {}
