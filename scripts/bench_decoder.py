@@ -35,6 +35,8 @@ def main():
                     "ENV=VAL settings read by the A/B library (HVAE_LIB=build_var/libhvae_ab.so; e.g. HVAE_DEC_V3=0), timed in "
                     "interleaved rounds")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--lam", type=float, default=3.0, help="--train: CSR entries per user 5 + Poisson(lam) (15 at "
+                                                           "the synthetic workloads)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
@@ -50,7 +52,7 @@ def main():
     if args.train:
         sys.path.insert(0, str(ROOT / "tests" / "golden"))
         from gen import synth_csr
-        x = ops.csr_from_scipy(synth_csr(args.nb, args.N, lam=3.0, seed=5), dev)
+        x = ops.csr_from_scipy(synth_csr(args.nb, args.N, lam=args.lam, seed=5), dev)
         step = lambda: ops.decoder_train(x, U, E, enorm, E32, 1.0 / args.nb)  # noqa: E731
     else:
         step = lambda: ops.decoder_fwd(U, E, enorm)  # noqa: E731
