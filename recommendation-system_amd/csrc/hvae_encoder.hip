@@ -978,12 +978,15 @@ extern "C" int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad*
     HVAE_LAUNCH_CHECK("k_rg_plan_small");
     return HVAE_OK;
   }
-  // the sorted plan (hvae_rgsort.hip): one stable radix sort instead of per-item atomics, for the large batches of
-  // data parallelism's union (W x B rows): 3.6x faster at W = 8 (782 -> 216 us), 1.5x at one rank's batch (121
-  // -> 79 us, profiles/r03_rowgrad_sorted_vs_atomic.jsonl). Below kSortedPlanMinCap entries the atomic plan stays:
-  // the sort's 15 launches against the atomic plan's 4 make the captured step's host-side replay outlast the GPU
-  // at Syn-1M (1.20 -> 1.30 ms per step). HVAE_RG_SORTED (A/B build): 1 always sorted, 0 never.
-  constexpr int64_t kSortedPlanMinCap = 150000;
+  // the sorted plan (hvae_rgsort.hip): one stable radix sort instead of per-item atomics: 3.6x faster at data
+  // parallelism's W = 8 union (782 -> 216 us), 1.5x at one rank's batch (121 -> 79 us,
+  // profiles/r03_rowgrad_sorted_vs_atomic.jsonl). Round 3 kept the atomic plan below 150 K entries because the
+  // step measured slower with the sort at Syn-1M (1.20 -> 1.30 ms) -- but that step was host-bound on a per-step
+  // sort of all row lengths in the run loop (fixed in round 6); with the host ahead of the device the sorted plan
+  // runs Syn-1M in 1.061-1.064 ms against 1.141 and the Syn-10M shard in 10.95-10.97 against 11.01-11.02
+  // (profiles/r06_rowgrad_sorted_ab.jsonl), so it now serves every batch past the one-block plan's reach from
+  // kSortedPlanMinCap entries. HVAE_RG_SORTED (A/B build): 1 always sorted, 0 never.
+  constexpr int64_t kSortedPlanMinCap = 32768;
   const int sorted_ab = env_flag_ab("HVAE_RG_SORTED", -1);
   if (sorted_ab == 1 || (sorted_ab == -1 && rg->cap >= kSortedPlanMinCap)) {
     const int rc = rg_plan_sorted(x, rg, st);

@@ -131,7 +131,7 @@ def test_decoder_d384_v5w_agrees_v2(ops, dev, nb, N, monkeypatch):
 @pytest.mark.parametrize("nb,N,lam,hot", [(4096, 100_000, 15.0, 300), (300, 2000, 8.0, 100), (40000, 3000, 1.0, 6000),
                                          (2000, 1_000_003, 15.0, 0), (32768, 1_000_000, 15.0, 0)])
 def test_rowgrad_sorted_plan_equals_atomic_plan(ops, dev, nb, N, lam, hot, monkeypatch):
-    """The radix-sort plan (hvae_rgsort.hip, HVAE_RG_SORTED=1; the product's for batches of >= 150 K entries) against
+    """The radix-sort plan (hvae_rgsort.hip, HVAE_RG_SORTED=1; the product's for batches of >= 32 K entries) against
     the atomic plan (HVAE_RG_SORTED=0): every
     output the apply and the lazy Adam read is bitwise equal (slots, segments, contributions and their slots,
     slot_of at the batch's items), and so are the gradient rows."""
