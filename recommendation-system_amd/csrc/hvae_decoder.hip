@@ -1104,15 +1104,6 @@ struct FinArgs {
   int v6_upb, v6_nub, v6_S, v6_main, v6_P;
 };
 
-// FIN_GROUPS=2 (A/B): at D <= 512 (V4) the sparse terms run on two 128-thread groups, group g taking the CSR entry
-// batches g, g + 2, ... of its row (each group's sum in entry order, then group 0 + group 1): twice the E-row
-// loads in flight per block, where one group of D / 4 threads left the other 256 - D / 4 idle. Measured at the
-// Syn-1M shape (5 + Poisson(15) entries a row): the finalize 42.3-42.7 -> 35.8-36.5 us, the Syn-1M step unchanged
-// (1.155-1.158 ms both, profiles/r06_finalize_groups_ab.jsonl), and its sum order differs from hvae_decoder_bwd's,
-// which the fused-train test holds bitwise; so it stays off
-#ifndef FIN_GROUPS
-#define FIN_GROUPS 1
-#endif
 #ifndef FIN_EB_V4
 #define FIN_EB_V4 8  // 16-B form: 8 entries x 16 B in flight per thread (59 VGPRs, 7 waves per SIMD) beat 16 (99, 4): Syn-1M shape 33.5 -> 27.9 us, Syn-10M 45.5 -> 39.8 (profiles/r05_finalize_eb_ab.jsonl)
 #endif
@@ -1148,13 +1139,9 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     sp_beg = a.row_ptr[r];
     sp_end = a.row_ptr[r + 1];
   }
-  // two entry groups (FIN_GROUPS): thread tid is column group tid % 128 of entry group tid / 128
-  const bool grp2 = V4 && FIN_GROUPS == 2 && a.D <= 512;
-  const int egrp = grp2 ? (tid >> 7) : 0;
-  const int ect = grp2 ? (tid & 127) : tid;
 #pragma unroll
   for (int u = 0; u < EB; ++u) {
-    const int64_t e = sp_beg + egrp * EB + u;
+    const int64_t e = sp_beg + u;
     sp_j[u] = e < sp_end ? a.col_idx[e] : 0;
     sp_x[u] = e < sp_end ? a.vals[e] : 0.f;
   }
@@ -1353,9 +1340,8 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
   // E loads in flight together (the first chunk's indices were fetched before the merge)
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   float n = 0.f;
-  const int64_t e_first = sp_beg + egrp * EB;
-  for (int64_t e0 = e_first; e0 < sp_end; e0 += (grp2 ? 2 : 1) * EB) {
-    if (e0 != e_first) {
+  for (int64_t e0 = sp_beg; e0 < sp_end; e0 += EB) {
+    if (e0 != sp_beg) {
 #pragma unroll
       for (int u = 0; u < EB; ++u) {
         const int64_t e = e0 + u;
@@ -1365,10 +1351,10 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     }
     float ev[EB][4];
     if constexpr (V4) {
-      const bool act = 4 * ect < D;
+      const bool act = 4 * tid < D;
 #pragma unroll
       for (int u = 0; u < EB; ++u) {
-        const float4 v = (e0 + u < sp_end && act) ? ld4(a.E32 + (int64_t)sp_j[u] * D + 4 * ect)
+        const float4 v = (e0 + u < sp_end && act) ? ld4(a.E32 + (int64_t)sp_j[u] * D + 4 * tid)
                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
         ev[u][0] = v.x; ev[u][1] = v.y; ev[u][2] = v.z; ev[u][3] = v.w;
       }
@@ -1387,21 +1373,6 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
       n += sp_x[u];
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc[k] += sp_x[u] * ev[u][k];
-    }
-  }
-  if (grp2) {  // group 0 + group 1, through obuf (free again: the fixup's use ended at its barrier)
-    __syncthreads();
-    if (egrp == 1 && 4 * ect < D) reinterpret_cast<float4*>(obuf)[ect] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    if (tid == 128) pbuf[0] = n;
-    __syncthreads();
-    if (egrp == 0) {
-      if (4 * ect < D) {
-        const float4 v = reinterpret_cast<const float4*>(obuf)[ect];
-        acc[0] += v.x; acc[1] += v.y; acc[2] += v.z; acc[3] += v.w;
-      }
-      n += pbuf[0];
-    } else {
-      acc[0] = acc[1] = acc[2] = acc[3] = 0.f;
     }
   }
   float dot = 0.f;
