@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define HVAE_ABI_VERSION 3
+#define HVAE_ABI_VERSION 4
 
 enum {
   HVAE_OK = 0,
@@ -157,6 +157,18 @@ size_t hvae_w1_rowgrad_workspace(int64_t n_items);
 int hvae_w1_rowgrad_plan(const hvae_csr_batch* x, const hvae_rowgrad* rg, void* ws, size_t ws_bytes,
                          void* stream);
 int hvae_w1_rowgrad_apply(const float* da, int64_t H, const hvae_rowgrad* rg, void* stream);
+
+/* Trainable item embeddings (HybridVAE(freeze_embeddings=False), reference src/ml/model.py:72-75): the pieces the
+ * fused step adds for E's gradient dE_i = (1/B) sum_b (n_b softmax(u_b E^T)_i - x_bi) u_b (ABI 4).
+ *   hvae_csr_row_sums:        out[b] = n_b = sum of batch row b's stored values.
+ *   hvae_softmax_weights:     S[b][c] = alpha * w[b] * exp(S[b][c] - lse[b]), in place (S: nb rows of ld floats).
+ *   hvae_rowgrad_scatter_rows: dst[item_of[s]][0:width] += alpha * rows[s][0:width] for the plan's slots
+ *                             s < n_unique (rows as hvae_w1_rowgrad_apply wrote them with H = width). */
+int hvae_csr_row_sums(const hvae_csr_batch* x, float* out, void* stream);
+int hvae_softmax_weights(float* S, int64_t ld, int64_t nb, int64_t ncol, const float* lse, const float* w,
+                         float alpha, void* stream);
+int hvae_rowgrad_scatter_rows(const hvae_rowgrad* rg, int64_t width, float alpha, float* dst, int64_t ldd,
+                              void* stream);
 /* Scatter the row-sparse gradient into a dense, caller-zeroed buffer laid out
  * [N, ld] (item-major; ld >= H). */
 int hvae_rowgrad_to_dense(const hvae_rowgrad* rg, int64_t H, float* dense, int64_t ld, void* stream);

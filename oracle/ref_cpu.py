@@ -146,9 +146,11 @@ def param_names(p: dict[str, torch.Tensor]) -> list[str]:
     return names
 
 
-def grads(p: dict[str, torch.Tensor], x: torch.Tensor, beta: float, enc_masks=None, proj_mask=None, eps=None):
-    """loss.backward() of VAETrainer.train_epoch (src/ml/train.py:88-90) -> (grads, losses)."""
-    names = param_names(p)
+def grads(p: dict[str, torch.Tensor], x: torch.Tensor, beta: float, enc_masks=None, proj_mask=None, eps=None,
+          train_e: bool = False):
+    """loss.backward() of VAETrainer.train_epoch (src/ml/train.py:88-90) -> (grads, losses). train_e: E is a
+    parameter too (HybridVAE(freeze_embeddings=False), src/ml/model.py:72-75; the first in parameters() order)."""
+    names = (["item_embeddings"] if train_e else []) + param_names(p)
     q = {k: (v.detach().clone().requires_grad_(k in names)) for k, v in p.items()}
     out = forward(q, x, True, enc_masks, proj_mask, eps)
     loss, recon, kl = vae_loss(out["scores"], x, out["mu"], out["logvar"], beta)
@@ -178,9 +180,9 @@ def adam_update(p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tens
 
 
 def train_step(p: dict[str, torch.Tensor], state: dict, x: torch.Tensor, beta: float, lr: float = 1e-3,
-               weight_decay: float = 0.0, enc_masks=None, proj_mask=None, eps=None) -> dict:
-    """One VAETrainer.train_epoch batch (src/ml/train.py:86-96): fwd, bwd, clip 5.0, Adam."""
-    g, losses = grads(p, x, beta, enc_masks, proj_mask, eps)
+               weight_decay: float = 0.0, enc_masks=None, proj_mask=None, eps=None, train_e: bool = False) -> dict:
+    """One VAETrainer.train_epoch batch (src/ml/train.py:86-96): fwd, bwd, clip 5.0, Adam (train_e: on E too)."""
+    g, losses = grads(p, x, beta, enc_masks, proj_mask, eps, train_e)
     total, coef = clip_coef(g)
     state["step"] = state.get("step", 0) + 1
     for n, gi in g.items():

@@ -15,7 +15,7 @@ import torch
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("HVAE_LIB", _HERE / "libhvae.so"))
 
-ABI_VERSION = 3  # include/hvae.h HVAE_ABI_VERSION
+ABI_VERSION = 4  # include/hvae.h HVAE_ABI_VERSION
 HVAE_OK = 0
 HVAE_F32 = 0
 HVAE_BF16 = 1
@@ -119,6 +119,9 @@ SIGNATURES = {
     "hvae_w1_rowgrad_plan": (cint, [P(CsrBatch), P(RowGrad), vp, sz, vp]),
     "hvae_w1_rowgrad_apply": (cint, [vp, i64, P(RowGrad), vp]),
     "hvae_rowgrad_to_dense": (cint, [P(RowGrad), i64, vp, i64, vp]),
+    "hvae_csr_row_sums": (cint, [P(CsrBatch), vp, vp]),
+    "hvae_softmax_weights": (cint, [vp, i64, i64, i64, vp, vp, f32, vp]),
+    "hvae_rowgrad_scatter_rows": (cint, [P(RowGrad), i64, f32, vp, i64, vp]),
     "hvae_rowgrad_part_floats": (i64, [i64, i64]),
     "hvae_gemm_f32": (cint, [cint, cint, i64, i64, i64, f32, vp, i64, vp, i64, f32, vp, i64, P(Epilogue), vp,
                              sz, vp]),

@@ -74,6 +74,11 @@ class FlatLayout:
 
         add("w1t", (self.n_items, self.hidden[0]))
         self.small_offset = off
+        # trainable item embeddings (HybridVAE(freeze_embeddings=False), reference model.py:72-75): E is the
+        # reference's first parameter and has a dense gradient, so it opens the dense segment (clip + Adam cover it)
+        self.train_e = bool(getattr(model, "item_embeddings_trainable", False))
+        if self.train_e:
+            add("item_embeddings", (self.n_items, self.d))
         prev = self.hidden[0]
         for k, hd in enumerate(self.hidden):
             i = 4 * k
@@ -206,8 +211,16 @@ class _StepBuffers:
         self.da = [f(B, hd) for hd in H]
         self.loss3 = f(3)
         # the local row gradient (single GPU); data parallel steps build the union's in the exchange
-        self.rg = ops.RowGradBuffers(lay.n_items, H[0], cap, dev) if (train and ex.dp is None) else None
+        # (with trainable E the plan also gathers rows of u, width d)
+        self.rg = (ops.RowGradBuffers(lay.n_items, H[0], cap, dev, width=d if ex.train_e else None)
+                   if (train and ex.dp is None) else None)
         self.cap = cap
+        # trainable E: dE's dense term in item chunks of e_chunk columns (S = u E_c^T, at most 64 M floats)
+        self.e_chunk = 0
+        if train and ex.train_e:
+            self.e_chunk = int(min(lay.n_items, max(64, (1 << 26) // max(B, 1) // 64 * 64)))
+            self.S = f(B, self.e_chunk)
+            self.nrow = f(B)
         L_ = lib()
         need = [
             L_.hvae_decoder_workspace(ex.dec_dtype, B, lay.n_items, d),
@@ -226,6 +239,8 @@ class _StepBuffers:
             gemms += [(B, d, L), (B, d, d), (d, d, B), (d, L, B), (B, d, d), (B, L, d)]
         for k in range(1, len(H)):
             gemms += [(B, H[k], H[k - 1]), (H[k], H[k - 1], B), (B, H[k - 1], H[k])]
+        if self.e_chunk:
+            gemms += [(B, self.e_chunk, d), (self.e_chunk, d, B)]
         for (m_, n_, k_) in gemms:
             need.append(L_.hvae_gemm_f32_workspace(m_, n_, k_))
         self.ws = torch.empty(max(int(max(need)), 256), dtype=torch.uint8, device=dev)
@@ -251,9 +266,12 @@ class FusedTrainer:
         self.layout = lay = FlatLayout(model)
         self.lr, self.wd, self.betas, self.eps, self.max_norm = lr, weight_decay, betas, eps, max_norm
         self.use_graphs = use_graphs
-        if getattr(model, "item_embeddings_trainable", False):
-            raise NotImplementedError("fused trainer: trainable item embeddings (freeze_embeddings=False) "
-                                      "are not supported; the reference trains with a frozen E")
+        # trainable item embeddings: E lives in the flat dense segment; each step refreshes the decoder's image of
+        # it, adds its gradient (hvae_embed.hip) and Adam moves it with the other dense parameters
+        self.train_e = lay.train_e
+        if self.train_e and process_group is not None and torch.distributed.get_world_size(process_group) > 1:
+            raise NotImplementedError("fused trainer: data parallelism covers frozen item embeddings only (a "
+                                      "trainable E would need its dense [N, d] gradient all-reduced every step)")
         self.seed = int(seed if seed is not None else torch.randint(0, 2 ** 62, (1,)).item())
         # ---- flat state
         self.flat = torch.zeros(lay.total, device=device)
@@ -400,6 +418,9 @@ class FusedTrainer:
             for n in names:
                 self.P[n] = V(f, n)
                 self.G[n] = V(self.g_small, n, base)
+        if lay.train_e:
+            self.P["item_embeddings"] = V(f, "item_embeddings")
+            self.G["item_embeddings"] = V(self.g_small, "item_embeddings", base)
         self.W_heads, self.b_heads = lay.heads(f)
         self.gW_heads, self.gb_heads = lay.heads(self.g_small, base)
         if lay.has_proj:
@@ -537,6 +558,11 @@ class FusedTrainer:
         # can read W1t through lazy Adam itself (rows replayed in registers), so no catch-up launch precedes it
         fused_enc = self._mlp_rows_ok(B) and len(H) == 1 and H[0] <= 512
         enc_lazy = train and not dp and self.lazy_adam and self.enc_lazy_read and fused_enc
+        if self.train_e:
+            # E moved with the last step's Adam: the decoder's image of it and max||E|| follow (in the captured step)
+            if isinstance(self.E_dec, ops.DecoderImage):
+                self.E_dec.refresh(self.E32)
+            ops.row_norm_max(self.E_dec, out=self.enorm)
         anneal = self._anneal if train else None
         beta_dev = None
         if anneal is not None:  # this step's (beta, beta / B) from the device schedule counter, which it advances
@@ -653,6 +679,11 @@ class FusedTrainer:
             gemm(0, 1, B, d, Lt, ptr(bf.z), Lt, ptr(Wa), Lt, ptr(bf.q), d, epi1)
             epi2 = Epilogue(_lib.EPI_BIAS, ptr(bb), None, None, 0.0, None, 0, None, 0, 0, None)
             gemm(0, 1, B, d, d, ptr(bf.q), d, ptr(Wb), d, ptr(bf.u), d, epi2)
+        if ev_plan is not None and self.plan_join == "sweep" and not dp:
+            # (HVAE_PLAN_JOIN=sweep: the plan's last kernels finish before the sweep takes every CU, instead of
+            # waiting beside it)
+            main.wait_event(ev_plan)
+            ev_plan = None
         accum = self.accum_train if train else self.accum_val
         # decoder sweep + finalize (split merge, sparse loss terms, du) + the batch loss means, one call
         check(L_.hvae_decoder_train(self.dec_dtype, ptr(bf.u), d, ptr(self.E_dec), ptr(self.enorm), ptr(self.E32),
@@ -663,6 +694,18 @@ class FusedTrainer:
             return
         # ----------------------------------------------------- backward ---
         G = self.G
+        if self.train_e:
+            # dE's dense term (1/B) sum_b n_b softmax(u_b E^T)_i u_b in item chunks: S = u E_c^T, S <- (n_b / B)
+            # exp(S - lse_b), dE_c = S^T u (hvae_embed.hip; the sparse term follows the plan, below)
+            gE = G["item_embeddings"]
+            check(L_.hvae_csr_row_sums(csr_ref, ptr(bf.nrow), st), "csr_row_sums")
+            Cc, N_ = bf.e_chunk, lay.n_items
+            for c0 in range(0, N_, Cc):
+                cn = min(Cc, N_ - c0)
+                gemm(0, 1, B, cn, d, ptr(bf.u), d, ptr(self.E32) + 4 * c0 * d, d, ptr(bf.S), Cc)
+                check(L_.hvae_softmax_weights(ptr(bf.S), Cc, B, cn, ptr(bf.lse), ptr(bf.nrow), 1.0 / B, st),
+                      "softmax_weights")
+                gemm(1, 0, cn, d, B, ptr(bf.S), Cc, ptr(bf.u), d, ptr(gE) + 4 * c0 * d, d)
 
         def layer_bwd(wgrad: tuple, wrowsum, xgrad: tuple, xepi=None):
             """A layer's weight gradient (trans_a GEMM on the side stream) and data gradient: with one stream,
@@ -759,6 +802,12 @@ class FusedTrainer:
         if ev_plan is not None:
             main.wait_event(ev_plan)
         if not dp:
+            if self.train_e:
+                # dE's sparse term -(1/B) sum_b x_bi u_b over the plan's item segments (the apply with u for da),
+                # before the W1 rows take the same buffer
+                check(L_.hvae_w1_rowgrad_apply(ptr(bf.u), d, bf.rg.ref, st), "w1_rowgrad_apply(u)")
+                check(L_.hvae_rowgrad_scatter_rows(bf.rg.ref, d, -1.0 / B, ptr(G["item_embeddings"]), d, st),
+                      "rowgrad_scatter_rows")
             check(L_.hvae_w1_rowgrad_apply(ptr(bf.da[0]), H[0], bf.rg.ref, st), "w1_rowgrad_apply")
         self._fork(side, main)  # join: every gradient is complete on the main stream
 

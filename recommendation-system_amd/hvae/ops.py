@@ -128,7 +128,10 @@ def ln_gelu_drop_bwd(dh, xhat, rstd, ln_w, ln_b, p_drop, train, seed, layer, ste
 class RowGradBuffers:
     """Device buffers of the row-sparse first-layer weight gradient."""
 
-    def __init__(self, n_items: int, H: int, cap: int, device):
+    def __init__(self, n_items: int, H: int, cap: int, device, width: int | None = None):
+        """width: the widest row the buffers must hold (default H): the fused step with trainable item embeddings
+        also gathers rows of the decoder input u (width d) through the same plan."""
+        W = max(H, width or H)
         i32 = dict(dtype=torch.int32, device=device)
         self.cnt = torch.zeros(n_items, **i32)
         self.slot_of = torch.full((n_items,), -1, **i32)
@@ -137,10 +140,10 @@ class RowGradBuffers:
         self.fill = torch.zeros(cap, **i32)
         self.contrib_row = torch.zeros(cap, **i32)
         self.contrib_val = torch.zeros(cap, dtype=torch.float32, device=device)
-        self.rows = torch.zeros(cap, H, dtype=torch.float32, device=device)
+        self.rows = torch.zeros(cap * W, dtype=torch.float32, device=device)[:cap * H].view(cap, H)
         self.n_unique = torch.zeros(1, **i32)
         self.contrib_slot = torch.zeros(cap, **i32)
-        self.part = torch.empty(int(lib().hvae_rowgrad_part_floats(cap, H)), dtype=torch.float32, device=device)
+        self.part = torch.empty(int(lib().hvae_rowgrad_part_floats(cap, W)), dtype=torch.float32, device=device)
         self.rowsq = torch.zeros(cap * ROWSQ_PARTS, dtype=torch.float64, device=device)
         self.cap, self.n_items, self.H = cap, n_items, H
         self.struct = RowGrad(ptr(self.cnt), ptr(self.slot_of), ptr(self.item_of), ptr(self.seg_off), ptr(self.fill),

@@ -13,6 +13,7 @@ from __future__ import annotations
 import argparse
 import json
 import logging
+import os
 import pickle
 import time
 from pathlib import Path
@@ -227,11 +228,12 @@ class VAETrainer:
             device = torch.device("cuda", torch.cuda.current_device())
         self.model = model.to(device)
         self.device = device
-        if getattr(model, "item_embeddings_trainable", False):
-            # trainable E: the module-API step on libhvae kernels (scores materialised per batch, as the
-            # reference does), E updated with the other parameters
+        if getattr(model, "item_embeddings_trainable", False) and (
+                process_group is not None or os.environ.get("HVAE_TRAINABLE_E_MODULE", "0") == "1"):
+            # trainable E under data parallelism (or HVAE_TRAINABLE_E_MODULE=1): the module-API step on libhvae
+            # kernels (scores materialised per batch, as the reference does), E updated with the other parameters
             if process_group is not None:
-                raise NotImplementedError("data parallelism covers the fused (frozen-embedding) trainer")
+                raise NotImplementedError("data parallelism covers frozen item embeddings only")
             self.fused = None
             self.optimizer = ModuleAdam(model.parameters(), lr=lr, weight_decay=weight_decay)
         else:
@@ -243,7 +245,8 @@ class VAETrainer:
         self.train_recon_losses: list[float] = []
         self.train_kl_losses: list[float] = []
         logger.info(f"Trainer on {device}, {sum(p.numel() for p in model.parameters()):,} params, "
-                    f"decoder {self.fused.precision if self.fused is not None else 'module path (trainable E)'}")
+                    f"decoder {self.fused.precision if self.fused is not None else 'module path (trainable E)'}"
+                    f"{' (trainable E)' if getattr(model, 'item_embeddings_trainable', False) and self.fused else ''}")
 
     # beta of one training batch (reference: _compute_loss, train.py:71-79): AnnealedVAE's schedule runs on the
     # device inside the captured step (AnnealedBeta), so annealed epochs replay one graph like constant-beta ones
