@@ -245,7 +245,7 @@ class _StepBuffers:
             need.append(L_.hvae_gemm_f32_workspace(m_, n_, k_))
         self.ws = torch.empty(max(int(max(need)), 256), dtype=torch.uint8, device=dev)
         # side-stream GEMMs: their split-K slabs must not alias the main stream's
-        self.ws2 = torch.empty_like(self.ws) if ex.two_streams else None
+        self.ws2 = torch.empty_like(self.ws) if ex.side is not None else None
         self.graph = None
         self.graph_k, self.graph_k_steps = None, 0  # single GPU: K consecutive steps in one graph (host-bound steps)
         self.graph_pre = self.graph_up = None  # data parallel: the CSR-packet and update graphs of a step
@@ -291,7 +291,10 @@ class FusedTrainer:
         # edge of the captured graph costs 5-10 us, more than the short kernels it overlaps. Off by
         # default; the dependency structure stays in place for the larger configurations.
         self.two_streams = bool(int(os.environ.get("HVAE_TWO_STREAMS", "0")))
-        self.side = torch.cuda.Stream(device) if self.two_streams else None
+        # HVAE_WGRAD_SIDE=1: only the weight-gradient GEMMs of the backward on the second stream (batches from
+        # plan_side_min_batch up), beside the data-gradient chain; the plan keeps its own stream
+        self.wgrad_side = bool(int(os.environ.get("HVAE_WGRAD_SIDE", "0")))
+        self.side = torch.cuda.Stream(device) if (self.two_streams or self.wgrad_side) else None
         # the W1-gradient plan needs only the batch: it runs on its own stream beside the forward and is joined
         # before the row-gradient apply (the lazy-Adam catch-up then reads the batch's rows from the CSR)
         self.plan_side = bool(int(os.environ.get("HVAE_PLAN_SIDE", "1")))
@@ -531,7 +534,8 @@ class FusedTrainer:
         """
         L_, lay = lib(), self.layout
         main = torch.cuda.current_stream(self.device)
-        side = self.side if self.side is not None else main
+        use_side = self.side is not None and (self.two_streams or bf.B >= self.plan_side_min_batch)
+        side = self.side if use_side else main
         st, st2 = main.cuda_stream, side.cuda_stream
         B, H, Lt, d = bf.B, lay.hidden, lay.L, lay.d
         ws, wsn = ptr(bf.ws), bf.ws.numel()
@@ -551,7 +555,7 @@ class FusedTrainer:
 
         ev_plan = None
         dp = self.dp is not None
-        plan_in_rows = (train and not dp and self.side is None and self.plan_in_rows and self._mlp_rows_ok(B)
+        plan_in_rows = (train and not dp and not use_side and self.plan_in_rows and self._mlp_rows_ok(B)
                         and not (self.plan_stream is not None and B >= self.plan_side_min_batch)
                         and bf.rg.struct.cap <= _lib.PLAN_SMALL_CAP and B <= _lib.PLAN_SMALL_CAP)
         # one hidden layer of H <= 512 with the row-parallel MLP: the encoder layer runs in hvae_mlp_fwd_rows, which
@@ -627,6 +631,9 @@ class FusedTrainer:
                 check(L_.hvae_adam_lazy_catchup(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
                                                 ptr(self.v), ptr(self.last_step), bf.rg.ref, lay.n_items, H[0],
                                                 st2), "adam_lazy_catchup")
+                # the forward reads the rows this catch-up replays: it waits for it (HVAE_TWO_STREAMS=1 let the
+                # encoder start beside it)
+                self._fork(side, main)
             if side is not main:
                 ev_plan = torch.cuda.Event()
                 ev_plan.record(side)
