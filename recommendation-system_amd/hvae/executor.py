@@ -291,9 +291,10 @@ class FusedTrainer:
         # edge of the captured graph costs 5-10 us, more than the short kernels it overlaps. Off by
         # default; the dependency structure stays in place for the larger configurations.
         self.two_streams = bool(int(os.environ.get("HVAE_TWO_STREAMS", "0")))
-        # HVAE_WGRAD_SIDE=1: only the weight-gradient GEMMs of the backward on the second stream (batches from
-        # plan_side_min_batch up), beside the data-gradient chain; the plan keeps its own stream
-        self.wgrad_side = bool(int(os.environ.get("HVAE_WGRAD_SIDE", "0")))
+        # the weight-gradient GEMMs of the backward run on a second stream beside the data-gradient chain (batches
+        # from plan_side_min_batch up; the plan keeps its own stream): Syn-1M 1.082 -> 1.061 ms per step, Syn-10M
+        # bf16 / fp8 -0.1 / -0.3 % (profiles/r06_wgrad_side_ab.jsonl). HVAE_WGRAD_SIDE=0: one stream
+        self.wgrad_side = bool(int(os.environ.get("HVAE_WGRAD_SIDE", "1")))
         self.side = torch.cuda.Stream(device) if (self.two_streams or self.wgrad_side) else None
         # the W1-gradient plan needs only the batch: it runs on its own stream beside the forward and is joined
         # before the row-gradient apply (the lazy-Adam catch-up then reads the batch's rows from the CSR)
