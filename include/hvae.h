@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define HVAE_ABI_VERSION 4
+#define HVAE_ABI_VERSION 5
 
 enum {
   HVAE_OK = 0,
@@ -490,6 +490,34 @@ int hvae_adam_lazy_catchup(const hvae_adam* cfg, const float* tab, float* p, flo
                            int32_t* last_step, const hvae_rowgrad* rows, int64_t N, int64_t H, void* stream);
 int hvae_adam_lazy_catchup_csr(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v,
                                int32_t* last_step, const hvae_csr_batch* x, int64_t H, void* stream);
+/* Deferred W1t update (ABI 5; no reference counterpart -- a schedule of the same torch.optim.Adam step,
+ * src/ml/train.py:92). hvae_adam_lazy_defer is hvae_adam_lazy except that the gradient rows do not move: the
+ * dense segment steps, and each gradient row j is recorded as pending (last_step[j] bit 30, pend->slot_of[j] =
+ * its slot in rg, pend->item_of[slot] = j, the step, rg->rows, H, the clip multiplier and the row count in
+ * pend->hdr). The rows then take that step later, with hvae_adam_lazy's float operations (bitwise the same
+ * parameters and moments):
+ *   hvae_adam_lazy_catchup_csr_pending -- hvae_adam_lazy_catchup_csr that also applies the recorded step to the
+ *     listed rows that carry it (the next batch's rows, before its forward reads them; *cfg->step_dev must equal
+ *     the recorded step, i.e. no clip in between);
+ *   hvae_adam_lazy_pending -- every pending row no catch-up has claimed, and the recorded step's sweep range
+ *     (hvae_adam_lazy_sweep_period), on any stream, beside the next step's forward; max_rows bounds the rows
+ *     recorded (grid size). A second run is a no-op.
+ * The recorded gradient rows (rg->rows) must stay as they are until hvae_adam_lazy_pending has run, and it must
+ * run before the next hvae_adam_lazy / _defer, a catch-up over all rows, or any other read of W1t, m or v.
+ *   pend->slot_of [N] int32, pend->item_of [N] int32, pend->hdr 32 bytes of device memory, zeroed once. */
+typedef struct hvae_adam_pend {
+  int32_t* slot_of;
+  int32_t* item_of;
+  void* hdr;
+} hvae_adam_pend;
+int hvae_adam_lazy_defer(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
+                         int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense,
+                         int64_t dense_off, int64_t n_dense, const hvae_adam_pend* pend, void* stream);
+int hvae_adam_lazy_catchup_csr_pending(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v,
+                                       int32_t* last_step, const hvae_csr_batch* x, int64_t H,
+                                       const hvae_adam_pend* pend, void* stream);
+int hvae_adam_lazy_pending(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v, int32_t* last_step,
+                           int64_t N, int64_t H, int64_t max_rows, const hvae_adam_pend* pend, void* stream);
 /* *counter += delta (device-side step/batch counters for graph replay). */
 int hvae_counter_add(int64_t* counter, int64_t delta, void* stream);
 /* *a += da and, if b != NULL, *b += db, in one launch (end of a train step). */

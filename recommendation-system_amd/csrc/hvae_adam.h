@@ -91,6 +91,19 @@ constexpr int kPAheadMax = 63;
 __device__ __forceinline__ int ls_mv(int32_t ls) { return ls & kStepMask; }
 __device__ __forceinline__ int ls_p(int32_t ls) { return (ls & kStepMask) + ((ls >> kStepBits) & kPAheadMax); }
 
+// Deferred updates (hvae_adam_lazy_defer, ABI 5): bit 30 of last_step[j] marks a row whose step-t update -- its
+// gradient row rows[pend_slot[j] * ld], times coef -- has been recorded but not applied yet; the low 30 bits keep
+// their meaning (the steps m, v and p had before it). The header of the recorded step lives in device memory.
+constexpr int32_t kPendBit = 1 << 30;
+struct PendHdr {
+  int64_t t;          // the recorded step (0: nothing was ever recorded)
+  const float* rows;  // its gradient rows
+  int64_t ld;         // their stride (H)
+  float coef;         // its clip multiplier
+  int32_t n;          // its gradient rows: pend_item[0 : n]
+};
+static_assert(sizeof(PendHdr) == 32, "hvae_adam_pend.hdr is 32 bytes");
+
 struct AdamArgs {
   double lr, b1, b2, eps, wd;
   const int64_t* step_dev;

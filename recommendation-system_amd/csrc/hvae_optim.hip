@@ -265,15 +265,26 @@ __global__ void __launch_bounds__(256) k_adam_catchup(AdamArgs a, const float2* 
 // s, s + S, s + 2 S, .. (S slices per row, so that a small batch still spreads its rows' replays over the
 // machine: at B = 64 one block per row left 64 blocks walking ~20 rows each, one memory round trip after
 // another); all of a group's entries claim at once, then every thread walks the claimed rows' float4 columns.
+// With a deferred step recorded (hdr != NULL, ABI 5), a listed row that carries it (last_step bit 30) is claimed
+// like any other and takes that step here -- its missed steps replayed, then step hdr->t with its gradient row
+// times hdr->coef, k_adam_lazy's float operations -- and stores p, m and v (the caller passes to == hdr->t).
 template <int U>
 __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const float2* __restrict__ tab, float* p,
                                                           float* m, float* v, int32_t* __restrict__ last_step,
-                                                          hvae_csr_batch x, int64_t H, int S, int p_only_arg) {
-  __shared__ int s_j[256], s_from[256], s_pst[256];
+                                                          hvae_csr_batch x, int64_t H, int S, int p_only_arg,
+                                                          const int32_t* __restrict__ pend_slot,
+                                                          const PendHdr* __restrict__ hdr) {
+  __shared__ int s_j[256], s_from[256], s_pst[256], s_slot[256];
   __shared__ int s_n;
   const int to = (int)load_step(a.step_dev);
   const int64_t H4 = H / 4;
   const AdamK none{};
+  // the recorded step's constants and gradient rows (when one is pending at step `to`)
+  const bool pend_on = hdr != nullptr && hdr->t == (int64_t)to && to > 0;
+  const float* prow = pend_on ? hdr->rows : nullptr;
+  const int64_t pld = pend_on ? hdr->ld : 0;
+  const float pcoef = pend_on ? hdr->coef : 1.f;
+  const AdamK kp = pend_on ? adam_consts_tab(a, tab[to]) : none;
   // p alone moves ahead unless weight decay couples m, v to p, or m, v are too far behind to say so in the stamp
   const bool p_only_ok = a.wd == 0.0 && p_only_arg;
   const int sl = (int)(blockIdx.x % (unsigned)S);
@@ -291,8 +302,9 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
         // stamp replays it; entries that find p already at `to` (another entry claimed it) do nothing
         int32_t old = __hip_atomic_load(last_step + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         while (ls_p(old) < to) {
+          const bool pend = pend_on && (old & kPendBit);
           const int mv = ls_mv(old);
-          const bool p_only = p_only_ok && to - mv <= kPAheadMax;
+          const bool p_only = !pend && p_only_ok && to - mv <= kPAheadMax;
           const int32_t want = p_only ? (int32_t)(mv | ((to - mv) << kStepBits)) : (int32_t)to;
           if (__hip_atomic_compare_exchange_strong(last_step + j, &old, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_AGENT)) {
@@ -300,6 +312,7 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
             s_j[k] = j;
             s_from[k] = p_only ? -1 - mv : mv;  // negative: store p only
             s_pst[k] = ls_p(old);
+            s_slot[k] = pend ? pend_slot[j] : -1;  // >= 0: take the recorded step with this gradient row
             break;
           }
         }
@@ -309,7 +322,8 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
       for (int64_t i0 = threadIdx.x; i0 < work; i0 += (int64_t)blockDim.x * U) {
         ColState cs[U];
         int64_t col[U];
-        int fr[U], ps[U];
+        int fr[U], ps[U], sl[U];
+        float4 gv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int64_t idx = i0 + (int64_t)u * blockDim.x;
@@ -317,13 +331,22 @@ __global__ void __launch_bounds__(256) k_adam_catchup_csr(AdamArgs a, const floa
           col[u] = idx < work ? (int64_t)s_j[k] * H4 + idx % H4 : -1;
           fr[u] = s_from[k];
           ps[u] = s_pst[k];
+          sl[u] = pend_on ? s_slot[k] : -1;
           if (col[u] >= 0) cs[u] = col_load(p, m, v, col[u]);
+          if (col[u] >= 0 && sl[u] >= 0) gv[u] = *reinterpret_cast<const float4*>(prow + sl[u] * pld + 4 * (idx % H4));
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (col[u] >= 0)
+        for (int u = 0; u < U; ++u) {
+          if (col[u] < 0) continue;
+          if (sl[u] >= 0) {  // k_adam_lazy's row update: replay to to - 1, then step `to` with coef * g
+            float4 g = gv[u];
+            g.x *= pcoef; g.y *= pcoef; g.z *= pcoef; g.w *= pcoef;
+            col_math_lazy(a, tab, cs[u], fr[u], ps[u], to - 1, true, kp, g);
+          } else {
             col_math_lazy(a, tab, cs[u], fr[u] < 0 ? -1 - fr[u] : fr[u], ps[u], to, false, none,
                           make_float4(0.f, 0.f, 0.f, 0.f));
+          }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if (col[u] < 0) continue;
@@ -366,7 +389,8 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
                                                    const int32_t* __restrict__ n_unique, int64_t N, int64_t H,
                                                    const float* __restrict__ g_dense, int64_t dense_off,
                                                    int64_t n_dense, int nb_rows, int nb_sweep, int period,
-                                                   RowMap rm) {
+                                                   RowMap rm, int32_t* __restrict__ pend_slot,
+                                                   int32_t* __restrict__ pend_item, PendHdr* __restrict__ hdr) {
   const int t = (int)load_step(a.step_dev) + 1;
   // tab[t] is written by hvae_clip_grad_norm_step_adam just before; a zero entry means no one did
   const float2 c0t = tab[t];
@@ -378,7 +402,19 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
   const int64_t H4 = H / 4;
   const int rr = threadIdx.x / rm.h4s, cc = threadIdx.x % rm.h4s;
   const int64_t span = (int64_t)rm.rpb * U;
-  if ((int)blockIdx.x < nb_rows) {
+  if (hdr != nullptr && (int)blockIdx.x < nb_rows) {
+    // deferred (hvae_adam_lazy_defer): the gradient rows are recorded as pending, nothing moves; the next
+    // catch-up or k_adam_pending applies step t to each of them
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      hdr->t = t; hdr->rows = rows; hdr->ld = H; hdr->coef = coef; hdr->n = nu;
+    }
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nu; s += (int64_t)nb_rows * blockDim.x) {
+      const int32_t j = item_of[s];
+      pend_item[s] = j;
+      pend_slot[j] = (int32_t)s;
+      last_step[j] = last_step[j] | kPendBit;
+    }
+  } else if ((int)blockIdx.x < nb_rows) {
     for (int64_t g0 = (int64_t)blockIdx.x * span; g0 < nu; g0 += (int64_t)nb_rows * span) {
       int64_t sidx[U], j[U];
       int from[U], pst[U];
@@ -502,6 +538,70 @@ __global__ void __launch_bounds__(256) k_adam_lazy(AdamArgs a, float2* __restric
       float pp = pd[i], mm = md[i], vv = vd[i];
       adam_elem(pp, mm, vv, g_dense[i] * coef, k);
       pd[i] = pp; md[i] = mm; vd[i] = vv;
+    }
+  }
+}
+
+// The recorded step's W1t rows (hvae_adam_lazy_pending): blocks [0, nb_rows) take the pending gradient rows that
+// no catch-up has claimed since (k_adam_lazy's row update: missed steps replayed, then step t with coef * g);
+// blocks [nb_rows, nb_rows + nb_sweep) take step t's sweep range (k_adam_lazy's sweep: rows without a pending
+// update brought through step t; a row the catch-up moved p of to t replays m and v alone). Same float operations
+// as the undeferred update, so the rows are bitwise k_adam_lazy's. A second run finds nothing left to do.
+__global__ void __launch_bounds__(256) k_adam_pending(AdamArgs a, const float2* __restrict__ tab,
+                                                     float* __restrict__ p, float* __restrict__ m,
+                                                     float* __restrict__ v, int32_t* __restrict__ last_step,
+                                                     const int32_t* __restrict__ pend_slot,
+                                                     const int32_t* __restrict__ pend_item,
+                                                     const PendHdr* __restrict__ hdr, int64_t N, int64_t H,
+                                                     int nb_rows, int nb_sweep, int period, RowMap rm) {
+  const int64_t t64 = hdr->t;
+  if (t64 <= 0) return;
+  const int t = (int)t64;
+  const float* __restrict__ rows = hdr->rows;
+  const int64_t ld = hdr->ld;
+  const float coef = hdr->coef;
+  const int nu = hdr->n;
+  const AdamK k = adam_consts_tab(a, tab[t]);
+  const int64_t H4 = H / 4;
+  const int rr = threadIdx.x / rm.h4s, cc = threadIdx.x % rm.h4s;
+  if ((int)blockIdx.x < nb_rows) {
+    for (int64_t g0 = (int64_t)blockIdx.x * rm.rpb; g0 < nu; g0 += (int64_t)nb_rows * rm.rpb) {
+      const int64_t s = g0 + rr;
+      bool act = rr < rm.rpb && s < nu;
+      const int64_t j = act ? (int64_t)pend_item[s] : 0;
+      const int32_t ls = act ? last_step[j] : 0;
+      act = act && (ls & kPendBit) && pend_slot[j] == (int32_t)s;
+      const int from = ls_mv(ls), pst = ls_p(ls);
+      for (int64_t c = cc; c < H4; c += rm.h4s) {
+        if (!act) continue;
+        ColState cs = col_load(p, m, v, j * H4 + c);
+        float4 g = *reinterpret_cast<const float4*>(rows + s * ld + 4 * c);
+        g.x *= coef; g.y *= coef; g.z *= coef; g.w *= coef;
+        col_math_lazy(a, tab, cs, from, pst, t - 1, true, k, g);
+        col_store(p, m, v, j * H4 + c, cs);
+      }
+      __syncthreads();
+      if (act && cc == 0) last_step[j] = t;
+    }
+  } else if ((int)blockIdx.x < nb_rows + nb_sweep) {
+    const int64_t chunk = (N + period - 1) / period;
+    const int64_t r0 = (int64_t)((t - 1) % period) * chunk, r1 = min(N, r0 + chunk);
+    for (int64_t g0 = r0 + (int64_t)(blockIdx.x - nb_rows) * rm.rpb; g0 < r1; g0 += (int64_t)nb_sweep * rm.rpb) {
+      const int64_t j = g0 + rr;
+      bool act = rr < rm.rpb && j < r1;
+      const int32_t ls = act ? last_step[j] : 0;
+      act = act && !(ls & kPendBit) && ls_mv(ls) < t;
+      const int from = ls_mv(ls), pst = ls_p(ls);
+      for (int64_t c = cc; c < H4; c += rm.h4s) {
+        if (!act) continue;
+        ColState cs = col_load(p, m, v, j * H4 + c);
+        // through step t with g = 0: adam_elem0 (or adam_elem at g = 0 with weight decay) is bitwise k_adam_lazy's
+        // adam_elem(g = 0) step; steps p already has move m and v alone
+        col_math_lazy(a, tab, cs, from, pst, t, false, k, make_float4(0.f, 0.f, 0.f, 0.f));
+        col_store(p, m, v, j * H4 + c, cs);
+      }
+      __syncthreads();
+      if (act && cc == 0) last_step[j] = t;
     }
   }
 }
@@ -666,14 +766,72 @@ extern "C" int hvae_adam_lazy_catchup_csr(const hvae_adam* cfg, const float* tab
   ProbeScope probe("adam_catchup", as_stream(stream));
   const int pon = catchup_p_only();
   HVAE_ADAM_U_CALL(adam_unroll(), (k_adam_catchup_csr<U><<<grid, 256, 0, as_stream(stream)>>>(
-                                      to_args(cfg), (const float2*)tab, p, m, v, last_step, *x, H, S, pon)));
+                                      to_args(cfg), (const float2*)tab, p, m, v, last_step, *x, H, S, pon, nullptr,
+                                      nullptr)));
   HVAE_LAUNCH_CHECK("k_adam_catchup_csr");
   return HVAE_OK;
 }
 
+extern "C" int hvae_adam_lazy_catchup_csr_pending(const hvae_adam* cfg, const float* tab, float* p, float* m,
+                                                  float* v, int32_t* last_step, const hvae_csr_batch* x, int64_t H,
+                                                  const hvae_adam_pend* pend, void* stream) {
+  HVAE_REQUIRE(cfg && cfg->step_dev && tab && p && m && v && last_step && H % 4 == 0 && x && x->row_ptr &&
+                   x->col_idx && pend && pend->slot_of && pend->hdr,
+               "hvae_adam_lazy_catchup_csr_pending: bad args");
+  if (x->nb == 0) return HVAE_OK;
+  const int S = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv(kCatchupBlocks, x->nb), 64));
+  const unsigned grid = (unsigned)(std::min<int64_t>(x->nb, 16384) * S);
+  ProbeScope probe("adam_catchup", as_stream(stream));
+  const int pon = catchup_p_only();
+  k_adam_catchup_csr<kAdamUnroll><<<grid, 256, 0, as_stream(stream)>>>(
+      to_args(cfg), (const float2*)tab, p, m, v, last_step, *x, H, S, pon, pend->slot_of,
+      (const PendHdr*)pend->hdr);
+  HVAE_LAUNCH_CHECK("k_adam_catchup_csr");
+  return HVAE_OK;
+}
+
+extern "C" int hvae_adam_lazy_pending(const hvae_adam* cfg, const float* tab, float* p, float* m, float* v,
+                                      int32_t* last_step, int64_t N, int64_t H, int64_t max_rows,
+                                      const hvae_adam_pend* pend, void* stream) {
+  HVAE_REQUIRE(cfg && tab && p && m && v && last_step && pend && pend->slot_of && pend->item_of && pend->hdr &&
+                   H % 4 == 0 && N >= 0 && max_rows >= 0,
+               "hvae_adam_lazy_pending: bad args");
+  HVAE_REQUIRE(((uintptr_t)p % 16) == 0 && ((uintptr_t)m % 16) == 0 && ((uintptr_t)v % 16) == 0,
+               "hvae_adam_lazy_pending: 16-B alignment required");
+  if (N == 0) return HVAE_OK;
+  const RowMap rm = row_map(H);
+  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(std::min(max_rows, N), (int64_t)rm.rpb), 4096));
+  const int period = lazy_sweep_period(N);
+  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, period), (int64_t)rm.rpb), 4096));
+  ProbeScope probe("adam_pending", as_stream(stream));
+  k_adam_pending<<<(unsigned)(b_rows + b_sweep), 256, 0, as_stream(stream)>>>(
+      to_args(cfg), (const float2*)tab, p, m, v, last_step, pend->slot_of, pend->item_of,
+      (const PendHdr*)pend->hdr, N, H, (int)b_rows, (int)b_sweep, period, rm);
+  HVAE_LAUNCH_CHECK("k_adam_pending");
+  return HVAE_OK;
+}
+
+static int adam_lazy_launch(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
+                            int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense,
+                            int64_t dense_off, int64_t n_dense, const hvae_adam_pend* pend, void* stream);
+
 extern "C" int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
                               int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense,
                               int64_t dense_off, int64_t n_dense, void* stream) {
+  return adam_lazy_launch(cfg, tab, tab_len, p, m, v, last_step, rg, H, g_dense, dense_off, n_dense, nullptr,
+                          stream);
+}
+
+extern "C" int hvae_adam_lazy_defer(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
+                                    int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense,
+                                    int64_t dense_off, int64_t n_dense, const hvae_adam_pend* pend, void* stream) {
+  HVAE_REQUIRE(pend && pend->slot_of && pend->item_of && pend->hdr, "hvae_adam_lazy_defer: bad pend");
+  return adam_lazy_launch(cfg, tab, tab_len, p, m, v, last_step, rg, H, g_dense, dense_off, n_dense, pend, stream);
+}
+
+static int adam_lazy_launch(const hvae_adam* cfg, float* tab, int64_t tab_len, float* p, float* m, float* v,
+                            int32_t* last_step, const hvae_rowgrad* rg, int64_t H, const float* g_dense,
+                            int64_t dense_off, int64_t n_dense, const hvae_adam_pend* pend, void* stream) {
   HVAE_REQUIRE(cfg && cfg->step_dev && tab && p && m && v && last_step && rg && rg->rows && rg->item_of &&
                    rg->n_unique,
                "hvae_adam_lazy: bad args");
@@ -686,14 +844,18 @@ extern "C" int hvae_adam_lazy(const hvae_adam* cfg, float* tab, int64_t tab_len,
   HVAE_REQUIRE(rg->slot_of, "hvae_adam_lazy: rowgrad without slot_of");
   const RowMap rm = row_map(H);
   const int uu = adam_unroll();
-  const int64_t b_rows = std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, (int64_t)rm.rpb * uu), 4096));
+  // deferred: the row blocks only record the rows (one thread a row) and the sweep waits for k_adam_pending
+  const int64_t b_rows = pend ? std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, 256), 1024))
+                              : std::max<int64_t>(1, std::min<int64_t>(cdiv(rg->cap, (int64_t)rm.rpb * uu), 4096));
   const int period = lazy_sweep_period(N);
-  const int64_t b_sweep = std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, period), (int64_t)rm.rpb * uu), 4096));
+  const int64_t b_sweep =
+      pend ? 0 : std::max<int64_t>(1, std::min<int64_t>(cdiv(cdiv(N, period), (int64_t)rm.rpb * uu), 4096));
   const int64_t b_dense = std::min<int64_t>(cdiv(cdiv(n_dense, 4), 256), 512);
   ProbeScope probe("adam_rows", as_stream(stream));
   HVAE_ADAM_U_CALL(uu, (k_adam_lazy<U><<<(unsigned)(b_rows + b_sweep + b_dense), 256, 0, as_stream(stream)>>>(
       to_args(cfg), (float2*)tab, p, m, v, last_step, rg->rows, rg->slot_of, rg->item_of, rg->n_unique, N, H,
-      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep, period, rm)));
+      g_dense, dense_off, n_dense, (int)b_rows, (int)b_sweep, period, rm, pend ? pend->slot_of : nullptr,
+      pend ? pend->item_of : nullptr, pend ? (PendHdr*)pend->hdr : nullptr)));
   HVAE_LAUNCH_CHECK("k_adam_lazy");
   return HVAE_OK;
 }

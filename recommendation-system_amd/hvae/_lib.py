@@ -15,7 +15,7 @@ import torch
 _HERE = Path(__file__).resolve().parent
 LIB_PATH = Path(os.environ.get("HVAE_LIB", _HERE / "libhvae.so"))
 
-ABI_VERSION = 4  # include/hvae.h HVAE_ABI_VERSION
+ABI_VERSION = 5  # include/hvae.h HVAE_ABI_VERSION
 HVAE_OK = 0
 HVAE_F32 = 0
 HVAE_BF16 = 1
@@ -100,6 +100,10 @@ class Adam(C.Structure):
     ]
 
 
+class AdamPend(C.Structure):  # hvae_adam_pend: a deferred W1t update's record (device pointers)
+    _fields_ = [("slot_of", vp), ("item_of", vp), ("hdr", vp)]
+
+
 P = C.POINTER
 # name -> (restype, argtypes); mirrors include/hvae.h one to one.
 SIGNATURES = {
@@ -163,6 +167,10 @@ SIGNATURES = {
     "hvae_adam_lazy_catchup": (cint, [P(Adam), vp, vp, vp, vp, vp, P(RowGrad), i64, i64, vp]),
     "hvae_adam_lazy_catchup_csr": (cint, [P(Adam), vp, vp, vp, vp, vp, P(CsrBatch), i64, vp]),
     "hvae_adam_lazy_sweep_period": (cint, [i64]),
+    "hvae_adam_lazy_defer": (cint, [P(Adam), vp, i64, vp, vp, vp, vp, P(RowGrad), i64, vp, i64, i64, P(AdamPend),
+                                    vp]),
+    "hvae_adam_lazy_catchup_csr_pending": (cint, [P(Adam), vp, vp, vp, vp, vp, P(CsrBatch), i64, P(AdamPend), vp]),
+    "hvae_adam_lazy_pending": (cint, [P(Adam), vp, vp, vp, vp, vp, i64, i64, i64, P(AdamPend), vp]),
     "hvae_counter_add": (cint, [vp, i64, vp]),
     "hvae_counters_add": (cint, [vp, i64, vp, i64, vp]),
     "hvae_score_candidates": (cint, [vp, i64, vp, vp, i64, vp, i64, i64, vp, vp]),

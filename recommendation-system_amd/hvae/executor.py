@@ -287,6 +287,29 @@ class FusedTrainer:
         self.last_step = torch.zeros(lay.n_items, dtype=torch.int32, device=device)
         self.tab_len = 1 << 22
         self.adam_tab = torch.zeros(2 * self.tab_len, dtype=torch.float32, device=device)
+        # Deferred W1t update (hvae_adam_lazy_defer, HVAE_ADAM_DEFER=1): a step's update records its gradient rows
+        # as pending instead of moving them; the next step's catch-up applies it to its batch's rows before the
+        # forward reads them, and hvae_adam_lazy_pending moves the rest (and the step's sweep range) on the defer
+        # stream beside the next step, joined before that step's row-gradient apply. Bitwise the same parameters.
+        # HVAE_DEFER_AT: "sweep" (after the decoder sweep, beside the finalize and the backward) or "fwd" (forked
+        # after the catch-up, beside the forward). It pays where few of a step's rows recur in the next batch: the
+        # Syn-10M shard (N = 1 M, ~20 % recur) bf16 / fp8 -0.2..-0.4 % / -0.5..-1.2 % per step with "sweep" in 3 A/B
+        # pairs each, "fwd" +-0.2 %; at Syn-1M (N = 100 K, ~48 % recur) the catch-up takes on half the rows' updates
+        # and the rest slows the encoder beside it: 1.051 -> 1.081 ("sweep") / 1.096 ("fwd") ms; at the W = 8 union
+        # (emulated, scripts/bench_dp_emul.py) the update graph's 0.96 ms moves into the next step's whole
+        # (12.32 -> 12.30 bf16, 7.32 -> 7.29 fp8 ms): profiles/r06_defer_ab.jsonl. So HVAE_ADAM_DEFER defaults to
+        # on from 2^19 items (HVAE_ADAM_DEFER=0 / 1 forces it)
+        env_defer = os.environ.get("HVAE_ADAM_DEFER")
+        self.adam_defer = self.lazy_adam and (bool(int(env_defer)) if env_defer is not None
+                                              else lay.n_items >= (1 << 19))
+        self.defer_at = os.environ.get("HVAE_DEFER_AT", "sweep")
+        self._pend_open = False  # (host-tracked) a recorded update may still be pending on the device
+        if self.adam_defer:
+            self.pend_slot = torch.zeros(lay.n_items, dtype=torch.int32, device=device)
+            self.pend_item = torch.zeros(lay.n_items, dtype=torch.int32, device=device)
+            self.pend_hdr = torch.zeros(4, dtype=torch.int64, device=device)  # PendHdr (t = 0: nothing recorded)
+            self._pend = _lib.AdamPend(ptr(self.pend_slot), ptr(self.pend_item), ptr(self.pend_hdr))
+            self.defer_stream = torch.cuda.Stream(device)
         # A second stream for the optimizer-only work measured slower on MI355X: every cross-stream
         # edge of the captured graph costs 5-10 us, more than the short kernels it overlaps. Off by
         # default; the dependency structure stays in place for the larger configurations.
@@ -464,6 +487,8 @@ class FusedTrainer:
         key = (B, train)
         b = self._bufs.get(key)
         if b is None or (train and b.cap < cap):
+            if b is not None:
+                self._resolve_pending()  # a recorded update may still read the gradient rows of the set it replaces
             b = _StepBuffers(self, B, cap, train)
             self._bufs[key] = b
         return b
@@ -489,6 +514,8 @@ class FusedTrainer:
             self.dp.communicate_grads()
             self._launch_dp_update(bf, advance)
             return
+        if train and not self._defers(bf.B) and not torch.cuda.is_current_stream_capturing():
+            self._resolve_pending()  # this step's forward reads rows without the deferred update's catch-up
         self._launch_fwd_bwd(bf, csr, train, beta, p_drop, ext)
         if train:
             self._launch_update(bf.rg, bf, advance)
@@ -563,6 +590,33 @@ class FusedTrainer:
         # can read W1t through lazy Adam itself (rows replayed in registers), so no catch-up launch precedes it
         fused_enc = self._mlp_rows_ok(B) and len(H) == 1 and H[0] <= 512
         enc_lazy = train and not dp and self.lazy_adam and self.enc_lazy_read and fused_enc
+        # the last step's W1t update was recorded (hvae_adam_lazy_defer): the catch-up applies it to this batch's
+        # rows, hvae_adam_lazy_pending to the rest on the defer stream
+        defer = train and self._defers(B)
+        ev_defer = None
+
+        def launch_pending():
+            nonlocal ev_defer
+            ds = self.defer_stream
+            self._fork(main, ds)
+            cfg_p = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
+            check(L_.hvae_adam_lazy_pending(C.byref(cfg_p), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
+                                            ptr(self.v), ptr(self.last_step), lay.n_items, H[0],
+                                            min(lay.n_items, bf.cap), C.byref(self._pend), ds.cuda_stream),
+                  "adam_lazy_pending")
+            ev_defer = torch.cuda.Event()
+            ev_defer.record(ds)
+
+        def catchup_csr():
+            cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
+            if defer:
+                check(L_.hvae_adam_lazy_catchup_csr_pending(
+                    C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m), ptr(self.v),
+                    ptr(self.last_step), csr_ref, H[0], C.byref(self._pend), st), "adam_lazy_catchup_csr_pending")
+            else:
+                check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
+                                                    ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
+                      "adam_lazy_catchup_csr")
         if self.train_e:
             # E moved with the last step's Adam: the decoder's image of it and max||E|| follow (in the captured step)
             if isinstance(self.E_dec, ops.DecoderImage):
@@ -580,10 +634,9 @@ class FusedTrainer:
             # batch's W1t rows replay their deferred steps, found from the CSR entries, before the forward
             # reads them
             if self.lazy_adam:
-                cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
-                check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
-                                                    ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
-                      "adam_lazy_catchup_csr")
+                catchup_csr()
+            if defer and self.defer_at == "fwd":
+                launch_pending()
             ps = self.plan_stream if self.plan_stream is not None else side
             if ps is not main:
                 self._fork(main, ps)
@@ -605,10 +658,9 @@ class FusedTrainer:
                 check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), ps.cuda_stream),
                       "w1_rowgrad_plan")
             if self.lazy_adam and not enc_lazy:
-                cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
-                check(L_.hvae_adam_lazy_catchup_csr(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
-                                                    ptr(self.v), ptr(self.last_step), csr_ref, H[0], st),
-                      "adam_lazy_catchup_csr")
+                catchup_csr()
+            if defer and self.defer_at == "fwd":
+                launch_pending()
             if not early:
                 self._fork(main, ps)
                 check(L_.hvae_w1_rowgrad_plan(csr_ref, bf.rg.ref, ptr(bf.rg.ws), bf.rg.ws.numel(), ps.cuda_stream),
@@ -700,6 +752,8 @@ class FusedTrainer:
                                     ptr(bf.loss3), ptr(accum), ws, wsn, st), "decoder_train")
         if not train:
             return
+        if defer and ev_defer is None:  # HVAE_DEFER_AT=sweep: beside the finalize and the backward
+            launch_pending()
         # ----------------------------------------------------- backward ---
         G = self.G
         if self.train_e:
@@ -809,6 +863,8 @@ class FusedTrainer:
                           (B, H[k - 1], H[k], ptr(bf.da[k]), H[k], ptr(W), H[k - 1], ptr(bf.dh[k - 1]), H[k - 1]))
         if ev_plan is not None:
             main.wait_event(ev_plan)
+        if ev_defer is not None:  # the recorded update's rows are done before this step's apply rewrites its rows
+            main.wait_event(ev_defer)
         if not dp:
             if self.train_e:
                 # dE's sparse term -(1/B) sum_b x_bi u_b over the plan's item segments (the apply with u for da),
@@ -869,7 +925,13 @@ class FusedTrainer:
                                               ptr(self.step_snap), ptr(self.boff) if advance else None, advance,
                                               ws, wsn, st), "clip_grad_norm_step")
         # W1t (row-sparse gradient, offset 0 of the flat buffer) and the dense segment in one launch
-        if self.lazy_adam:
+        if self.lazy_adam and self._defers(bf.B):  # W1t's rows recorded, moved by the next step (or a flush)
+            check(L_.hvae_adam_lazy_defer(C.byref(cfg), ptr(self.adam_tab), self.tab_len, ptr(self.flat),
+                                          ptr(self.m), ptr(self.v), ptr(self.last_step), rg.ref, H[0],
+                                          ptr(self.g_small), lay.small_offset, lay.n_small, C.byref(self._pend), st),
+                  "adam_lazy_defer")
+            self._pend_open = True
+        elif self.lazy_adam:
             check(L_.hvae_adam_lazy(C.byref(cfg), ptr(self.adam_tab), self.tab_len, ptr(self.flat), ptr(self.m),
                                     ptr(self.v), ptr(self.last_step), rg.ref, H[0], ptr(self.g_small),
                                     lay.small_offset, lay.n_small, st), "adam_lazy")
@@ -885,11 +947,39 @@ class FusedTrainer:
         """
         if not self.lazy_adam:
             return
+        self._resolve_pending()
         cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
         check(lib().hvae_adam_lazy_catchup(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
                                            ptr(self.v), ptr(self.last_step), None, self.layout.n_items,
                                            self.layout.hidden[0], torch.cuda.current_stream(self.device).cuda_stream),
               "adam_lazy_flush")
+
+    def _defers(self, B: int) -> bool:
+        """Whether a train step of B users records its W1t update (hvae_adam_lazy_defer) instead of applying it:
+        the steps whose forward is preceded by the CSR catch-up and whose plan runs on its own stream (data
+        parallel, or B >= plan_side_min_batch), not the small batches whose fused encoder reads W1t through lazy
+        Adam itself."""
+        if not self.adam_defer or self.two_streams:
+            return False
+        if self.dp is not None:
+            return True
+        if self.plan_stream is None or B < self.plan_side_min_batch:
+            return False
+        H = self.layout.hidden
+        return not (self.enc_lazy_read and self._mlp_rows_ok(B) and len(H) == 1 and H[0] <= 512)
+
+    def _resolve_pending(self):
+        """Apply a recorded W1t update still pending, on the current stream (eager; a no-op on the device when
+        the next step's catch-up and hvae_adam_lazy_pending already did)."""
+        if not self._pend_open:
+            return
+        lay = self.layout
+        cfg0 = ops.adam_config(self.lr, self.betas, self.eps, self.wd, self.step_dev, None)
+        check(lib().hvae_adam_lazy_pending(C.byref(cfg0), ptr(self.adam_tab), ptr(self.flat), ptr(self.m),
+                                           ptr(self.v), ptr(self.last_step), lay.n_items, lay.hidden[0],
+                                           lay.n_items, C.byref(self._pend),
+                                           torch.cuda.current_stream(self.device).cuda_stream), "adam_lazy_pending")
+        self._pend_open = False
 
     def _hyper(self) -> tuple:
         """The optimizer constants a captured step bakes in (part of its graph key)."""
@@ -897,6 +987,7 @@ class FusedTrainer:
 
     def mark_all_current(self):
         """Every row has had every step applied (after an external dense update of W1t)."""
+        self._resolve_pending()
         self.last_step.copy_(self.step_dev.to(torch.int32).expand_as(self.last_step))
 
     def _check_steps(self, more: int):
@@ -1113,8 +1204,12 @@ class FusedTrainer:
                              weight=key[-1] if self.dp is not None and train else 1.0)
                 return 1
             self._capture(bf, data, train, beta, p_drop, key)
+        defer = train and self._defers(bf.B)
+        if train and not defer:
+            self._resolve_pending()  # the graph's forward reads rows without the recorded update's catch-up
         if bf.graph_k is not None and left >= bf.graph_k_steps:
             bf.graph_k.replay()
+            self._pend_open = self._pend_open or defer
             return bf.graph_k_steps
         if bf.graph_pre is not None:  # data parallel: the CSR packet, then its exchange
             bf.graph_pre.replay()
@@ -1123,6 +1218,7 @@ class FusedTrainer:
         if bf.graph_up is not None:  # data parallel: the gradients' exchange between the step's graphs
             self.dp.communicate_grads()
             bf.graph_up.replay()
+        self._pend_open = self._pend_open or defer
         return 1
 
     # ------------------------------------------------------ data parallel ---
@@ -1205,6 +1301,7 @@ class FusedTrainer:
                 self._launch_pack_grads(bfc, c / T)
                 sums = sums + self.accum_train.cpu().numpy() * (c / T)
             else:  # no users here: the union batch's plan still runs (and the schedule counter advances)
+                self._resolve_pending()  # (no forward here to carry it; the apply below rewrites the rows it reads)
                 dp.merge_plan()
                 self._launch_pack_grads(None, 0.0)
                 if anneal is not None:

@@ -135,7 +135,7 @@ def test_abi_exports_every_declared_symbol():
     from hvae import _lib
     assert set(_lib.SIGNATURES) == set(syms), "ctypes binding out of sync with include/hvae.h"
     L.hvae_version.restype = ctypes.c_int
-    assert L.hvae_version() == _lib.ABI_VERSION == 4
+    assert L.hvae_version() == _lib.ABI_VERSION == 5
 
 
 def test_abi_argument_errors_without_gpu():

@@ -263,6 +263,65 @@ def test_dp_global_sharding_epochs(hip_device):
     assert ra[5] is True and rb[5] is True
 
 
+def _defer_worker(rank, world, port, q):
+    """Data-parallel epochs with the deferred W1t update against the undeferred one, in one process group: the
+    union's pending rows are moved by the next step's catch-up (this rank's batch) and hvae_adam_lazy_pending (the
+    rest), and the last global batch (385 = 6 x 64 + 1: one user on rank 0, none on rank 1) resolves them eagerly
+    on the empty rank."""
+    try:
+        import sys
+        from pathlib import Path
+        root = Path(__file__).resolve().parents[1]
+        sys.path[:0] = [str(root / "recommendation-system_amd"), str(root), str(root / "tests" / "golden")]
+        import torch.distributed as dist
+        from gen import synth_csr, synth_embeddings
+        from hvae.executor import ConstBeta, FusedTrainer
+        from src.ml.model import HybridVAE
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        X = synth_csr(385, 900, seed=51)
+        E = synth_embeddings(900, 128, seed=52)
+        out = []
+        for defer in ("0", "1"):
+            os.environ["HVAE_ADAM_DEFER"] = defer
+            torch.manual_seed(0)
+            model = HybridVAE(900, E, latent_dim=64, hidden_dims=[128], dropout=0.3, beta=0.2).to(dev)
+            fused = FusedTrainer(model, dev, precision="bf16", seed=5, use_graphs=True,
+                                 process_group=dist.group.WORLD)
+            assert fused._defers(32) == (defer == "1")
+            data = fused.device_data(X, list(range(385)))
+            data.dp_global = True
+            r = [fused.run_epoch(data, 32, True, ConstBeta(0.2), 0.3) for _ in range(2)]
+            torch.cuda.synchronize()
+            out.append((r, fused.flat.cpu().numpy(), fused.m.cpu().numpy(), fused.v.cpu().numpy()))
+        (ra, fa, ma, va), (rb, fb, mb, vb) = out
+        q.put((rank, ra == rb, bool((fa == fb).all() and (ma == mb).all() and (va == vb).all())))
+        dist.barrier()
+        dist.destroy_process_group()
+    except BaseException:
+        import traceback
+        traceback.print_exc()
+        raise
+
+
+def test_dp_deferred_adam_is_bitwise(hip_device):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_defer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=600) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert all(r[1] and r[2] for r in res), res
+
+
 def test_dp_two_ranks_one_gpu(hip_device):
     world = 2
     ctx = mp.get_context("spawn")

@@ -207,6 +207,41 @@ def test_lazy_adam_is_bitwise_dense(hip_device, wd, plan_side, lazy_read, monkey
     assert torch.equal(fa, fb) and torch.equal(ma, mb) and torch.equal(sa, sb)
 
 
+@pytest.mark.parametrize("graphs", [True, False])
+@pytest.mark.parametrize("wd,at", [(0.0, "fwd"), (0.01, "fwd"), (0.0, "sweep")])
+def test_deferred_adam_is_bitwise(hip_device, wd, at, graphs, monkeypatch):
+    """The deferred W1t update (HVAE_ADAM_DEFER=1: hvae_adam_lazy_defer records a step's gradient rows, the next
+    step's CSR catch-up applies it to its batch's rows and hvae_adam_lazy_pending to the rest on the defer stream)
+    leaves losses, parameters and both moments bitwise those of the undeferred update: over graph-replayed (or
+    eager) epochs of deferring B = 32 steps, each followed by a short 2-user tail that does not defer (the pending
+    update resolved eagerly before it), an epoch at another batch size, and validation. wd != 0: the catch-up's
+    full-store branch; at = sweep: the pending rows moved beside the finalize instead of the forward."""
+    monkeypatch.setenv("HVAE_PLAN_SIDE_MIN_BATCH", "32")  # B = 32 defers, the tail of 2 does not
+    monkeypatch.setenv("HVAE_ENC_LAZY_READ", "0")
+    monkeypatch.setenv("HVAE_DEFER_AT", at)
+    from hvae.executor import ConstBeta, FusedTrainer
+    from src.ml.model import HybridVAE
+    X = synth_csr(290, 700, seed=13)
+    E = synth_embeddings(700, 128, seed=14)
+    outs = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("HVAE_ADAM_DEFER", defer)
+        torch.manual_seed(0)
+        model = HybridVAE(700, E, latent_dim=64, hidden_dims=[128], dropout=0.3, beta=0.2).to(hip_device)
+        fused = FusedTrainer(model, hip_device, weight_decay=wd, precision="bf16", seed=77, use_graphs=graphs)
+        assert fused.adam_defer == (defer == "1") and fused._defers(32) == (defer == "1") and not fused._defers(2)
+        data = fused.device_data(X, list(range(290)))
+        gen = torch.Generator().manual_seed(6)
+        r = [fused.run_epoch(data, 32, True, ConstBeta(0.2), 0.3, generator=gen) for _ in range(3)]
+        r.append(fused.run_epoch(data, 48, True, ConstBeta(0.2), 0.3, generator=gen))
+        v = fused.run_epoch(data, 32, False, ConstBeta(0.2), 0.3)
+        outs.append((r, v, fused.flat.clone(), fused.m.clone(), fused.v.clone(), int(fused.step_dev.item())))
+    (ra, va, fa, ma, sa, na), (rb, vb, fb, mb, sb, nb) = outs
+    assert na == nb
+    assert ra == rb and va == vb
+    assert torch.equal(fa, fb) and torch.equal(ma, mb) and torch.equal(sa, sb)
+
+
 def test_annealed_epoch_graph_is_bitwise_eager(hip_device):
     """AnnealedVAE (reference src/ml/model.py:295-334, stepped once per train batch, src/ml/train.py:74-76): the
     schedule evaluated on the device inside the captured step (AnnealedBeta -> hvae_anneal_beta) replays one graph
