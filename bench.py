@@ -167,8 +167,8 @@ def cpu_baseline(w: dict, X, E, seconds: float, threads: int | None = None) -> d
 
 
 # kernel families the library's probe can bracket (ProbeScope names in csrc/)
-FAMILIES = ("decoder_sweep", "decoder_finalize", "gemm", "adam_rows", "adam_catchup", "encoder_fwd", "ln_bwd",
-            "rowgrad_plan", "rowgrad_apply", "clip", "mlp_fwd", "mlp_bwd")
+FAMILIES = ("decoder_sweep", "decoder_finalize", "gemm", "adam_rows", "adam_catchup", "adam_pending", "encoder_fwd",
+            "ln_bwd", "rowgrad_plan", "rowgrad_apply", "clip", "mlp_fwd", "mlp_bwd")
 
 
 def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int, kernels: dict) -> dict:
@@ -225,7 +225,13 @@ def roofline_models(w: dict, precision: str, B: int, fused, X, users, rank: int,
         gemm_flops += 6.0 * B * w["hidden"][k] * w["hidden"][k - 1]
     put("gemm", "mfma", gemm_flops / n_gemm, PEAK_F32_TFLOPS, "TFLOP/s")
     n_small = fused.layout.n_small
-    if fused.lazy_adam:
+    if fused.lazy_adam and fused._defers(B):
+        # deferred update (hvae_adam_lazy_defer): the launch steps the dense segment and only records the gradient
+        # rows (item_of read; pend item / slot and last_step written: 16 B a row); their bytes move to the next
+        # step's catch-up and hvae_adam_lazy_pending ("adam_pending", timed in launch_us, no model: how many of the
+        # rows the catch-up takes first depends on the next batch)
+        adam_bytes = 16.0 * uniq + 28.0 * n_small
+    elif fused.lazy_adam:
         from hvae._lib import lib
         swept = -(-N // int(lib().hvae_adam_lazy_sweep_period(N)))
         adam_bytes = 24.0 * H * (uniq + swept) + 8.0 * swept + 28.0 * n_small
