@@ -31,7 +31,6 @@
 //     kernel combines the (m, l, O) partials.
 #include <algorithm>
 #include <array>
-#include <cstdlib>
 #include <type_traits>
 
 #include "hvae_common.h"
@@ -1412,169 +1411,6 @@ __global__ void __launch_bounds__(256) k_dec_finalize(FinArgs a) {
     loss_block_reduce(a.recon_rows, true, a.kl_rows, a.nb, a.beta_dev ? *a.beta_dev : a.beta, a.loss3, a.accum3);
 }
 
-// Two users per block (the large batches' common case: at most 8 split partials, or one direct split; 16-B rows;
-// D <= 512): threads [0, 128) finalise user 2 blockIdx.x, [128, 256) user 2 blockIdx.x + 1. Each half runs
-// k_dec_finalize<false, true>'s per-user arithmetic with the same lanes holding the same values (the splits in the
-// first lanes of its first wave, columns 4 t .. 4 t + 3 on thread t), so its results are that kernel's; the rare
-// exact fixup of a flagged user takes the whole block, one flagged user after the other. With one user per 256
-// threads only D / 4 threads worked past the merge, and the merge's 16 KB of split weights held a CU to 7 blocks:
-// here 16 users are in flight per CU instead of 7.
-constexpr int kFinPairMaxD = 512;
-constexpr int kFinPairMaxSplits = 8;
-__global__ void __launch_bounds__(256) k_dec_finalize_pair(FinArgs a) {
-  constexpr int EB = FIN_EB_V4;
-  __shared__ float wsh[2][kFinPairMaxSplits];
-  __shared__ __attribute__((aligned(16))) float obuf[1024];  // exact fixup's columns -> the owning half's layout
-  __shared__ float red[4];   // per-wave sums: waves 0, 1 are half 0, waves 2, 3 half 1
-  __shared__ float pbuf[256];
-  __shared__ int any_flag[2];
-  __shared__ float lse_x[2];
-  const int tid = threadIdx.x, hf = tid >> 7, t = tid & 127, lane = tid & 63, w = tid >> 6;
-  const int64_t b = 2 * (int64_t)blockIdx.x + hf;
-  const bool live = b < a.nb;
-  const int64_t D = a.D;
-  const bool act = live && 4 * t < D;
-  // half-wide sum: each wave's butterfly, then the half's two waves in order
-  auto half_sum = [&](float v) {
-    v = wave_sum(v);
-    __syncthreads();
-    if (lane == 0) red[w] = v;
-    __syncthreads();
-    return red[2 * hf] + red[2 * hf + 1];
-  };
-  int64_t sp_beg = 0, sp_end = 0;
-  int sp_j[EB];
-  float sp_x[EB];
-  if (live && a.row_ptr) {
-    const int64_t r = batch_row(a.rows, a.rows_offset, b);
-    sp_beg = a.row_ptr[r];
-    sp_end = a.row_ptr[r + 1];
-  }
-#pragma unroll
-  for (int u = 0; u < EB; ++u) {
-    const int64_t e = sp_beg + u;
-    sp_j[u] = e < sp_end ? a.col_idx[e] : 0;
-    sp_x[u] = e < sp_end ? a.vals[e] : 0.f;
-  }
-  if (tid < 2) any_flag[tid] = 0;
-  __syncthreads();
-  float lse_b = 0.f;
-  float o[4] = {0.f, 0.f, 0.f, 0.f};
-  const int nsp = a.splits;
-  if (nsp > 1) {
-    float M = -INFINITY;
-    int fl = 0;
-    if (live && t < nsp) {
-      const int64_t r = (int64_t)t * a.nb + b;
-      M = a.pm[r];
-      if (a.flag) fl = a.flag[r];
-    }
-    if (fl) any_flag[hf] = 1;
-    M = wave_max(M);
-    __syncthreads();
-    if (lane == 0) red[w] = M;
-    __syncthreads();
-    M = fmaxf(red[2 * hf], red[2 * hf + 1]);  // (max is exact in any order)
-    float L = 0.f;
-    if (live && t < nsp) {
-      const int64_t r = (int64_t)t * a.nb + b;
-      const float ms = a.pm[r];
-      const float wv = (ms == -INFINITY) ? 0.f : __expf(ms - M);
-      wsh[hf][t] = wv;
-      L += wv * a.pl[r];
-    }
-    L = half_sum(L);  // (its barriers also publish wsh and any_flag)
-    lse_b = M + logf(L);
-    const float inv = 1.0f / L;
-    if (a.pO) {
-      float4 acc4 = make_float4(0.f, 0.f, 0.f, 0.f);
-      float4 v[kFinPairMaxSplits];
-#pragma unroll
-      for (int j = 0; j < kFinPairMaxSplits; ++j)
-        v[j] = (act && j < nsp) ? ld4(a.pO + ((int64_t)j * a.nb + b) * D + 4 * t) : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int j = 0; j < kFinPairMaxSplits; ++j)
-        if (j < nsp) f4_fma(acc4, wsh[hf][j], v[j]);
-      o[0] = acc4.x * inv; o[1] = acc4.y * inv; o[2] = acc4.z * inv; o[3] = acc4.w * inv;
-    }
-  } else {
-    if (live && a.flag && a.flag[b] && t == 0) any_flag[hf] = 1;
-    if (live) lse_b = a.lse_in[b];
-    if (a.O_in && act) {
-      const float4 v = ld4(a.O_in + b * D + 4 * t);
-      o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-    }
-    __syncthreads();
-  }
-  // flagged users (rare, block-uniform): the whole block recomputes one user at a time
-  for (int u = 0; u < 2; ++u) {
-    if (!any_flag[u]) continue;
-    float ox[4];
-    const float lx = exact_user(2 * (int64_t)blockIdx.x + u, a.U, a.ldu, a.Ebf, a.N, D, ox, red, pbuf);
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (tid + 256 * k < D) obuf[tid + 256 * k] = ox[k];
-    if (tid == 0) lse_x[u] = lx;
-    __syncthreads();
-    if (hf == u) {
-      lse_b = lse_x[u];
-      if (4 * t < D) {
-        const float4 v = reinterpret_cast<const float4*>(obuf)[t];
-        o[0] = v.x; o[1] = v.y; o[2] = v.z; o[3] = v.w;
-      }
-    }
-    __syncthreads();
-  }
-  if (live && t == 0) a.lse_out[b] = lse_b;
-  if (a.O_out && act) *reinterpret_cast<float4*>(a.O_out + b * D + 4 * t) = make_float4(o[0], o[1], o[2], o[3]);
-  float dot = 0.f;
-  float n = 0.f;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (a.row_ptr) {
-    for (int64_t e0 = sp_beg; e0 < sp_end; e0 += EB) {
-      if (e0 != sp_beg) {
-#pragma unroll
-        for (int u = 0; u < EB; ++u) {
-          const int64_t e = e0 + u;
-          sp_j[u] = e < sp_end ? a.col_idx[e] : 0;
-          sp_x[u] = e < sp_end ? a.vals[e] : 0.f;
-        }
-      }
-      float ev[EB][4];
-#pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        const float4 v = (e0 + u < sp_end && act) ? ld4(a.E32 + (int64_t)sp_j[u] * D + 4 * t)
-                                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-        ev[u][0] = v.x; ev[u][1] = v.y; ev[u][2] = v.z; ev[u][3] = v.w;
-      }
-#pragma unroll
-      for (int u = 0; u < EB; ++u) {
-        if (e0 + u >= sp_end) break;
-        n += sp_x[u];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) acc[k] += sp_x[u] * ev[u][k];
-      }
-    }
-    if (act) {
-      const float4 uu = ld4(a.U + b * a.ldu + 4 * t);
-      dot = uu.x * acc[0] + uu.y * acc[1] + uu.z * acc[2] + uu.w * acc[3];
-    }
-  }
-  // (every thread reaches the reduction: the halves' batch rows have different entry counts)
-  dot = half_sum(dot);
-  if (!a.row_ptr) return;
-  if (live && a.recon_rows && t == 0) {
-    if (a.loss3) st_shared_f(&a.recon_rows[b], n * lse_b - dot);
-    else a.recon_rows[b] = n * lse_b - dot;
-  }
-  if (a.dU && act)
-    *reinterpret_cast<float4*>(a.dU + b * D + 4 * t) =
-        make_float4(a.scale * (n * o[0] - acc[0]), a.scale * (n * o[1] - acc[1]), a.scale * (n * o[2] - acc[2]),
-                    a.scale * (n * o[3] - acc[3]));
-  if (a.loss3 && last_block_arrives(a.ticket, gridDim.x))
-    loss_block_reduce(a.recon_rows, true, a.kl_rows, a.nb, a.beta_dev ? *a.beta_dev : a.beta, a.loss3, a.accum3);
-}
-
 // Exact recompute of one user flagged by k_dec_bf16 (its max score sits more
 // than kUnderflowSpan below the fixed offset: only possible for |u| in the
 // hundreds). Two passes in fp32 over the bf16 E by one 256-thread block.
@@ -2151,12 +1987,7 @@ static int decoder_finalize(FinArgs& a, const float* U, int64_t ldu, const void*
   }
   ProbeScope probe("decoder_finalize", st);
   const bool v4 = fin_v4(a);
-  // two users per block where the per-user kernel leaves most of its threads idle (HVAE_FIN_PAIR=0: one per block)
-  const char* pe = std::getenv("HVAE_FIN_PAIR");  // (read at every launch: a test switches it)
-  const bool pair_on = !(pe && std::atoi(pe) == 0);
-  if (pair_on && !grouped && v4 && D <= kFinPairMaxD && a.splits <= kFinPairMaxSplits && !a.v6_upb) {
-    k_dec_finalize_pair<<<(unsigned)cdiv(nb, 2), 256, 0, st>>>(a);
-  } else if (grouped) {
+  if (grouped) {
     if (v4) k_dec_finalize<true, true><<<(unsigned)nb, 256, 0, st>>>(a);
     else k_dec_finalize<true, false><<<(unsigned)nb, 256, 0, st>>>(a);
   } else {

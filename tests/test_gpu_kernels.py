@@ -296,35 +296,6 @@ def test_decoder_large_norm_fixup(ops, hip_device, D, reps):
     assert torch.equal(dU_n, dU_t)
 
 
-@pytest.mark.parametrize("nb,N,D,big", [(1001, 5000, 384, False), (513, 4000, 256, False), (301, 2400, 128, False),
-                                        (300, 2400, 384, True), (257, 2000, 128, True), (4096, 12000, 384, False)])
-def test_decoder_finalize_pair_equals_single(ops, hip_device, monkeypatch, nb, N, D, big):
-    """The two-users-per-block finalize (k_dec_finalize_pair, D <= 512, <= 8 splits) gives k_dec_finalize's lse, O,
-    recon rows, dU and fused loss bit for bit (HVAE_FIN_PAIR=0 runs the one-user kernel): odd user counts, one and
-    several splits, and users with |u| in the hundreds whose flagged exact fixup takes the whole block."""
-    X = synth_csr(nb, N, lam=5.0, seed=nb + 3)
-    E = torch.as_tensor(synth_embeddings(N, D, seed=7))
-    g = torch.Generator().manual_seed(nb)
-    U = torch.randn(nb, D, generator=g) * 2
-    if big:
-        U[::3] = U[::3] / U[::3].norm(dim=1, keepdim=True) * 800.0
-    xd = ops.csr_from_scipy(X, hip_device)
-    Ed, Ud = E.to(hip_device), U.to(hip_device)
-    Ek = ops.decoder_image(Ed)
-    enorm = ops.row_norm_max(Ek)
-    kl = torch.rand(nb, generator=g).to(hip_device)
-    outs = []
-    for pair in ("0", "1"):
-        monkeypatch.setenv("HVAE_FIN_PAIR", pair)
-        loss3 = torch.empty(3, device=hip_device)
-        acc3 = torch.zeros(3, dtype=torch.float64, device=hip_device)
-        lse, O, rr, dU = ops.decoder_train(xd, Ud, Ek, enorm, Ed, 1.0 / nb, want_o=True, kl_rows=kl, beta=0.2,
-                                           loss3=loss3, accum3=acc3)
-        outs.append((lse, O, rr, dU, loss3, acc3))
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
-
-
 def test_decoder_bwd_sparse(ops, hip_device):
     X = synth_csr(40, 700, lam=5.0, seed=4)
     x = torch.as_tensor(X.toarray(), dtype=torch.float32)
