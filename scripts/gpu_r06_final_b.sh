@@ -6,6 +6,8 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${OUT:-r06_final}
 mkdir -p $O
 cd $R
+# the A/B library rebuilt from the end tree's sources (part A's suite ran a stale one)
+timeout -k 10 600 python -u -m pytest tests/test_gpu_ab_variant.py -m gpu -q --timeout 500 --timeout-method thread > $O/pytest_ab.log 2>&1 || exit 10
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit 1
 timeout -k 10 420 python -u bench.py > $O/bench_syn10m.json 2> $O/bench_syn10m.log || exit 2
 cd /tmp && export TMPDIR=/tmp
