@@ -959,7 +959,7 @@ class FusedTrainer:
         the steps whose forward is preceded by the CSR catch-up and whose plan runs on its own stream (data
         parallel, or B >= plan_side_min_batch), not the small batches whose fused encoder reads W1t through lazy
         Adam itself."""
-        if not self.adam_defer or self.two_streams:
+        if not (self.adam_defer and self.lazy_adam) or self.two_streams:  # (lazy_adam may be switched off later)
             return False
         if self.dp is not None:
             return True
